@@ -1,0 +1,149 @@
+#!/usr/bin/env python3
+"""Headline benchmark: allreduce bus bandwidth + p50 latency, 1 GB float[] (BASELINE.json).
+
+``python bench.py --gpus N --steps K --warmup W`` — for N>1 the driver launches one rank
+per GPU with ``torch.distributed.run``.  Every step is ONE public-API call
+
+    comm.allreduceArray(buf, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
+
+on a 1e9-byte float32 array (250,000,000 elements, synthetic random data) resident on the
+rank's MI355X, i.e. the reference's ``ProcessCommSlave.allreduceArray`` on the BASELINE
+config.  Timing: W untimed warmup calls, barrier + device sync, K timed calls with a
+hipEvent pair around each (p50 / p99), barrier + sync; MAX over ranks.
+
+busbw follows the nccl-tests convention used in BASELINE.md: algbw = bytes / t,
+busbw = algbw * 2(p-1)/p.  ``value`` is the whole-job aggregate ``N * busbw``.
+With one rank nothing crosses a link (factor 2(p-1)/p = 0) and the in-place call is a
+no-op by the reference's contract, so N=1 times the OUT-OF-PLACE form of the same call
+(``out=``; a 1 GB device copy) and reports busbw := algbw for it.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# reference busbw (MB/s) for ~1 GB allreduce, BASELINE.md section D (mean of 1e8 and 5e8 rows)
+REF_BUSBW_MBPS = {2: 85.2, 4: 92.1, 6: 86.8, 8: 88.0}
+METRIC = "allreduce bus bandwidth (GB/s) + p50 latency, 1 GB float[], 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--bytes", type=int, default=1_000_000_000)
+    ap.add_argument("--algo", default=None, help="force device algorithm: rccl | a2a")
+    ap.add_argument("--codec", default=None, help="wire codec for the fp8-compressed config: fp8")
+    args = ap.parse_args()
+    if args.algo:
+        os.environ["MP4X_DEVICE_ALGO"] = args.algo
+
+    import torch
+    import torch.distributed as dist
+    from mp4x import Operands, Operators
+    from mp4x.launch import init_from_env
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    comm = init_from_env(heartbeat=False)
+    p = comm.getSlaveNum()
+    n = args.bytes // 4
+    operand = Operands.FLOAT_OPERAND(codec=args.codec)
+    op = Operators.Float.SUM
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    buf = torch.randn(n, device=dev, dtype=torch.float32, generator=g)
+    out = torch.empty_like(buf) if p == 1 else None
+
+    def step():
+        if p == 1:
+            comm.allreduceArray(buf, operand, op, 0, n, out=out)
+        else:
+            comm.allreduceArray(buf, operand, op, 0, n)
+
+    def sync_all():
+        torch.cuda.synchronize()
+        if p > 1:
+            comm.device.barrier()
+            torch.cuda.synchronize()
+
+    if p > 1:
+        comm.device  # bring up the RCCL communicator before timing
+    for _ in range(args.warmup):
+        step()
+    sync_all()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        starts[i].record()
+        step()
+        ends[i].record()
+    torch.cuda.synchronize()
+    if p > 1:
+        comm.device.barrier()
+        torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    lat = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))   # ms
+
+    # MAX over ranks
+    vals = torch.tensor([wall, lat[len(lat) // 2], lat[min(len(lat) - 1, int(0.99 * len(lat)))]],
+                        dtype=torch.float64, device=dev)
+    if p > 1:
+        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+    wall, p50, p99 = vals.tolist()
+
+    ms_per_step = wall * 1e3 / args.steps
+    nbytes = n * 4
+    algbw = nbytes / (ms_per_step * 1e-3) / 1e9
+    factor = 2.0 * (p - 1) / p if p > 1 else 1.0
+    busbw = algbw * factor
+    ref = REF_BUSBW_MBPS.get(p)
+    algo = "copy" if p == 1 else comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand)
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(busbw * p, 3),
+            "unit": "GB/s",
+            "n_gpus": p,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(busbw / (ref / 1e3), 2) if ref else None,
+            "dtype": "fp32",
+            "data": "synthetic (torch.randn per rank)",
+            "config": {"model": "allreduceArray float[250000000] (1e9 bytes), Operators.Float.SUM",
+                       "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
+                       "payload_bytes": nbytes, "algo": algo,
+                       "in_place": p > 1},
+            "busbw_gbps_per_rank": round(busbw, 3),
+            "algbw_gbps": round(algbw, 3),
+            "p50_ms": round(p50, 4),
+            "p99_ms": round(p99, 4),
+            "busbw_factor": factor,
+            "note": ("p=1: nothing crosses a link; busbw := algbw of the out-of-place single-rank allreduce"
+                     if p == 1 else "busbw = algbw * 2(p-1)/p; value = p * busbw"),
+        }
+        print(json.dumps(rec), flush=True)
+    comm.close(0)
+    if p > 1 and dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

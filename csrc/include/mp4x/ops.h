@@ -1,0 +1,97 @@
+// mp4x native C API (CDNA4 / gfx950).
+//
+// One C ABI shared by every kernel translation unit and called from Python via
+// ctypes (mp4x/ops/native.py).  All entry points are stream-ordered (no host
+// synchronisation, no allocation) so they can be captured in hipGraphs.
+// Return value: 0 on success, otherwise a hipError_t / MP4X_E* code.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+// Element types — keep in sync with mp4x/operators.py DType.
+enum mp4x_dtype {
+  MP4X_F64 = 0, MP4X_F32 = 1, MP4X_I64 = 2, MP4X_I32 = 3, MP4X_I16 = 4, MP4X_I8 = 5,
+  MP4X_BF16 = 6, MP4X_F16 = 7, MP4X_U8 = 8,
+};
+
+// Reduction operators — keep in sync with mp4x/operators.py OpCode.
+// Reference table: /root/reference/src/main/java/com/fenbi/mp4j/operator/Operators.java:29-353
+enum mp4x_op {
+  MP4X_SUM = 0, MP4X_MAX = 1, MP4X_MIN = 2, MP4X_PROD = 3,
+  MP4X_BAND = 4, MP4X_BOR = 5, MP4X_BXOR = 6,
+  MP4X_FMAXLOC = 7, MP4X_FMINLOC = 8,   // f64 word: f32 value in hi 32 bits, int32 loc in lo 32 bits
+  MP4X_IMAXLOC = 9, MP4X_IMINLOC = 10,  // i64 word: i32 value in hi 32 bits, int32 loc in lo 32 bits
+};
+
+enum { MP4X_E_BADARG = 1001, MP4X_E_UNSUPPORTED = 1002 };
+
+#define MP4X_MAX_NIN 8
+
+// ---------------------------------------------------------------- K1 / K1b / K2
+// out[i] = op(...op(op(in[0][i], in[1][i]), in[2][i])..., in[nin-1][i])  for i < n.
+// `out` may alias in[0] (the usual in-place accumulate).  nin in [1, MP4X_MAX_NIN]
+// per launch; larger fan-in is chained by the caller.  16-bit floats accumulate in f32
+// across the whole fan-in and round once.
+int mp4x_reduce(int dtype, int op, void* out, const void* const* ins, int nin, int64_t n, void* stream);
+
+// Same, but every input is the same buffer at a different element offset:
+// in[k] = base + k * stride_elems.  Used after an all-to-all (p received chunks laid
+// out contiguously) without building a pointer array.
+int mp4x_reduce_strided(int dtype, int op, void* out, const void* base, int64_t stride_elems, int nin,
+                        int64_t n, void* stream);
+
+// out[i] = in[i] * scale (f32 / f64 / bf16 / f16), e.g. gradient averaging after a SUM.
+int mp4x_scale(int dtype, void* out, const void* in, double scale, int64_t n, void* stream);
+
+// ---------------------------------------------------------------- K3 segment copy
+// Copy nseg byte segments in ONE launch: dst + dst_off[s] <- src + src_off[s], len[s] bytes.
+// The three int64 tables live in DEVICE memory (3 * nseg entries: dst_off | src_off | len).
+int mp4x_segment_copy(void* dst, const void* src, const int64_t* dev_table, int nseg, int64_t max_len,
+                      void* stream);
+
+// Row gather: out[i, :] = in[idx[i], :] for rows of `row_bytes` bytes.
+int mp4x_gather_rows(void* out, const void* in, const int64_t* idx, int64_t nrows, int64_t row_bytes,
+                     void* stream);
+
+// ---------------------------------------------------------------- K6 codec (fp8 e4m3, OCP)
+// Block-scaled quantisation: scale[b] = amax(block b) / 448, q = fp8(x / scale).
+// block must be 256 (one wave, 4 elements per lane).  n must be a multiple of 4.
+int mp4x_quant_fp8(int dtype_in, const void* in, int64_t n, uint8_t* q, float* scales, void* stream);
+// out = dequant(q[0]) + ... + dequant(q[nin-1])  (f32 accumulate), optionally + out (accumulate=1).
+// If q_out != NULL the f32 result is also re-quantised into (q_out, s_out).
+int mp4x_dequant_reduce_fp8(int dtype_out, void* out, const uint8_t* const* qs, const float* const* scales,
+                            int nin, int64_t n, int accumulate, uint8_t* q_out, float* s_out, void* stream);
+int mp4x_dequant_fp8(int dtype_out, void* out, const uint8_t* q, const float* scales, int64_t n, void* stream);
+
+// ---------------------------------------------------------------- K4 / K5 / K7 sparse
+// Owner of each key: dest[i] = (uint64)key[i] % p.  hist[p] += counts (hist zeroed by caller).
+int mp4x_key_owner(const int64_t* keys, int64_t n, int p, int32_t* dest, int32_t* hist, void* stream);
+// Stable radix sort of (key, idx) pairs on bits [begin_bit, end_bit).
+size_t mp4x_sort_pairs_temp_bytes(int64_t n, int key_is_i32);
+int mp4x_sort_pairs_i64(const int64_t* keys_in, int64_t* keys_out, const int64_t* idx_in, int64_t* idx_out,
+                        int64_t n, int begin_bit, int end_bit, void* temp, size_t temp_bytes, void* stream);
+int mp4x_sort_pairs_i32key(const int32_t* keys_in, int32_t* keys_out, const int64_t* idx_in, int64_t* idx_out,
+                           int64_t n, int begin_bit, int end_bit, void* temp, size_t temp_bytes, void* stream);
+// Run-length encode a SORTED key array: starts[u] = first index of run u, *nruns (device int64).
+size_t mp4x_rle_temp_bytes(int64_t n);
+int mp4x_run_starts(const int64_t* sorted_keys, int64_t n, int64_t* starts, int64_t* nruns_dev,
+                    int32_t* flags_scratch, void* temp, size_t temp_bytes, void* stream);
+// Reduce-by-key over runs: for run u (rows perm[starts[u] .. starts[u+1])), out_vals[u, :] =
+// op over those rows of `vals` (row length dim, dtype), in run order; out_keys[u] = key;
+// out_count[u] = run length.  nruns is read from device memory.
+int mp4x_segment_reduce_rows(int dtype, int op, const int64_t* sorted_keys, const int64_t* perm,
+                             const int64_t* starts, const int64_t* nruns_dev, int64_t n, int64_t max_runs,
+                             const void* vals, int64_t dim, int64_t* out_keys, void* out_vals, int32_t* out_count,
+                             void* stream);
+
+// ---------------------------------------------------------------- info
+const char* mp4x_version(void);
+int mp4x_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,248 @@
+"""torch-facing wrappers of the native CDNA4 kernels.
+
+Every wrapper validates shapes, dtypes, devices and contiguity on the host BEFORE the
+launch (a bad pointer on a GPU is a machine-wide fault, not an exception) and launches on
+the current torch stream.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from ..operators import DType, OpCode, dtype_of_torch
+from . import native
+from .native import check, ptr_array, stream_ptr
+
+QBLOCK = 256
+
+
+def _dev_check(*ts):
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise ValueError("device op needs GPU tensors")
+        if not t.is_contiguous():
+            raise ValueError("device op needs contiguous tensors")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError("all tensors must be on one device")
+
+
+def reduce_(out: torch.Tensor, inputs: Sequence[torch.Tensor], op: int, dtype: Optional[DType] = None,
+            stream=None) -> torch.Tensor:
+    """out = op(inputs[0], inputs[1], ...) elementwise, in input order (out may alias inputs[0])."""
+    if not inputs:
+        raise ValueError("no inputs")
+    _dev_check(out, *inputs)
+    n = out.numel()
+    for t in inputs:
+        if t.numel() != n or t.dtype != out.dtype:
+            raise ValueError(f"reduce_: shape/dtype mismatch {t.shape}/{t.dtype} vs {out.shape}/{out.dtype}")
+    dt = dtype if dtype is not None else dtype_of_torch(out.dtype)
+    pp, keep = ptr_array([t.data_ptr() for t in inputs])
+    check(native.hip().mp4x_reduce(int(dt), int(op), out.data_ptr(), pp, len(inputs), n, stream_ptr(stream)),
+          "mp4x_reduce")
+    return out
+
+
+def reduce_strided_(out: torch.Tensor, base: torch.Tensor, nin: int, op: int, stream=None) -> torch.Tensor:
+    """out = op over nin equal chunks of ``base`` (laid out back to back, each out.numel() long)."""
+    _dev_check(out, base)
+    n = out.numel()
+    if base.numel() < n * nin or base.dtype != out.dtype:
+        raise ValueError("reduce_strided_: base too small or dtype mismatch")
+    dt = dtype_of_torch(out.dtype)
+    check(native.hip().mp4x_reduce_strided(int(dt), int(op), out.data_ptr(), base.data_ptr(), n, nin, n,
+                                           stream_ptr(stream)), "mp4x_reduce_strided")
+    return out
+
+
+def scale_(out: torch.Tensor, inp: torch.Tensor, s: float, stream=None) -> torch.Tensor:
+    _dev_check(out, inp)
+    if out.numel() != inp.numel() or out.dtype != inp.dtype:
+        raise ValueError("scale_: mismatch")
+    check(native.hip().mp4x_scale(int(dtype_of_torch(out.dtype)), out.data_ptr(), inp.data_ptr(), float(s),
+                                  out.numel(), stream_ptr(stream)), "mp4x_scale")
+    return out
+
+
+def segment_copy_(dst: torch.Tensor, src: torch.Tensor, segs: Sequence[Tuple[int, int, int]], stream=None):
+    """segs = [(dst_elem_off, src_elem_off, nelems)] copied in one launch."""
+    _dev_check(dst, src)
+    if not segs:
+        return dst
+    es = dst.element_size()
+    if src.element_size() != es:
+        raise ValueError("segment_copy_: element size mismatch")
+    dn, sn = dst.numel(), src.numel()
+    for d, s, l in segs:
+        if d < 0 or s < 0 or l < 0 or d + l > dn or s + l > sn:
+            raise ValueError(f"segment_copy_: segment {(d, s, l)} out of bounds ({dn}, {sn})")
+    segs = [x for x in segs if x[2] > 0]
+    if not segs:
+        return dst
+    table = torch.tensor([d * es for d, _, _ in segs] + [s * es for _, s, _ in segs] + [l * es for _, _, l in segs],
+                         dtype=torch.int64).pin_memory().to(dst.device, non_blocking=True)
+    max_len = max(l for _, _, l in segs) * es
+    check(native.hip().mp4x_segment_copy(dst.data_ptr(), src.data_ptr(), table.data_ptr(), len(segs), max_len,
+                                         stream_ptr(stream)), "mp4x_segment_copy")
+    # `table` may be freed right away: the caching allocator only reuses it in stream order
+    return dst
+
+
+def gather_rows(inp: torch.Tensor, idx: torch.Tensor, out: Optional[torch.Tensor] = None, stream=None):
+    """out[i] = inp[idx[i]] for a 2-D (rows, ...) tensor."""
+    _dev_check(inp, idx)
+    if idx.dtype != torch.int64:
+        raise ValueError("gather_rows: idx must be int64")
+    rows = inp.shape[0]
+    row_bytes = inp[0].numel() * inp.element_size() if rows else 0
+    if out is None:
+        out = torch.empty((idx.numel(),) + tuple(inp.shape[1:]), dtype=inp.dtype, device=inp.device)
+    _dev_check(out)
+    check(native.hip().mp4x_gather_rows(out.data_ptr(), inp.data_ptr(), idx.data_ptr(), idx.numel(), row_bytes,
+                                        stream_ptr(stream)), "mp4x_gather_rows")
+    return out
+
+
+# ------------------------------------------------------------------ fp8 codec (K6)
+def quant_fp8(x: torch.Tensor, q: Optional[torch.Tensor] = None, scales: Optional[torch.Tensor] = None,
+              stream=None):
+    """Block-scaled e4m3 quantisation (256 elements / scale). Returns (q uint8[n], scales f32[nblk])."""
+    _dev_check(x)
+    n = x.numel()
+    if n % 4:
+        raise ValueError("quant_fp8: n must be a multiple of 4")
+    nblk = (n + QBLOCK - 1) // QBLOCK
+    if q is None:
+        q = torch.empty(n, dtype=torch.uint8, device=x.device)
+    if scales is None:
+        scales = torch.empty(nblk, dtype=torch.float32, device=x.device)
+    if q.numel() < n or scales.numel() < nblk:
+        raise ValueError("quant_fp8: output too small")
+    check(native.hip().mp4x_quant_fp8(int(dtype_of_torch(x.dtype)), x.data_ptr(), n, q.data_ptr(), scales.data_ptr(),
+                                      stream_ptr(stream)), "mp4x_quant_fp8")
+    return q, scales
+
+
+def dequant_reduce_fp8(out: Optional[torch.Tensor], qs: Sequence[torch.Tensor], ss: Sequence[torch.Tensor], n: int,
+                       accumulate: bool = False, q_out: Optional[torch.Tensor] = None,
+                       s_out: Optional[torch.Tensor] = None, out_dtype=None, stream=None):
+    nblk = (n + QBLOCK - 1) // QBLOCK
+    for q, s in zip(qs, ss):
+        _dev_check(q, s)
+        if q.numel() < n or s.numel() < nblk:
+            raise ValueError("dequant_reduce_fp8: input too small")
+    if out is not None:
+        _dev_check(out)
+        if out.numel() < n:
+            raise ValueError("dequant_reduce_fp8: out too small")
+        dt = dtype_of_torch(out.dtype)
+    else:
+        dt = dtype_of_torch(out_dtype or torch.float32)
+    if q_out is not None and (q_out.numel() < n or s_out is None or s_out.numel() < nblk):
+        raise ValueError("dequant_reduce_fp8: requant outputs too small")
+    lib = native.hip()
+    done = 0
+    first = True
+    while done < len(qs):
+        k = min(8, len(qs) - done)
+        qp, k1 = ptr_array([t.data_ptr() for t in qs[done:done + k]])
+        sp, k2 = ptr_array([t.data_ptr() for t in ss[done:done + k]])
+        last = done + k == len(qs)
+        check(lib.mp4x_dequant_reduce_fp8(int(dt), out.data_ptr() if out is not None else None, qp, sp, k, n,
+                                          int(accumulate or not first),
+                                          q_out.data_ptr() if (q_out is not None and last) else None,
+                                          s_out.data_ptr() if (s_out is not None and last) else None,
+                                          stream_ptr(stream)), "mp4x_dequant_reduce_fp8")
+        done += k
+        first = False
+    return out
+
+
+def dequant_fp8(q: torch.Tensor, scales: torch.Tensor, n: int, out: torch.Tensor, stream=None):
+    return dequant_reduce_fp8(out, [q], [scales], n, stream=stream)
+
+
+# ------------------------------------------------------------------ sparse (K4/K5/K7)
+def key_owner(keys: torch.Tensor, p: int, stream=None):
+    _dev_check(keys)
+    n = keys.numel()
+    dest = torch.empty(n, dtype=torch.int32, device=keys.device)
+    hist = torch.zeros(p, dtype=torch.int32, device=keys.device)
+    check(native.hip().mp4x_key_owner(keys.data_ptr(), n, p, dest.data_ptr(), hist.data_ptr(), stream_ptr(stream)),
+          "mp4x_key_owner")
+    return dest, hist
+
+
+def sort_pairs(keys: torch.Tensor, idx: Optional[torch.Tensor] = None, end_bit: Optional[int] = None, stream=None):
+    """Stable radix sort of int64 (or int32) keys with an int64 payload (default arange)."""
+    _dev_check(keys)
+    n = keys.numel()
+    if idx is None:
+        idx = torch.arange(n, dtype=torch.int64, device=keys.device)
+    ko = torch.empty_like(keys)
+    io = torch.empty_like(idx)
+    lib = native.hip()
+    is32 = keys.dtype == torch.int32
+    tb = lib.mp4x_sort_pairs_temp_bytes(n, int(is32))
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
+    eb = end_bit if end_bit is not None else (32 if is32 else 64)
+    fn = lib.mp4x_sort_pairs_i32key if is32 else lib.mp4x_sort_pairs_i64
+    check(fn(keys.data_ptr(), ko.data_ptr(), idx.data_ptr(), io.data_ptr(), n, 0, eb, temp.data_ptr(), tb,
+             stream_ptr(stream)), "mp4x_sort_pairs")
+    return ko, io
+
+
+def run_starts(sorted_keys: torch.Tensor, stream=None):
+    """Start index of every run of equal keys; returns (starts[n] buffer, nruns device scalar)."""
+    _dev_check(sorted_keys)
+    n = sorted_keys.numel()
+    dev = sorted_keys.device
+    starts = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    nruns = torch.zeros(1, dtype=torch.int64, device=dev)
+    flags = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    lib = native.hip()
+    tb = lib.mp4x_rle_temp_bytes(max(n, 1))
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+    check(lib.mp4x_run_starts(sorted_keys.data_ptr(), n, starts.data_ptr(), nruns.data_ptr(), flags.data_ptr(),
+                              temp.data_ptr(), tb, stream_ptr(stream)), "mp4x_run_starts")
+    return starts, nruns
+
+
+def reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op: int, stream=None):
+    """Deterministic reduce-by-key: returns (unique_keys, reduced_vals, counts), keys ascending.
+
+    Rows with equal keys are combined in their input order (stable sort), so inputs laid out
+    rank after rank reduce in rank order.
+    """
+    _dev_check(keys, vals)
+    n = keys.numel()
+    dev = keys.device
+    if n == 0:
+        d = vals.shape[1] if vals is not None and vals.dim() == 2 else 1
+        ev = None if vals is None else torch.empty((0, d) if vals.dim() == 2 else (0,), dtype=vals.dtype, device=dev)
+        return keys.new_empty(0), ev, torch.empty(0, dtype=torch.int32, device=dev)
+    sk, perm = sort_pairs(keys, stream=stream)
+    starts, nruns = run_starts(sk, stream=stream)
+    dim = 1 if vals is None or vals.dim() == 1 else int(vals[0].numel())
+    out_keys = torch.empty(n, dtype=torch.int64, device=dev)
+    out_count = torch.empty(n, dtype=torch.int32, device=dev)
+    out_vals = None
+    if vals is not None:
+        if vals.shape[0] != n:
+            raise ValueError("reduce_by_key: vals rows != keys")
+        out_vals = torch.empty((n,) + tuple(vals.shape[1:]), dtype=vals.dtype, device=dev)
+    dt = dtype_of_torch(vals.dtype) if vals is not None else DType.F32
+    check(native.hip().mp4x_segment_reduce_rows(int(dt), int(op), sk.data_ptr(), perm.data_ptr(), starts.data_ptr(),
+                                                nruns.data_ptr(), n, n,
+                                                vals.data_ptr() if vals is not None else None, dim,
+                                                out_keys.data_ptr(),
+                                                out_vals.data_ptr() if out_vals is not None else None,
+                                                out_count.data_ptr(), stream_ptr(stream)), "mp4x_segment_reduce_rows")
+    m = int(nruns.item())
+    return out_keys[:m], (out_vals[:m] if out_vals is not None else None), out_count[:m]

@@ -1,0 +1,134 @@
+"""ctypes binding of the in-tree native libraries (``mp4x/_native``).
+
+``libmp4x_hip.so`` holds the hand-written CDNA4 kernels (csrc/kernels) and the device
+runtime (csrc/runtime).  It links against the libamdhip64 that PyTorch-ROCm ships, and
+torch is imported before it is loaded, so both share ONE HIP runtime: torch stream
+handles and device pointers are passed straight through.
+
+On a GPU box a missing/unloadable library is an error (``NativeUnavailable``), never a
+silent fallback: every device collective that needs a kernel goes through here.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional, Sequence
+
+from ..exceptions import NativeError, Mp4jException
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+NATIVE_DIR = os.path.join(os.path.dirname(_HERE), "_native")
+HIP_LIB = os.path.join(NATIVE_DIR, "libmp4x_hip.so")
+HOST_LIB = os.path.join(NATIVE_DIR, "libmp4x_host.so")
+
+c_void_p, c_int, c_int64, c_double, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t
+PP = ctypes.POINTER(ctypes.c_void_p)
+
+
+class NativeUnavailable(Mp4jException):
+    pass
+
+
+_lock = threading.Lock()
+_hip = None
+_host = None
+
+_HIP_SIGS = {
+    "mp4x_reduce": (c_int, [c_int, c_int, c_void_p, PP, c_int, c_int64, c_void_p]),
+    "mp4x_reduce_strided": (c_int, [c_int, c_int, c_void_p, c_void_p, c_int64, c_int, c_int64, c_void_p]),
+    "mp4x_scale": (c_int, [c_int, c_void_p, c_void_p, c_double, c_int64, c_void_p]),
+    "mp4x_segment_copy": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p]),
+    "mp4x_gather_rows": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, c_void_p]),
+    "mp4x_quant_fp8": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mp4x_dequant_reduce_fp8": (c_int, [c_int, c_void_p, PP, PP, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "mp4x_dequant_fp8": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "mp4x_key_owner": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
+    "mp4x_sort_pairs_temp_bytes": (c_size_t, [c_int64, c_int]),
+    "mp4x_sort_pairs_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "mp4x_sort_pairs_i32key": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "mp4x_rle_temp_bytes": (c_size_t, [c_int64]),
+    "mp4x_run_starts": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mp4x_segment_reduce_rows": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
+                                         c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mp4x_version": (ctypes.c_char_p, []),
+    "mp4x_device_count": (c_int, []),
+}
+
+_OPTIONAL = set()
+
+
+def _bind(lib, sigs):
+    for name, (res, args) in sigs.items():
+        try:
+            f = getattr(lib, name)
+        except AttributeError:
+            if name in _OPTIONAL:
+                continue
+            raise
+        f.restype = res
+        f.argtypes = args
+
+
+def register_signatures(sigs: dict, optional: bool = False) -> None:
+    """Extra modules (device runtime) add their C signatures here before first load."""
+    _HIP_SIGS.update(sigs)
+    if optional:
+        _OPTIONAL.update(sigs.keys())
+    if _hip is not None:
+        _bind(_hip, sigs)
+
+
+def hip():
+    """Load libmp4x_hip.so (after torch, to share its HIP runtime)."""
+    global _hip
+    if _hip is not None:
+        return _hip
+    with _lock:
+        if _hip is None:
+            import torch  # noqa: F401  -- must be loaded first (shared libamdhip64)
+            if not os.path.exists(HIP_LIB):
+                raise NativeUnavailable(f"{HIP_LIB} not built: run `python tools/build_native.py`")
+            lib = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_GLOBAL)
+            _bind(lib, _HIP_SIGS)
+            _hip = lib
+    return _hip
+
+
+def host():
+    global _host
+    if _host is not None:
+        return _host
+    with _lock:
+        if _host is None:
+            if not os.path.exists(HOST_LIB):
+                raise NativeUnavailable(f"{HOST_LIB} not built: run `python tools/build_native.py`")
+            _host = ctypes.CDLL(HOST_LIB)
+            from .host_sigs import HOST_SIGS
+            _bind(_host, HOST_SIGS)
+    return _host
+
+
+def available() -> bool:
+    try:
+        hip()
+        return True
+    except Exception:
+        return False
+
+
+def check(rc: int, where: str) -> None:
+    if rc != 0:
+        msgs = {1001: "bad argument", 1002: "unsupported dtype/op"}
+        raise NativeError(where, rc, msgs.get(rc, "hip error"))
+
+
+def ptr_array(ptrs: Sequence[int]):
+    arr = (c_void_p * len(ptrs))(*ptrs)
+    return ctypes.cast(arr, PP), arr
+
+
+def stream_ptr(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)

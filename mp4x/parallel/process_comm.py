@@ -1,0 +1,617 @@
+"""ProcessComm — one communicator per process (one process per GPU on MI355X).
+
+Public API = the reference's ``ProcessCommSlave``
+(/root/reference/src/main/java/com/fenbi/mp4j/comm/ProcessCommSlave.java), same
+method names and argument order, plus snake_case aliases.  Shared semantics
+(SURVEY §2.2):
+
+* array collectives work IN PLACE on ``[from, to)`` ranges and return the same
+  buffer; non-root results of gather/reduce are unspecified;
+* ``slaveNum == 1`` returns the input unchanged;
+* ranges are validated like ``CommUtils`` and raise :class:`Mp4jException`.
+
+Data placement decides the engine:
+
+* ``torch.Tensor`` on a GPU → :class:`~mp4x.parallel.device_engine.DeviceEngine`
+  (RCCL over xGMI + the hand-written HIP kernels in ``csrc/``);
+* numpy arrays / CPU tensors / Python lists (String / Object operands) /
+  dicts → :class:`~mp4x.parallel.host_engine.HostEngine` over the TCP mesh.
+
+Lifecycle (bootstrap, heartbeat, close/exception protocol, remote logs) follows
+ProcessCommSlave.java:143-387.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+import threading
+import time
+import traceback
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ..control.client import MasterClient
+from ..control.protocol import local_ip
+from ..exceptions import Mp4jException, RangeError
+from ..operands import Operand, Operands, Serializer, DEFAULT_SERIALIZER
+from ..operators import CustomOperator, DType, Operator, dtype_of_numpy
+from ..utils.commutils import CommUtils
+from ..utils.hashing import owner_of
+from .host_engine import HostEngine
+from .transport import HostTransport
+from . import wire
+
+LOG = logging.getLogger("mp4x.comm")
+
+HEARTBEAT_DELAY = float(os.environ.get("MP4X_HEARTBEAT_DELAY", 5.0))
+HEARTBEAT_PERIOD = float(os.environ.get("MP4X_HEARTBEAT_PERIOD", 15.0))
+HEARTBEAT_MAX_FAIL = int(os.environ.get("MP4X_HEARTBEAT_MAX_FAIL", 4))
+BCAST_TREE_BYTES = int(os.environ.get("MP4X_BCAST_TREE_BYTES", 1 << 16))
+
+
+def _is_device_tensor(x) -> bool:
+    t = type(x)
+    if t.__module__.startswith("torch") and t.__name__ in ("Tensor", "Parameter"):
+        return bool(x.is_cuda)
+    return False
+
+
+def _is_torch(x) -> bool:
+    t = type(x)
+    return t.__module__.startswith("torch") and t.__name__ in ("Tensor", "Parameter")
+
+
+def _host_view(arr, operand: Operand):
+    """Returns (buffer usable by the host engine, restore fn)."""
+    if isinstance(arr, np.ndarray):
+        if arr.ndim != 1:
+            raise Mp4jException("array collectives take 1-D arrays")
+        return arr
+    if _is_torch(arr):
+        return arr.numpy()
+    if isinstance(arr, list):
+        return arr
+    raise Mp4jException(f"unsupported array type {type(arr)}")
+
+
+class _FaultInjector:
+    """``MP4X_FAULT_INJECT="rank:op_index[:mode]"`` — kill rank at its op_index-th collective
+    (mode ``exit`` = os._exit(9), ``raise`` = Mp4jException).  Used by the failure tests."""
+
+    def __init__(self, rank: int):
+        spec = os.environ.get("MP4X_FAULT_INJECT", "")
+        self.active = False
+        if spec:
+            parts = spec.split(":")
+            self.rank, self.at = int(parts[0]), int(parts[1])
+            self.mode = parts[2] if len(parts) > 2 else "exit"
+            self.active = self.rank == rank
+        self.count = 0
+
+    def tick(self, name: str):
+        if not self.active:
+            return
+        self.count += 1
+        if self.count == self.at:
+            if self.mode == "raise":
+                raise Mp4jException(f"fault injected in {name}")
+            os._exit(9)
+
+
+class ProcessCommSlave:
+    """Process-level communicator (reference ``ProcessCommSlave``)."""
+
+    def __init__(self, loginName: Optional[str] = None, masterHost: str = "127.0.0.1",
+                 masterPort: int = 61235, *, rank: Optional[int] = None,
+                 heartbeat: bool = True, device: Optional[int] = None):
+        self.loginName = loginName or os.environ.get("USER", "mp4x")
+        self.closed = False
+        self._device_engine = None
+        self._device_index = device
+        LOG.info("master host:%s, master port:%s", masterHost, masterPort)
+        self.server = MasterClient(masterHost, masterPort)
+        loop = masterHost in ("127.0.0.1", "localhost", "::1")
+        self.transport = HostTransport(advertise_host="127.0.0.1" if loop else local_ip())
+        req = rank if rank is not None else int(os.environ.get("MP4X_RANK", -1))
+        info = self.server.call("register", self.transport.address, int(req))
+        if info is None:  # reference bug fixed: it tested `address == null` (ProcessCommSlave.java:159)
+            raise Mp4jException("slaves connecting master failed, may be this slave restarted "
+                                "or master port is occupied, task failed!")
+        self.rank: int = int(info["rank"])
+        self.addresses: List[str] = list(info["addresses"])
+        self.slaveNum: int = len(self.addresses)
+        self.rankMsgPrefix = f"[rank={self.rank}] "
+        self.transport.set_peers(self.rank, self.addresses)
+        self.engine = HostEngine(self.transport, self.rank, self.slaveNum)
+        self._fault = _FaultInjector(self.rank)
+        self.stats: Dict[str, Any] = {"calls": {}, "bytes": 0}
+
+        pid = os.getpid()
+        host = self.transport.advertise_host
+        if self.slaveNum > 1 and not loop:
+            script = f'ssh {self.loginName}@{host} "kill -9 {pid}"'
+        else:
+            script = f"kill -9 {pid}"
+        self.server.call("kill_me", self.rank, script)
+
+        self._hb_stop = threading.Event()
+        self._hb_fail = 0
+        if heartbeat:
+            self._hb_client = MasterClient(masterHost, masterPort)
+            self._hb_thread = threading.Thread(target=self._heartbeat_loop, daemon=True, name="mp4x-heartbeat")
+            self._hb_thread.start()
+        else:
+            self._hb_client = None
+        self.info("this slave init finished!")
+
+    # ================================================================ lifecycle
+    def _heartbeat_loop(self):
+        if self._hb_stop.wait(HEARTBEAT_DELAY):
+            return
+        while not self._hb_stop.is_set():
+            try:
+                if not self.closed:
+                    self._hb_client.call("heartbeat", self.rank)
+                self._hb_fail = 0
+            except Exception as e:  # reference: >4 failures → System.exit(4) (ProcessCommSlave.java:212-227)
+                self._hb_fail += 1
+                LOG.error("rank:%d send heartbeat exception, exception time:%d: %s", self.rank, self._hb_fail, e)
+                if self._hb_fail > HEARTBEAT_MAX_FAIL:
+                    LOG.error("heart beat exception > %d master may be shutdowned! this slave will be shutdowned...",
+                              HEARTBEAT_MAX_FAIL)
+                    os._exit(4)
+            if self._hb_stop.wait(HEARTBEAT_PERIOD):
+                return
+
+    def close(self, code: int = 0) -> None:
+        """Reference ProcessCommSlave.close (:234-271)."""
+        if self.closed:
+            return
+        LOG.info("close code=%s", code)
+        try:
+            self.server.call("close", self.rank, int(code))
+        finally:
+            self.closed = True
+            self._hb_stop.set()
+            if self._device_engine is not None:
+                try:
+                    self._device_engine.shutdown()
+                except Exception:
+                    pass
+            self.transport.close()
+            self.server.close()
+            if self._hb_client is not None:
+                self._hb_client.close()
+
+    def exception(self, e: BaseException) -> None:
+        """Report the stack to the master, wait, then ``close(1)`` (reference :360-373)."""
+        tb = "".join(traceback.format_exception(type(e), e, e.__traceback__))
+        try:
+            self.error("slave exception:" + tb)
+            time.sleep(float(os.environ.get("MP4X_EXCEPTION_SLEEP", 5.0)))
+        finally:
+            self.close(1)
+
+    def writeFile(self, content: str, fileName: str) -> None:
+        self.server.call("write_file", content, fileName)
+
+    def info(self, s: str, onlyRank0: bool = True) -> None:
+        if not onlyRank0:
+            self.server.call("info", self.rank, self.rankMsgPrefix + str(s))
+        elif self.rank == 0:
+            self.server.call("info", self.rank, str(s))
+
+    def debug(self, s: str, onlyRank0: bool = True) -> None:
+        if not onlyRank0:
+            self.server.call("debug", self.rank, self.rankMsgPrefix + str(s))
+        elif self.rank == 0:
+            self.server.call("debug", self.rank, str(s))
+
+    def error(self, s: str) -> None:
+        self.server.call("error", self.rank, self.rankMsgPrefix + str(s))
+
+    def getSlaveNum(self) -> int:
+        return self.slaveNum
+
+    def getRank(self) -> int:
+        return self.rank
+
+    def barrier(self) -> None:
+        """Master barrier (reference :432-438); device work queued before it is NOT waited for."""
+        self._tick("barrier")
+        self.server.call("barrier", self.rank)
+
+    def peer_barrier(self) -> None:
+        """O(log p) barrier over the data plane (no master round trip)."""
+        self.engine.dissemination_barrier()
+
+    # ================================================================ device engine
+    @property
+    def device(self):
+        if self._device_engine is None:
+            from .device_engine import DeviceEngine
+            self._device_engine = DeviceEngine(self, self._device_index)
+        return self._device_engine
+
+    def _tick(self, name: str):
+        self._fault.tick(name)
+        c = self.stats["calls"]
+        c[name] = c.get(name, 0) + 1
+
+    def _check_len(self, a, name):
+        if len(a) != self.slaveNum:
+            raise Mp4jException(f"{name} array length must be equal to slaveNum")
+
+    # ================================================================ gather
+    def gatherArray(self, arrData, operand: Operand, sendfroms: Sequence[int], sendtos: Sequence[int],
+                    rootRank: int):
+        self._tick("gatherArray")
+        self._check_len(sendfroms, "sendfroms")
+        self._check_len(sendtos, "sendtos")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isfromsTosLegal(sendfroms, sendtos)
+        self._check_root(rootRank)
+        if _is_device_tensor(arrData):
+            return self.device.gather(arrData, list(sendfroms), list(sendtos), rootRank)
+        buf = _host_view(arrData, operand)
+        self.engine.tree_gather(buf, sendfroms, sendtos, operand, rootRank)
+        return arrData
+
+    def gatherMap(self, mapData: Dict, operand: Operand, rootRank: int) -> Dict:
+        self._tick("gatherMap")
+        if self.slaveNum == 1:
+            return mapData
+        self._check_root(rootRank)
+        return self.engine.tree_gather_map(mapData, operand, rootRank)
+
+    # ================================================================ allgather
+    def allgatherArray(self, arrData, operand: Operand, froms: Sequence[int], tos: Sequence[int]):
+        self._tick("allgatherArray")
+        self._check_len(froms, "froms")
+        self._check_len(tos, "tos")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isfromsTosLegal(froms, tos)
+        if _is_device_tensor(arrData):
+            return self.device.allgather(arrData, list(froms), list(tos))
+        buf = _host_view(arrData, operand)
+        self.engine.ring_allgather(buf, froms, tos, operand)
+        return arrData
+
+    def allgatherMap(self, mapData: Dict, operand: Operand) -> List[Dict]:
+        self._tick("allgatherMap")
+        if self.slaveNum == 1:
+            return [mapData]
+        blocks = self.engine.ring_allgather_maps([mapData], operand)
+        return [b[0] for b in blocks]
+
+    # ================================================================ broadcast
+    def broadcastArray(self, arrData, operand: Operand, frm: int, to: int, rootRank: int):
+        self._tick("broadcastArray")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isFromToLegal(frm, to)
+        self._check_root(rootRank)
+        if _is_device_tensor(arrData):
+            return self.device.broadcast(arrData, frm, to, rootRank)
+        buf = _host_view(arrData, operand)
+        nbytes = (to - frm) * (operand.np_dtype.itemsize if operand.is_primitive else 64)
+        if nbytes <= BCAST_TREE_BYTES or (to - frm) < self.slaveNum:
+            self.engine.tree_bcast(buf, frm, to, operand, rootRank)
+        else:
+            # van de Geijn: scatter + allgather (reference :750-775)
+            froms, tos, _ = CommUtils.even_split(frm, to, self.slaveNum)
+            self.engine.tree_scatter(buf, froms, tos, operand, rootRank)
+            self.engine.ring_allgather(buf, froms, tos, operand)
+        return arrData
+
+    def broadcast(self, value, operand: Operand, rootRank: int):
+        self._tick("broadcast")
+        if self.slaveNum == 1:
+            return value
+        arr = operand.box(value)
+        self.broadcastArray(arr, operand, 0, 1, rootRank)
+        return operand.unbox(arr)
+
+    def broadcastMap(self, mapData: Dict, operand: Operand, rootRank: int) -> Dict:
+        """Root partitions by key hash → scatterMap → allgatherMap → merge (reference :842-883)."""
+        self._tick("broadcastMap")
+        if self.slaveNum == 1:
+            return mapData
+        self._check_root(rootRank)
+        p = self.slaveNum
+        blocks = None
+        if self.rank == rootRank:
+            blocks = [[{}] for _ in range(p)]
+            for k, v in mapData.items():
+                blocks[owner_of(k, p)][0][k] = v
+        mine = self.engine.tree_scatter_maps(blocks, operand, rootRank)
+        allb = self.engine.ring_allgather_maps(mine, operand)
+        out: Dict = {}
+        for blk in allb:
+            for d in blk:
+                out.update(d)
+        return out
+
+    # ================================================================ scatter
+    def scatterArray(self, arrData, operand: Operand, recvfroms: Sequence[int], recvtos: Sequence[int],
+                     rootRank: int):
+        self._tick("scatterArray")
+        self._check_len(recvfroms, "recvfroms")
+        self._check_len(recvtos, "recvtos")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isfromsTosLegal(recvfroms, recvtos)
+        self._check_root(rootRank)
+        if _is_device_tensor(arrData):
+            return self.device.scatter(arrData, list(recvfroms), list(recvtos), rootRank)
+        buf = _host_view(arrData, operand)
+        self.engine.tree_scatter(buf, recvfroms, recvtos, operand, rootRank)
+        return arrData
+
+    def scatterMap(self, mapDataList: List[Dict], operand: Operand, rootRank: int) -> Dict:
+        self._tick("scatterMap")
+        if self.rank == rootRank and len(mapDataList) != self.slaveNum:
+            raise Mp4jException("mapDataList size must be equal to slaveNum")
+        if self.slaveNum == 1:
+            return mapDataList[0]
+        self._check_root(rootRank)
+        blocks = [[d] for d in mapDataList] if self.rank == rootRank else None
+        got = self.engine.tree_scatter_maps(blocks, operand, rootRank)
+        if not got:
+            raise Mp4jException("scatter error retmap must not be null!")
+        return got[0]
+
+    def scatterMapSpecial(self, mapDataListList: List[List[Dict]], operand: Operand, rootRank: int) -> List[Dict]:
+        """``list[rank][t]`` → rank receives its list of T maps (reference :999-1051)."""
+        if self.slaveNum == 1:
+            return mapDataListList[0]
+        blocks = mapDataListList if self.rank == rootRank else None
+        return self.engine.tree_scatter_maps(blocks, operand, rootRank)
+
+    # ================================================================ reduce-scatter
+    def reduceScatterArray(self, arrData, operand: Operand, operator, frm: int, counts: Sequence[int]):
+        self._tick("reduceScatterArray")
+        self._check_len(counts, "counts")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isFromCountsLegal(frm, counts)
+        froms = CommUtils.getFromsFromCount(frm, counts, self.slaveNum)
+        tos = CommUtils.getTosFromCount(frm, counts, self.slaveNum)
+        if _is_device_tensor(arrData):
+            return self.device.reduce_scatter(arrData, froms, tos, operator, operand)
+        buf = _host_view(arrData, operand)
+        self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
+        return arrData
+
+    def reduceScatterMap(self, mapDataList: List[Dict], operand: Operand, operator) -> Dict:
+        self._tick("reduceScatterMap")
+        if self.slaveNum == 1:
+            return mapDataList[0]
+        if len(mapDataList) != self.slaveNum:
+            raise Mp4jException(f"mapDataList size={len(mapDataList)}, must be equal to slaveNum={self.slaveNum}")
+        return self.engine.ring_reduce_scatter_maps([[d] for d in mapDataList], operand, operator)[0]
+
+    def reduceScatterMapSpecial(self, mapDataListList: List[List[Dict]], operand: Operand, operator) -> List[Dict]:
+        if self.slaveNum == 1:
+            return mapDataListList[0]
+        if len(mapDataListList) != self.slaveNum:
+            raise Mp4jException(f"mapDataListList size={len(mapDataListList)}, must be equal to slaveNum={self.slaveNum}")
+        return self.engine.ring_reduce_scatter_maps(mapDataListList, operand, operator)
+
+    # ================================================================ reduce
+    def reduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, rootRank: int):
+        """reduce-scatter + gather (reference :1390-1421)."""
+        self._tick("reduceArray")
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isFromToLegal(frm, to)
+        self._check_root(rootRank)
+        if _is_device_tensor(arrData):
+            return self.device.reduce(arrData, frm, to, operator, operand, rootRank)
+        buf = _host_view(arrData, operand)
+        froms, tos, counts = CommUtils.even_split(frm, to, self.slaveNum)
+        self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
+        self.engine.tree_gather(buf, froms, tos, operand, rootRank)
+        return arrData
+
+    def reduce(self, value, operand: Operand, operator, rootRank: int):
+        self._tick("reduce")
+        if self.slaveNum == 1:
+            return value
+        arr = operand.box(value)
+        self.reduceArray(arr, operand, operator, 0, 1, rootRank)
+        return operand.unbox(arr)
+
+    def _partition(self, mapData: Dict) -> List[Dict]:
+        p = self.slaveNum
+        parts: List[Dict] = [{} for _ in range(p)]
+        for k, v in mapData.items():
+            parts[owner_of(k, p)][k] = v
+        return parts
+
+    def reduceMap(self, mapData: Dict, operand: Operand, operator, rootRank: int) -> Dict:
+        """hash-partition → reduceScatterMap → gatherMap (reference :1490-1516)."""
+        self._tick("reduceMap")
+        if self.slaveNum == 1:
+            return mapData
+        self._check_root(rootRank)
+        mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)[0]
+        return self.engine.tree_gather_map(mine, operand, rootRank)
+
+    # ---- set / list specials (reference :1518-1720, :2099-2230)
+    @staticmethod
+    def _set_operand(elementSerializer=None) -> Operand:
+        return Operands.OBJECT_OPERAND(elementSerializer or DEFAULT_SERIALIZER)
+
+    _UNION = CustomOperator(lambda a, b: set(a) | set(b), name="set_union")
+    _INTERSECT = CustomOperator(lambda a, b: set(a) & set(b), name="set_intersection")
+    _CONCAT = CustomOperator(lambda a, b: list(a) + list(b), name="list_concat")
+
+    def reduceMapSetUnion(self, mapData: Dict, rootRank: int, elementSerializer=None, elementType=None) -> Dict:
+        return self.reduceMap(mapData, self._set_operand(elementSerializer), self._UNION, rootRank)
+
+    def reduceSetUnion(self, setData, rootRank: int, elementSerializer=None, elementType=None):
+        r = self.reduceMapSetUnion({"key": setData}, rootRank, elementSerializer, elementType)
+        return None if r is None else r.get("key")
+
+    def reduceMapSetIntersection(self, mapData: Dict, rootRank: int, elementSerializer=None, elementType=None) -> Dict:
+        return self.reduceMap(mapData, self._set_operand(elementSerializer), self._INTERSECT, rootRank)
+
+    def reduceSetIntersection(self, setData, rootRank: int, elementSerializer=None, elementType=None):
+        r = self.reduceMapSetIntersection({"key": setData}, rootRank, elementSerializer, elementType)
+        return None if r is None else r.get("key")
+
+    def reduceMapListConcat(self, mapData: Dict, rootRank: int, elementSerializer=None, elementType=None) -> Dict:
+        return self.reduceMap(mapData, self._set_operand(elementSerializer), self._CONCAT, rootRank)
+
+    def reduceListConcat(self, listData, rootRank: int, elementSerializer=None, elementType=None):
+        r = self.reduceMapListConcat({"key": listData}, rootRank, elementSerializer, elementType)
+        return None if r is None else r.get("key")
+
+    def allreduceMapSetUnion(self, mapData: Dict, elementSerializer=None, elementType=None) -> Dict:
+        return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._UNION)
+
+    def allreduceSetUnion(self, setData, elementSerializer=None, elementType=None):
+        return self.allreduceMapSetUnion({"key": setData}, elementSerializer, elementType).get("key")
+
+    def allreduceMapSetIntersection(self, mapData: Dict, elementSerializer=None, elementType=None) -> Dict:
+        return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._INTERSECT)
+
+    def allreduceSetIntersection(self, setData, elementSerializer=None, elementType=None):
+        return self.allreduceMapSetIntersection({"key": setData}, elementSerializer, elementType).get("key")
+
+    def allreduceMapListConcat(self, mapData: Dict, elementSerializer=None, elementType=None) -> Dict:
+        return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._CONCAT)
+
+    def allreduceListConcat(self, listData, elementSerializer=None, elementType=None):
+        return self.allreduceMapListConcat({"key": listData}, elementSerializer, elementType).get("key")
+
+    # ================================================================ allreduce
+    def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, out=None):
+        """reduce-scatter + allgather with the last rank taking the remainder (reference :1733-1763).
+
+        ``out`` (extension): out-of-place form — ``out[from:to]`` receives the result and
+        ``arrData`` is left untouched (with one rank this is a plain copy).
+        """
+        self._tick("allreduceArray")
+        if out is not None:
+            CommUtils.isFromToLegal(frm, to)
+            if _is_torch(out):
+                out.view(-1)[frm:to].copy_(arrData.view(-1)[frm:to])
+            else:
+                out[frm:to] = arrData[frm:to]
+            if self.slaveNum == 1:
+                return out
+            arrData = out
+        if self.slaveNum == 1:
+            return arrData
+        CommUtils.isFromToLegal(frm, to)
+        if _is_device_tensor(arrData):
+            return self.device.allreduce(arrData, frm, to, operator, operand)
+        buf = _host_view(arrData, operand)
+        froms, tos, _ = CommUtils.even_split(frm, to, self.slaveNum)
+        self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
+        self.engine.ring_allgather(buf, froms, tos, operand)
+        return arrData
+
+    def allreduce(self, value, operand: Operand, operator):
+        self._tick("allreduce")
+        if self.slaveNum == 1:
+            return value
+        arr = operand.box(value)
+        self.allreduceArray(arr, operand, operator, 0, 1)
+        return operand.unbox(arr)
+
+    def allreduceArrayRpc(self, arrData, operand: Operand, operator):
+        """Small-data allreduce through the master (reference :1776-1926, Server.java:373-514).
+
+        Every rank uploads its whole array; the master returns all p copies in
+        RANK order; each rank folds them locally (op(op(r0, r1), r2) ...).  For
+        device tensors the latency path is the device engine's small-message
+        allreduce instead.
+        """
+        self._tick("allreduceArrayRpc")
+        if self.slaveNum == 1:
+            return arrData
+        if _is_device_tensor(arrData):
+            return self.device.allreduce(arrData, 0, arrData.numel(), operator, operand, small=True)
+        buf = _host_view(arrData, operand)
+        if operand.is_primitive:
+            payload = np.ascontiguousarray(buf).tobytes()
+        else:
+            payload = operand.serializer.write_list(buf)
+        copies = self.server.call("rpc_allreduce", self.rank, payload)
+        if operand.is_primitive:
+            acc = np.frombuffer(copies[0], dtype=operand.np_dtype).copy()
+            for c in copies[1:]:
+                x = np.frombuffer(c, dtype=operand.np_dtype)
+                with np.errstate(over="ignore", invalid="ignore"):
+                    operator.reduce_into(acc, x)
+            buf[:] = acc
+        else:
+            acc = operand.serializer.read_list(copies[0])
+            for c in copies[1:]:
+                x = operand.serializer.read_list(c)
+                acc = [operator.apply(a, b) for a, b in zip(acc, x)]
+            buf[:] = acc
+        return arrData
+
+    def allreduceRpc(self, value, operand: Operand, operator):
+        self._tick("allreduceRpc")
+        if self.slaveNum == 1:
+            return value
+        arr = operand.box(value)
+        self.allreduceArrayRpc(arr, operand, operator)
+        return operand.unbox(arr)
+
+    def allreduceMap(self, mapData: Dict, operand: Operand, operator) -> Dict:
+        """partition → reduceScatterMap → allgatherMap → merge (reference :2053-2088)."""
+        self._tick("allreduceMap")
+        if self.slaveNum == 1:
+            return mapData
+        if mapData and _is_device_tensor(next(iter(mapData.values()))):
+            return self.device.allreduce_map(mapData, operator)
+        mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)
+        allb = self.engine.ring_allgather_maps(mine, operand)
+        out: Dict = {}
+        for blk in allb:
+            for d in blk:
+                out.update(d)
+        return out
+
+    # ================================================================ helpers
+    def _check_root(self, root: int):
+        if not (0 <= root < self.slaveNum):
+            raise RangeError(f"root rank {root} out of range [0, {self.slaveNum})")
+
+    # torch-style conveniences ---------------------------------------------------
+    def allreduce_tensor(self, tensor, operator=None, operand: Optional[Operand] = None):
+        """Whole-tensor in-place allreduce (flattened view), SUM by default."""
+        from ..operators import Operators
+        op = operator or Operators.Float.SUM
+        flat = tensor.view(-1) if _is_torch(tensor) else tensor.reshape(-1)
+        opnd = operand or Operands.FLOAT_OPERAND()
+        self.allreduceArray(flat, opnd, op, 0, flat.shape[0])
+        return tensor
+
+
+# snake_case aliases --------------------------------------------------------------
+def _snake(name: str) -> str:
+    out = []
+    for i, ch in enumerate(name):
+        if ch.isupper() and i > 0:
+            out.append("_")
+        out.append(ch.lower())
+    return "".join(out)
+
+
+for _n in [n for n in dir(ProcessCommSlave) if not n.startswith("_")]:
+    _sn = _snake(_n)
+    if _sn != _n and not hasattr(ProcessCommSlave, _sn):
+        setattr(ProcessCommSlave, _sn, getattr(ProcessCommSlave, _n))
+
+ProcessComm = ProcessCommSlave

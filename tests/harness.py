@@ -1,0 +1,75 @@
+"""Local multi-process harness: a CommMaster thread + p rank processes on 127.0.0.1.
+
+The reference's integration checks run a real master and N slave JVMs
+(bin/comm_cluster_error_check.sh); this is the same topology on one host.
+"""
+import multiprocessing as mp
+import os
+import traceback
+
+from mp4x.control.master import CommMaster
+
+
+def _worker(fn, rank_hint, port, args, q, kind, threads):
+    try:
+        from mp4x import ProcessCommSlave, ThreadCommSlave
+        if kind == "thread":
+            comm = ThreadCommSlave("test", threads, "127.0.0.1", port, heartbeat=False)
+        else:
+            comm = ProcessCommSlave("test", "127.0.0.1", port, heartbeat=False)
+        res = fn(comm, *args)
+        comm.close(0)
+        q.put((comm.getRank(), "ok", res))
+    except BaseException as e:  # noqa
+        q.put((rank_hint, "err", traceback.format_exc()))
+
+
+def run_ranks(p, fn, args=(), timeout=120, kind="process", threads=1, master_kwargs=None, expect_fail=False,
+              env=None):
+    ctx = mp.get_context("fork")
+    import tempfile
+    mk = dict(master_kwargs or {})
+    mk.setdefault("workdir", tempfile.mkdtemp(prefix="mp4x_master_"))
+    master = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, **mk).start()
+    q = ctx.Queue()
+    old = {}
+    for k, v in (env or {}).items():
+        old[k] = os.environ.get(k)
+        os.environ[k] = v
+    try:
+        procs = [ctx.Process(target=_worker, args=(fn, i, master.port, args, q, kind, threads)) for i in range(p)]
+        for pr in procs:
+            pr.start()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    results = {}
+    errors = []
+    import queue as _q
+    try:
+        for _ in range(p):
+            try:
+                r, st, val = q.get(timeout=timeout)
+            except _q.Empty:
+                break
+            if st == "ok":
+                results[r] = val
+            else:
+                errors.append(val)
+                if not expect_fail:
+                    break
+    finally:
+        for pr in procs:
+            pr.join(timeout=5)
+            if pr.is_alive():
+                pr.kill()
+                pr.join(timeout=5)
+        code = master.stop(timeout=5)
+    if errors and not expect_fail:
+        raise AssertionError("rank failed:\n" + "\n".join(errors))
+    if not expect_fail and len(results) != p:
+        raise AssertionError(f"only {len(results)}/{p} ranks finished")
+    return results, code, errors

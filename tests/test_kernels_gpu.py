@@ -1,0 +1,207 @@
+"""Numerics of the hand-written HIP kernels vs plain PyTorch references (GPU only)."""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from mp4x.operators import OpCode, DType  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _native():
+    from mp4x.ops import device_ops, native
+    native.hip()
+    return device_ops
+
+
+def _ref_reduce(xs, code, dtype):
+    acc = xs[0].clone()
+    for x in xs[1:]:
+        if code == OpCode.SUM:
+            acc = acc + x
+        elif code == OpCode.PROD:
+            acc = acc * x
+        elif code == OpCode.MAX:
+            acc = torch.maximum(acc, x)
+        elif code == OpCode.MIN:
+            acc = torch.minimum(acc, x)
+        elif code == OpCode.BAND:
+            acc = acc & x
+        elif code == OpCode.BOR:
+            acc = acc | x
+        elif code == OpCode.BXOR:
+            acc = acc ^ x
+    return acc
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64, torch.int16, torch.int8])
+@pytest.mark.parametrize("code", [OpCode.SUM, OpCode.MAX, OpCode.MIN, OpCode.PROD])
+@pytest.mark.parametrize("nin", [1, 2, 3, 8, 11])
+def test_reduce_arith(dtype, code, nin):
+    K = _native()
+    n = 100_003  # odd: exercises the vector body and the scalar tail
+    g = torch.Generator(device=DEV).manual_seed(nin * 31 + int(code))
+    if dtype.is_floating_point:
+        xs = [torch.randn(n, device=DEV, dtype=dtype, generator=g) for _ in range(nin)]
+        if code == OpCode.PROD:
+            xs = [x.clamp(-1.5, 1.5) for x in xs]
+    else:
+        xs = [torch.randint(-50, 50, (n,), device=DEV, dtype=dtype, generator=g) for _ in range(nin)]
+    out = torch.empty_like(xs[0])
+    K.reduce_(out, xs, int(code))
+    if dtype.is_floating_point:
+        ref = _ref_reduce([x.double() for x in xs], code, dtype).to(dtype)
+        tol = 1e-5 if dtype == torch.float32 else 1e-12
+        torch.testing.assert_close(out, ref, rtol=tol * nin, atol=tol * nin)
+    else:
+        # integer math wraps (two's complement) like the reference's Java operators
+        ref = _ref_reduce([x.long() for x in xs], code, dtype)
+        bits = torch.iinfo(dtype).bits
+        ref = ((ref + (1 << (bits - 1))) % (1 << bits)) - (1 << (bits - 1)) if bits < 64 else ref
+        assert torch.equal(out.long(), ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.int32, torch.int64, torch.int16, torch.int8])
+@pytest.mark.parametrize("code", [OpCode.BAND, OpCode.BOR, OpCode.BXOR])
+def test_reduce_bitwise(dtype, code):
+    K = _native()
+    n = 65_537
+    xs = [torch.randint(-100, 100, (n,), device=DEV, dtype=dtype) for _ in range(4)]
+    out = xs[0].clone()
+    K.reduce_(out, [out] + xs[1:], int(code))
+    assert torch.equal(out, _ref_reduce(xs, code, dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_reduce_half_accumulates_in_f32(dtype):
+    K = _native()
+    n = 1 << 20
+    xs = [torch.randn(n, device=DEV).to(dtype) for _ in range(8)]
+    out = torch.empty_like(xs[0])
+    K.reduce_(out, xs, int(OpCode.SUM))
+    ref = sum(x.float() for x in xs).to(dtype)   # one rounding, like the kernel
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+def test_reduce_loc_ops():
+    K = _native()
+    import numpy as np
+    from mp4x.operators import Operators
+    n = 10_001
+    rng = np.random.default_rng(0)
+    vals = [rng.integers(-5, 5, n).astype(np.float32) for _ in range(3)]   # many ties
+    words = []
+    for k, v in enumerate(vals):
+        bits = (v.view(np.uint32).astype(np.uint64) << np.uint64(32)) | np.uint64(k)
+        words.append(bits.view(np.float64))
+    for op in (Operators.Double.FLOAT_MAX_LOC, Operators.Double.FLOAT_MIN_LOC):
+        acc = words[0].copy()
+        for w in words[1:]:
+            op.reduce_into(acc, w)
+        ts = [torch.from_numpy(w).to(DEV) for w in words]
+        out = torch.empty_like(ts[0])
+        K.reduce_(out, ts, int(op.code))
+        assert np.array_equal(out.cpu().numpy().view(np.uint64), acc.view(np.uint64))
+    ivals = [rng.integers(-5, 5, n).astype(np.int32) for _ in range(3)]
+    iw = [((v.astype(np.int64) << 32) | k).astype(np.int64) for k, v in enumerate(ivals)]
+    for op in (Operators.Long.INT_MAX_LOC, Operators.Long.INT_MIN_LOC):
+        acc = iw[0].copy()
+        for w in iw[1:]:
+            op.reduce_into(acc, w)
+        out = torch.empty(n, dtype=torch.int64, device=DEV)
+        K.reduce_(out, [torch.from_numpy(w).to(DEV) for w in iw], int(op.code))
+        assert np.array_equal(out.cpu().numpy(), acc)
+
+
+def test_reduce_unaligned_views():
+    K = _native()
+    base = [torch.randn(5000, device=DEV) for _ in range(3)]
+    xs = [b[1:4001] for b in base]            # 4-byte aligned, not 16-byte aligned
+    out = torch.empty(4000, device=DEV)
+    K.reduce_(out, xs, int(OpCode.SUM))
+    torch.testing.assert_close(out, xs[0] + xs[1] + xs[2])
+
+
+def test_scale():
+    K = _native()
+    x = torch.randn(12345, device=DEV)
+    y = torch.empty_like(x)
+    K.scale_(y, x, 0.125)
+    torch.testing.assert_close(y, x * 0.125)
+
+
+def test_segment_copy_and_gather_rows():
+    K = _native()
+    src = torch.arange(10_000, device=DEV, dtype=torch.float32)
+    dst = torch.zeros(10_000, device=DEV)
+    segs = [(0, 5000, 100), (100, 0, 3), (5000, 17, 4096), (9999, 1, 1)]
+    K.segment_copy_(dst, src, segs)
+    ref = torch.zeros(10_000, device=DEV)
+    for d, s, l in segs:
+        ref[d:d + l] = src[s:s + l]
+    assert torch.equal(dst, ref)
+    table = torch.randn(300, 40, device=DEV)
+    idx = torch.randint(0, 300, (1000,), device=DEV)
+    assert torch.equal(K.gather_rows(table, idx), table[idx])
+    t3 = torch.randn(50, 7, device=DEV).to(torch.bfloat16)   # 14-byte rows: byte path
+    i3 = torch.randint(0, 50, (77,), device=DEV)
+    assert torch.equal(K.gather_rows(t3, i3), t3[i3])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fp8_codec_roundtrip_error(dtype):
+    K = _native()
+    n = 256 * 1000 + 4
+    x = (torch.randn(n, device=DEV) * torch.linspace(0.01, 100, n, device=DEV)).to(dtype)
+    q, s = K.quant_fp8(x)
+    y = torch.empty(n, device=DEV, dtype=torch.float32)
+    K.dequant_fp8(q, s, n, y)
+    xf = x.float()
+    # e4m3 has 3 mantissa bits: relative error <= 2^-4 of the block amax
+    blk = torch.nn.functional.pad(xf.abs(), (0, (-n) % 256)).view(-1, 256).amax(1)
+    bound = blk.repeat_interleave(256)[:n] * (2 ** -4) + 1e-30
+    assert ((y - xf).abs() <= bound).all()
+
+
+def test_fp8_dequant_reduce_requant():
+    K = _native()
+    n = 256 * 64
+    xs = [torch.randn(n, device=DEV) for _ in range(5)]
+    qs, ss = zip(*[K.quant_fp8(x) for x in xs])
+    out = torch.empty(n, device=DEV)
+    q2 = torch.empty(n, dtype=torch.uint8, device=DEV)
+    s2 = torch.empty(n // 256, device=DEV)
+    K.dequant_reduce_fp8(out, list(qs), list(ss), n, q_out=q2, s_out=s2)
+    ref = sum(xs)
+    assert (out - ref).abs().max() < 0.5   # 5 inputs x e4m3 error
+    back = torch.empty(n, device=DEV)
+    K.dequant_fp8(q2, s2, n, back)
+    assert (back - out).abs().max() <= out.abs().max() * 2 ** -4 + 1e-6
+
+
+@pytest.mark.parametrize("dim", [1, 8, 100])
+def test_reduce_by_key_matches_torch(dim):
+    K = _native()
+    n = 20_000
+    keys = torch.randint(0, 3000, (n,), device=DEV, dtype=torch.int64) * 7919
+    vals = torch.randn(n, dim, device=DEV)
+    uk, uv, cnt = K.reduce_by_key(keys, vals, int(OpCode.SUM))
+    ref_k, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    ref_v = torch.zeros(ref_k.numel(), dim, device=DEV).index_add_(0, inv, vals)
+    assert torch.equal(uk, ref_k)
+    torch.testing.assert_close(uv, ref_v, rtol=1e-5, atol=1e-4)
+    assert int(cnt.sum()) == n
+    uk2, uv2, _ = K.reduce_by_key(keys, vals, int(OpCode.MAX))
+    ref_m = torch.full((ref_k.numel(), dim), -float("inf"), device=DEV).scatter_reduce_(
+        0, inv[:, None].expand(-1, dim), vals, "amax")
+    torch.testing.assert_close(uv2, ref_m)
+
+
+def test_key_owner_hist():
+    K = _native()
+    keys = torch.randint(0, 1 << 62, (50_000,), device=DEV, dtype=torch.int64)
+    dest, hist = K.key_owner(keys, 7)
+    assert torch.equal(dest.long(), keys % 7)
+    assert torch.equal(hist.long(), torch.bincount(keys % 7, minlength=7))

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the mp4x CDNA4 kernels vs the HBM roofline and vs PyTorch.
+
+Reports achieved bandwidth (bytes moved / time) per kernel.  Used under rocprofv3 for the
+profiles in profiles/.  Interleaves variants in one process (cdna guide §5.4 rule 24).
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from mp4x.operators import OpCode  # noqa: E402
+from mp4x.ops import device_ops as K  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(iters):
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mb", type=int, default=1024, help="per-input size in MiB")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    n = a.mb * (1 << 20) // 4
+    res = {}
+    xs = [torch.randn(n, device=dev) for _ in range(8)]
+    out = torch.empty_like(xs[0])
+    for nin in ([2, 8] if a.quick else [1, 2, 4, 8]):
+        ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
+        nbytes = (nin + 1) * n * 4
+        res[f"k1_reduce_f32_nin{nin}"] = {"ms": ms, "GBps": nbytes / ms / 1e6}
+        if nin == 2:
+            ms_t = timeit(lambda: torch.add(xs[0], xs[1], out=out), a.iters)
+            res["torch_add_f32"] = {"ms": ms_t, "GBps": nbytes / ms_t / 1e6}
+    # bf16
+    xb = [x.to(torch.bfloat16) for x in xs[:4]]
+    ob = torch.empty_like(xb[0])
+    ms = timeit(lambda: K.reduce_(ob, xb, int(OpCode.SUM)), a.iters)
+    res["k1_reduce_bf16_nin4"] = {"ms": ms, "GBps": 5 * n * 2 / ms / 1e6}
+    # copy (D2D) baseline
+    ms = timeit(lambda: out.copy_(xs[0]), a.iters)
+    res["torch_copy_f32"] = {"ms": ms, "GBps": 2 * n * 4 / ms / 1e6}
+    # fp8 codec
+    q = torch.empty(n, dtype=torch.uint8, device=dev)
+    s = torch.empty((n + 255) // 256, device=dev)
+    ms = timeit(lambda: K.quant_fp8(xs[0], q, s), a.iters)
+    res["k6_quant_fp8_f32"] = {"ms": ms, "GBps": (n * 4 + n) / ms / 1e6}
+    qs = [q] * 8
+    ss = [s] * 8
+    ms = timeit(lambda: K.dequant_reduce_fp8(out, qs, ss, n), a.iters)
+    res["k6_dequant_reduce_fp8_nin8"] = {"ms": ms, "GBps": (8 * n + n * 4) / ms / 1e6}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Build the mp4x native libraries in-tree (gfx950).
+
+* ``mp4x/_native/libmp4x_hip.so``  — HIP kernels (csrc/kernels/*.hip) + device runtime
+  (csrc/runtime/*.hip): compiled with ``hipcc --offload-arch=gfx950`` and linked against the
+  SAME ``libamdhip64.so`` that PyTorch-ROCm loads (torch/lib), so kernels launch on torch's
+  streams inside one HIP runtime instance.
+* ``mp4x/_native/libmp4x_host.so`` — host runtime (csrc/host/*.cpp): CPU reduction kernels,
+  the TCP data-plane engine; plain g++, no GPU dependency.
+
+Incremental: objects are rebuilt only when a source or header is newer.
+Usage: python tools/build_native.py [--clean] [-j N]
+"""
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "csrc")
+OUT = os.path.join(ROOT, "mp4x", "_native")
+OBJ = os.path.join(ROOT, "build", "obj")
+ARCH = os.environ.get("MP4X_ARCH", os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")).split(";")[0]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def torch_lib_dir():
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec and spec.origin:
+            d = os.path.join(os.path.dirname(spec.origin), "lib")
+            if os.path.exists(os.path.join(d, "libamdhip64.so")):
+                return d
+    except Exception:
+        pass
+    return None
+
+
+def headers():
+    return glob.glob(os.path.join(CSRC, "**", "*.h*"), recursive=True)
+
+
+def newer(src, obj, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in deps)
+
+
+def run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(" ".join(cmd) + "\n" + r.stdout)
+        raise SystemExit(f"build failed: {cmd[-1]}")
+    return r.stdout
+
+
+def build_hip(jobs):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "runtime", "*.hip")))
+    deps = headers()
+    os.makedirs(OBJ, exist_ok=True)
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if newer(s, o, deps):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+             "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+        return s
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for s in ex.map(comp, todo):
+            print("  hipcc", os.path.relpath(s, ROOT))
+    out = os.path.join(OUT, "libmp4x_hip.so")
+    if todo or not os.path.exists(out):
+        tl = torch_lib_dir()
+        libdir = tl or "/opt/rocm/lib"
+        # Link with the host compiler (not hipcc, which would add /opt/rocm's libamdhip64.so.7):
+        # the kernels must bind to the SAME HIP runtime instance PyTorch-ROCm loaded, or torch's
+        # stream handles and device pointers would belong to a different runtime.
+        link = ["g++", "-shared", "-fPIC", "-o", out] + objs
+        if tl:
+            link += ["-L", tl, "-l:libamdhip64.so", "-Wl,-rpath," + tl]
+        else:
+            link += ["-L", libdir, "-lamdhip64", "-Wl,-rpath," + libdir]
+        run(link)
+        print("  link ", os.path.relpath(out, ROOT), "(hip runtime from", libdir + ")")
+    return out
+
+
+def build_host(jobs):
+    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    if not srcs:
+        return None
+    deps = headers()
+    os.makedirs(OBJ, exist_ok=True)
+    objs, todo = [], []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if newer(s, o, deps):
+            todo.append((s, o))
+
+    def comp(so):
+        s, o = so
+        run(["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-Wall", "-fopenmp", "-pthread",
+             "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+        return s
+
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        for s in ex.map(comp, todo):
+            print("  g++  ", os.path.relpath(s, ROOT))
+    out = os.path.join(OUT, "libmp4x_host.so")
+    if todo or not os.path.exists(out):
+        run(["g++", "-shared", "-fPIC", "-fopenmp", "-pthread", "-o", out] + objs)
+        print("  link ", os.path.relpath(out, ROOT))
+    return out
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    a = ap.parse_args(argv)
+    if a.clean:
+        shutil.rmtree(os.path.join(ROOT, "build"), ignore_errors=True)
+        for f in glob.glob(os.path.join(OUT, "*.so")):
+            os.remove(f)
+    os.makedirs(OUT, exist_ok=True)
+    print(f"mp4x native build (arch {ARCH})")
+    build_hip(a.j)
+    build_host(a.j)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
