@@ -31,6 +31,19 @@ REF_BUSBW_MBPS = {2: 85.2, 4: 92.1, 6: 86.8, 8: 88.0}
 METRIC = "allreduce bus bandwidth (GB/s) + p50 latency, 1 GB float[], 1/2/4/8 MI355X"
 
 
+class _CpuEvent:
+    """time.perf_counter stand-in for torch.cuda.Event in the --cpu dry run."""
+
+    def __init__(self, enable_timing=True):
+        self.t = 0.0
+
+    def record(self, *a):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -39,6 +52,7 @@ def main():
     ap.add_argument("--bytes", type=int, default=1_000_000_000)
     ap.add_argument("--algo", default=None, help="force device algorithm: rccl | a2a")
     ap.add_argument("--codec", default=None, help="wire codec for the fp8-compressed config: fp8")
+    ap.add_argument("--cpu", action="store_true", help="dry run of the launch/rendezvous path on CPU (gloo)")
     args = ap.parse_args()
     if args.algo:
         os.environ["MP4X_DEVICE_ALGO"] = args.algo
@@ -53,8 +67,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.cpu:
+        dev = torch.device("cpu")
+        torch.cuda.synchronize = lambda *a, **k: None
+        torch.cuda.Event = _CpuEvent
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
 
     comm = init_from_env(heartbeat=False)
     p = comm.getSlaveNum()
@@ -76,10 +95,10 @@ def main():
     def sync_all():
         torch.cuda.synchronize()
         if p > 1:
-            comm.device.barrier()
+            comm.peer_barrier() if args.cpu else comm.device.barrier()
             torch.cuda.synchronize()
 
-    if p > 1:
+    if p > 1 and not args.cpu:
         comm.device  # bring up the RCCL communicator before timing
     for _ in range(args.warmup):
         step()
@@ -92,10 +111,7 @@ def main():
         starts[i].record()
         step()
         ends[i].record()
-    torch.cuda.synchronize()
-    if p > 1:
-        comm.device.barrier()
-        torch.cuda.synchronize()
+    sync_all()
     wall = time.perf_counter() - t0
     lat = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))   # ms
 
@@ -103,7 +119,11 @@ def main():
     vals = torch.tensor([wall, lat[len(lat) // 2], lat[min(len(lat) - 1, int(0.99 * len(lat)))]],
                         dtype=torch.float64, device=dev)
     if p > 1:
-        dist.all_reduce(vals, op=dist.ReduceOp.MAX)
+        if args.cpu:
+            vals = torch.from_numpy(comm.allreduceArray(vals.numpy(), Operands.DOUBLE_OPERAND(),
+                                                        Operators.Double.MAX, 0, 3))
+        else:
+            dist.all_reduce(vals, op=dist.ReduceOp.MAX)
     wall, p50, p99 = vals.tolist()
 
     ms_per_step = wall * 1e3 / args.steps
@@ -112,7 +132,8 @@ def main():
     factor = 2.0 * (p - 1) / p if p > 1 else 1.0
     busbw = algbw * factor
     ref = REF_BUSBW_MBPS.get(p)
-    algo = "copy" if p == 1 else comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand)
+    algo = "copy" if p == 1 else ("host-tcp" if args.cpu else
+                                  comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand))
     if rank == 0:
         rec = {
             "metric": METRIC,

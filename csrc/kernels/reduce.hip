@@ -15,6 +15,7 @@
 //  * 16-bit floats accumulate in f32 across the whole fan-in and round once;
 //  * operands with mismatched 16-byte alignment fall back to the scalar kernel.
 #include "common.hpp"
+#include <stdlib.h>
 
 namespace mp4x {
 
@@ -74,6 +75,98 @@ __global__ __launch_bounds__(kBlock) void k_reduce_vec(void* __restrict__ out_, 
   }
 }
 
+// Tile variant: block b owns vectors [b*kBlock*U, (b+1)*kBlock*U); lane t handles
+// b*kBlock*U + t + k*kBlock (k < U) — every load instruction of a wave covers 1 KiB contiguous,
+// all U*NIN loads are issued before the first combine.  NT selects nontemporal loads/stores
+// (streamed once, keep them out of L2/MALL).
+template <typename T, bool NT>
+__device__ __forceinline__ T ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <typename T, bool NT>
+__device__ __forceinline__ void st(T* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int DT, int OP, int NIN, int U, bool NT>
+__global__ __launch_bounds__(kBlock) void k_reduce_tile(void* __restrict__ out_, InPtrs<NIN> ins, int64_t nvec,
+                                                        int64_t n) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  using A = typename E::A;
+  constexpr int W = 16 / sizeof(S);
+  const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+  u32x4* out = reinterpret_cast<u32x4*>(out_);
+  if (base + (int64_t)(U - 1) * kBlock < nvec) {
+    u32x4 r[U][NIN];
+#pragma unroll
+    for (int k = 0; k < NIN; ++k)
+#pragma unroll
+      for (int u = 0; u < U; ++u) r[u][k] = ld<u32x4, NT>(reinterpret_cast<const u32x4*>(ins.p[k]) + base + u * kBlock);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      S a_s[W];
+      __builtin_memcpy(a_s, &r[u][0], 16);
+      A acc[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = E::load(a_s[j]);
+#pragma unroll
+      for (int k = 1; k < NIN; ++k) {
+        S x[W];
+        __builtin_memcpy(x, &r[u][k], 16);
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] = combine<DT, OP>(acc[j], E::load(x[j]));
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j) a_s[j] = E::store(acc[j]);
+      u32x4 o;
+      __builtin_memcpy(&o, a_s, 16);
+      st<u32x4, NT>(out + base + u * kBlock, o);
+    }
+  } else {
+    for (int u = 0; u < U; ++u) {
+      const int64_t v = base + (int64_t)u * kBlock;
+      if (v >= nvec) break;
+      S a_s[W];
+      u32x4 t0 = reinterpret_cast<const u32x4*>(ins.p[0])[v];
+      __builtin_memcpy(a_s, &t0, 16);
+      A acc[W];
+      for (int j = 0; j < W; ++j) acc[j] = E::load(a_s[j]);
+      for (int k = 1; k < NIN; ++k) {
+        S x[W];
+        u32x4 tk = reinterpret_cast<const u32x4*>(ins.p[k])[v];
+        __builtin_memcpy(x, &tk, 16);
+        for (int j = 0; j < W; ++j) acc[j] = combine<DT, OP>(acc[j], E::load(x[j]));
+      }
+      for (int j = 0; j < W; ++j) a_s[j] = E::store(acc[j]);
+      u32x4 o;
+      __builtin_memcpy(&o, a_s, 16);
+      out[v] = o;
+    }
+  }
+  // scalar tail handled by block 0
+  if (blockIdx.x == 0) {
+    const int64_t tb = nvec * W;
+    if ((int64_t)threadIdx.x < n - tb) {
+      const int64_t i = tb + threadIdx.x;
+      A acc = E::load(reinterpret_cast<const S*>(ins.p[0])[i]);
+      for (int k = 1; k < NIN; ++k) acc = combine<DT, OP>(acc, E::load(reinterpret_cast<const S*>(ins.p[k])[i]));
+      reinterpret_cast<S*>(out_)[i] = E::store(acc);
+    }
+  }
+}
+
+static int g_k1_variant = -1;
+static int k1_variant() {
+  if (g_k1_variant < 0) {
+    const char* e = getenv("MP4X_K1_VARIANT");
+    g_k1_variant = e ? atoi(e) : 2;   // default: tile + nontemporal (fastest, tools/bench_kernels.py --variants)
+  }
+  return g_k1_variant;
+}
+
 template <int DT, int OP, int NIN>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(void* __restrict__ out_, InPtrs<NIN> ins, int64_t n) {
   using E = Elem<DT>;
@@ -100,8 +193,21 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
   }
   if (aligned) {
     int64_t nvec = n / W;
-    int g = grid_for(nvec > 0 ? nvec : 1, 2);
-    hipLaunchKernelGGL((k_reduce_vec<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, nvec, n);
+    const int var = k1_variant();
+    if (var == 0) {
+      int g = grid_for(nvec > 0 ? nvec : 1, 2);
+      hipLaunchKernelGGL((k_reduce_vec<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, nvec, n);
+    } else {
+      // U vectors per lane: keep ~4-8 16-B loads in flight per lane
+      constexpr int U = NIN >= 4 ? 1 : (NIN == 1 ? 4 : 2);
+      int64_t per_block = (int64_t)kBlock * U;
+      int64_t g = (nvec + per_block - 1) / per_block;
+      if (g < 1) g = 1;
+      if (var == 1)
+        hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, false>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
+      else
+        hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, true>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
+    }
   } else {
     int g = grid_for(n, 4);
     hipLaunchKernelGGL((k_reduce_scalar<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, n);
@@ -231,6 +337,9 @@ extern "C" int mp4x_scale(int dtype, void* out, const void* in, double scale, in
   }
   return (int)hipGetLastError();
 }
+
+// A/B hook for the kernel-variant sweep (tools/bench_kernels.py --variants).
+extern "C" void mp4x_set_k1_variant(int v) { g_k1_variant = v; }
 
 extern "C" const char* mp4x_version(void) { return "mp4x-native 0.1 gfx950"; }
 

@@ -29,6 +29,14 @@ import numpy as np
 from .operators import DType, NP_DTYPE
 
 
+def _dumps(obj) -> bytes:
+    try:
+        return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+    except (pickle.PicklingError, AttributeError, TypeError):
+        import cloudpickle   # local classes / lambdas (the reference's Kryo handles any class)
+        return cloudpickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+
+
 class Serializer:
     """Host object serializer (reference: Kryo ``Serializer<T>``).
 
@@ -38,7 +46,7 @@ class Serializer:
     """
 
     def write(self, obj: Any) -> bytes:
-        return pickle.dumps(obj, protocol=pickle.HIGHEST_PROTOCOL)
+        return _dumps(obj)
 
     def read(self, data: bytes) -> Any:
         return pickle.loads(data)
@@ -46,7 +54,7 @@ class Serializer:
     # list helpers (one frame per list keeps the wire format simple)
     def write_list(self, objs) -> bytes:
         return pickle.dumps([self.write(o) for o in objs], protocol=pickle.HIGHEST_PROTOCOL) \
-            if type(self) is not Serializer else pickle.dumps(list(objs), protocol=pickle.HIGHEST_PROTOCOL)
+            if type(self) is not Serializer else _dumps(list(objs))
 
     def read_list(self, data: bytes):
         if type(self) is Serializer:

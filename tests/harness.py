@@ -49,12 +49,23 @@ def run_ranks(p, fn, args=(), timeout=120, kind="process", threads=1, master_kwa
     results = {}
     errors = []
     import queue as _q
+    import time as _t
+    deadline = _t.monotonic() + timeout
     try:
-        for _ in range(p):
+        got = 0
+        while got < p and _t.monotonic() < deadline:
             try:
-                r, st, val = q.get(timeout=timeout)
+                r, st, val = q.get(timeout=0.25)
             except _q.Empty:
-                break
+                # a rank that died without reporting (fault injection) ends the wait
+                if any(pr.exitcode not in (None, 0) for pr in procs) and q.empty():
+                    alive = [pr for pr in procs if pr.exitcode is None]
+                    if not alive:
+                        break
+                    if expect_fail and got + len(alive) < p and all(pr.exitcode is not None for pr in procs):
+                        break
+                continue
+            got += 1
             if st == "ok":
                 results[r] = val
             else:

@@ -40,12 +40,30 @@ def main():
     ap.add_argument("--mb", type=int, default=1024, help="per-input size in MiB")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--variants", action="store_true", help="A/B the K1 kernel variants (interleaved rounds)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     n = a.mb * (1 << 20) // 4
     res = {}
     xs = [torch.randn(n, device=dev) for _ in range(8)]
     out = torch.empty_like(xs[0])
+    if a.variants:
+        from mp4x.ops import native
+        lib = native.hip()
+        names = {0: "gridstride_u2", 1: "tile", 2: "tile_nt"}
+        rounds = {}
+        for rnd in range(3):
+            for v in (0, 1, 2):
+                lib.mp4x_set_k1_variant(v)
+                for nin in (1, 2, 4, 8):
+                    ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
+                    rounds.setdefault(f"k1_{names[v]}_nin{nin}", []).append((nin + 1) * n * 4 / ms / 1e6)
+                ms = timeit(lambda: torch.add(xs[0], xs[1], out=out), a.iters)
+                rounds.setdefault("torch_add", []).append(3 * n * 4 / ms / 1e6)
+        for k, v in rounds.items():
+            print(f"{k:28s} GB/s median {sorted(v)[1]:.0f}  all {[round(x) for x in v]}")
+        lib.mp4x_set_k1_variant(2)
+        return
     for nin in ([2, 8] if a.quick else [1, 2, 4, 8]):
         ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
         nbytes = (nin + 1) * n * 4
