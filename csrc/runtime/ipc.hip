@@ -1,0 +1,272 @@
+// Custom xGMI allreduce over IPC-mapped peer buffers (gfx950, one process per GPU).
+//
+// RCCL moves large messages well; for small and medium messages its ring/tree protocol
+// overheads dominate.  These kernels read peer HBM directly through xGMI mappings
+// (hipIpcOpenMemHandle) so every one of the 7 links of an MI355X is used at once:
+//
+//   one-shot : each rank reads all p buffers and reduces in registers (1 hop, p*S read/rank)
+//   two-shot : direct reduce-scatter (rank r reduces chunk r from all p buffers into its own
+//              buffer) + direct all-gather (rank r pulls chunk c from rank c); 2(p-1)/p*S
+//              remote bytes per rank — the bandwidth-optimal full-mesh schedule.
+//
+// Reference analogue: the fused recv+reduce of the ring reduce-scatter
+// (/root/reference/src/main/java/com/fenbi/mp4j/operand/DoubleOperand.java:196) and the
+// small-message RPC allreduce (ProcessCommSlave.java:1776-1926) — here as one kernel.
+//
+// Synchronisation (cdna guide §6 G16, system scope because peers are other GPUs):
+//  * every rank owns a Signal block in fine-grained, UNCACHED memory; flags are epochs
+//    (monotonic per call, never reset) stored by the signalling lane with a relaxed
+//    system-scope atomic store into the PEER's slot, after every wave of the block drained
+//    its stores (s_waitcnt vmcnt(0)) + __syncthreads + a system-scope release fence;
+//  * waiting lanes poll their own slots with relaxed system-scope loads + s_sleep, then a
+//    system-scope acquire;  barriers are per BLOCK: block b of every rank touches exactly
+//    the same element offsets, so block b only has to meet block b of the peers;
+//  * every spin is bounded (s_memrealtime, 100 MHz): on timeout the block records an
+//    error word and exits instead of hanging the GPU;
+//  * data buffers are uncached as well, so remote reads never see stale L2 lines.
+#include <hip/hip_runtime.h>
+
+#include "../kernels/common.hpp"
+
+namespace mp4x {
+
+constexpr int kIpcMaxRanks = 8;
+constexpr int kIpcMaxBlocks = 256;
+constexpr int kIpcThreads = 512;
+
+struct alignas(128) Signal {
+  uint32_t start[kIpcMaxBlocks][kIpcMaxRanks];
+  uint32_t mid[kIpcMaxBlocks][kIpcMaxRanks];
+  uint32_t end[kIpcMaxBlocks][kIpcMaxRanks];
+  uint32_t error;
+};
+
+struct IpcPtrs {
+  const void* data[kIpcMaxRanks];   // every rank's data buffer (own one included)
+  Signal* sig[kIpcMaxRanks];        // every rank's signal block
+};
+
+__device__ __forceinline__ bool block_barrier(uint32_t (*slots)[kIpcMaxRanks] /*Signal::start etc*/,
+                                              const IpcPtrs& P, int which, int rank, int p, uint32_t epoch,
+                                              Signal* self) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its stores
+  __syncthreads();
+  __shared__ int s_fail;
+  if (threadIdx.x == 0) s_fail = 0;
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < p) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    Signal* peer = P.sig[t];
+    uint32_t* slot = which == 0 ? &peer->start[blockIdx.x][rank]
+                   : which == 1 ? &peer->mid[blockIdx.x][rank] : &peer->end[blockIdx.x][rank];
+    __hip_atomic_store(slot, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t* mine = which == 0 ? &self->start[blockIdx.x][t]
+                   : which == 1 ? &self->mid[blockIdx.x][t] : &self->end[blockIdx.x][t];
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {   // 10 s at 100 MHz
+        __hip_atomic_store(&self->error, 1u + (uint32_t)which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_fail = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  }
+  __syncthreads();
+  (void)slots;
+  return s_fail == 0;
+}
+
+// NR (rank count) is a template parameter: the NR remote loads are issued unconditionally
+// and back to back (no per-load branch, cdna guide §5 trap (c)).
+template <int DT, int OP, int NR>
+__device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  using A = typename E::A;
+  constexpr int W = 16 / sizeof(S);
+  u32x4 r[NR];
+#pragma unroll
+  for (int k = 0; k < NR; ++k) r[k] = reinterpret_cast<const u32x4*>(P.data[k])[v];   // NR loads in flight
+  S s[W];
+  __builtin_memcpy(s, &r[0], 16);
+  A acc[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) acc[j] = E::load(s[j]);
+#pragma unroll
+  for (int k = 1; k < NR; ++k) {
+    S x[W];
+    __builtin_memcpy(x, &r[k], 16);
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[j] = combine<DT, OP>(acc[j], E::load(x[j]));
+  }
+#pragma unroll
+  for (int j = 0; j < W; ++j) s[j] = E::store(acc[j]);
+  u32x4 o;
+  __builtin_memcpy(&o, s, 16);
+  return o;
+}
+
+// one-shot: out[v] = op over all ranks' data[v]
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
+                                                              u32x4* __restrict__ out, uint32_t epoch) {
+  constexpr int p = NR;
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
+    out[v] = reduce_vec<DT, OP, NR>(P, v);
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+// two-shot: direct reduce-scatter into own buffer chunk `rank`, then direct all-gather.
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
+                                                              u32x4* __restrict__ out, uint32_t epoch) {
+  constexpr int p = NR;
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int64_t chunk = (nvec + p - 1) / p;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
+  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  {
+    const int64_t b = (int64_t)rank * chunk;
+    const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+    for (int64_t v = b + off0; v < e; v += stride) {
+      u32x4 o = reduce_vec<DT, OP, NR>(P, v);
+      mine[v] = o;
+      out[v] = o;
+    }
+  }
+  if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
+  for (int c = 1; c < p; ++c) {
+    const int src = (rank + c) % p;            // stagger peers so links load evenly
+    const u32x4* pd = reinterpret_cast<const u32x4*>(P.data[src]);
+    const int64_t b = (int64_t)src * chunk;
+    const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+    for (int64_t v = b + off0; v < e; v += stride) out[v] = pd[v];
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+template <int DT, int OP, int NR>
+static int launch_nr(int algo, const IpcPtrs& P, Signal* self, int rank, int64_t nvec, void* out, uint32_t epoch,
+                     int blocks, hipStream_t st) {
+  if (algo == 0)
+    hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
+                       (u32x4*)out, epoch);
+  else
+    hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
+                       (u32x4*)out, epoch);
+  return (int)hipGetLastError();
+}
+
+template <int DT, int OP>
+static int launch_ipc(int algo, const IpcPtrs& P, Signal* self, int rank, int p, int64_t nvec, void* out,
+                      uint32_t epoch, int blocks, hipStream_t st) {
+  switch (p) {
+    case 2: return launch_nr<DT, OP, 2>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 3: return launch_nr<DT, OP, 3>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 4: return launch_nr<DT, OP, 4>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 5: return launch_nr<DT, OP, 5>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 6: return launch_nr<DT, OP, 6>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 7: return launch_nr<DT, OP, 7>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 8: return launch_nr<DT, OP, 8>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    default: return MP4X_E_BADARG;
+  }
+}
+
+// IPC path covers the common gradient / statistic reductions; other (dtype, op) pairs use
+// the RCCL or a2a schedules.
+template <int DT>
+static int ipc_dt(int op, int algo, const IpcPtrs& P, Signal* self, int rank, int p, int64_t nvec, void* out,
+                  uint32_t epoch, int blocks, hipStream_t st) {
+  switch (op) {
+    case MP4X_SUM: return launch_ipc<DT, MP4X_SUM>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_MAX:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return launch_ipc<DT, MP4X_MAX>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+      return MP4X_E_UNSUPPORTED;
+    case MP4X_MIN:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return launch_ipc<DT, MP4X_MIN>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+      return MP4X_E_UNSUPPORTED;
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+}  // namespace mp4x
+
+using namespace mp4x;
+
+extern "C" size_t mp4x_ipc_signal_bytes(void) { return sizeof(Signal); }
+
+// Fine-grained, uncached device allocation (signal blocks and IPC data buffers), zeroed.
+extern "C" int mp4x_ipc_alloc(size_t bytes, void** ptr) {
+  hipError_t e = hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*ptr, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
+extern "C" int mp4x_ipc_free(void* ptr) { return (int)hipFree(ptr); }
+
+extern "C" int mp4x_ipc_handle_size(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+extern "C" int mp4x_ipc_get_handle(void* ptr, void* handle_out) {
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle_out), ptr);
+}
+
+extern "C" int mp4x_ipc_open_handle(const void* handle, void** ptr) {
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, handle, sizeof(h));
+  return (int)hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+extern "C" int mp4x_ipc_close_handle(void* ptr) { return (int)hipIpcCloseMemHandle(ptr); }
+
+extern "C" int mp4x_memcpy_async(void* dst, const void* src, size_t bytes, void* stream) {
+  return (int)hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream);
+}
+
+extern "C" int mp4x_ipc_read_error(void* signal, uint32_t* err) {
+  return (int)hipMemcpy(err, (char*)signal + offsetof(Signal, error), 4, hipMemcpyDeviceToHost);
+}
+
+// algo 0 = one-shot, 1 = two-shot.  data_ptrs / signal_ptrs: p entries (own rank included,
+// peers as mapped by mp4x_ipc_open_handle).  nbytes must be a multiple of 16; the caller has
+// already placed this rank's input in data_ptrs[rank] (stream-ordered before this launch).
+extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
+                                  void* stream) {
+  if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
+  if (((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  IpcPtrs P;
+  for (int k = 0; k < kIpcMaxRanks; ++k) {
+    P.data[k] = k < p ? data_ptrs[k] : nullptr;
+    P.sig[k] = k < p ? (Signal*)signal_ptrs[k] : nullptr;
+    if (k < p && (((uintptr_t)P.data[k] & 15) || !P.sig[k])) return MP4X_E_BADARG;
+  }
+  int64_t nvec = nbytes / 16;
+  if (blocks <= 0) {
+    int64_t b = (nvec + kIpcThreads - 1) / kIpcThreads;
+    blocks = (int)(b < 1 ? 1 : (b > 128 ? 128 : b));
+  }
+  if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+  // element count per 16-byte vector is encoded in the dtype; nvec is the vector count
+  switch (dtype) {
+    case MP4X_F64: return ipc_dt<MP4X_F64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_F32: return ipc_dt<MP4X_F32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_I64: return ipc_dt<MP4X_I64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_I32: return ipc_dt<MP4X_I32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_BF16: return ipc_dt<MP4X_BF16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_F16: return ipc_dt<MP4X_F16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}

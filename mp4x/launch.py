@@ -32,7 +32,8 @@ def init_from_env(thread_num: int = 0, heartbeat: bool = True, timeout: float = 
     host = "127.0.0.1" if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost") \
         else os.environ["MASTER_ADDR"]
     if world == 1:
-        _embedded = CommMaster(1, 0, host=host, exit_on_timeout=False).start()
+        _embedded = CommMaster(1, 0, host=host, exit_on_timeout=False,
+                               heartbeat_timeout=None if heartbeat else float("inf")).start()
         mhost, mport = host, _embedded.port
     else:
         import torch.distributed as dist
@@ -41,7 +42,8 @@ def init_from_env(thread_num: int = 0, heartbeat: bool = True, timeout: float = 
         if rank == 0:
             os.environ["MP4X_EMBEDDED_MASTER"] = "1"
             bind = "127.0.0.1" if host == "127.0.0.1" else "0.0.0.0"
-            _embedded = CommMaster(world, 0, host=bind, exit_on_timeout=True).start()
+            _embedded = CommMaster(world, 0, host=bind, exit_on_timeout=True,
+                                   heartbeat_timeout=None if heartbeat else float("inf")).start()
             store.set(key, f"{host}:{_embedded.port}")
         addr = store.get(key).decode()
         mhost, mport = addr.rsplit(":", 1)

@@ -116,6 +116,11 @@ class DeviceEngine:
             self._init_pg()
         self.algo = _env_algo()
         self.a2a_bytes = int(os.environ.get("MP4X_A2A_MIN_BYTES", 0))
+        # custom xGMI IPC allreduce (csrc/runtime/ipc.hip) below these sizes
+        self.ipc_enabled = os.environ.get("MP4X_IPC", "1") == "1" and self.device.type == "cuda" and 2 <= self.p <= 8
+        self.ipc_oneshot_max = int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))
+        self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
+        self._ipc_obj = None
 
     # ------------------------------------------------------------------ bootstrap
     def _init_pg(self):
@@ -140,6 +145,12 @@ class DeviceEngine:
         LOG.info("rank %d: device communicator up (%s, %s)", self.rank, self.backend, self.device)
 
     def shutdown(self):
+        if self._ipc_obj is not None:
+            try:
+                self._ipc_obj.close()
+            except Exception:
+                pass
+            self._ipc_obj = None
         if self._owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()
@@ -169,17 +180,46 @@ class DeviceEngine:
             return op.code in _RCCL_OPS and dtype not in (torch.bfloat16, torch.float16, torch.int16)
         return op.code in _RCCL_OPS and dtype in _RCCL_DTYPES
 
+    def ipc(self):
+        """Lazily set up the IPC peer mappings (collective: every rank reaches this together)."""
+        if self._ipc_obj is None and self.ipc_enabled:
+            try:
+                from .ipc import IpcAllreduce
+                self._ipc_obj = IpcAllreduce(self.comm)
+            except Exception as e:
+                LOG.warning("IPC allreduce disabled: %s", e)
+                self.ipc_enabled = False
+        return self._ipc_obj
+
+    def _ipc_ok(self, op, dtype, nbytes) -> bool:
+        if not self.ipc_enabled or nbytes % 16 or getattr(op, "is_custom", False):
+            return False
+        from .ipc import SUPPORTED_DTYPES
+        if dtype not in SUPPORTED_DTYPES:
+            return False
+        if op.code == OpCode.SUM:
+            return True
+        return op.code in (OpCode.MAX, OpCode.MIN) and dtype in (torch.float32, torch.bfloat16, torch.float16)
+
     def select(self, kind: str, nbytes: int, op, dtype, operand=None) -> str:
+        """Per-call algorithm choice (size tiers, dtype/op support, MP4X_DEVICE_ALGO override)."""
         forced = self.algo
         codec = getattr(operand, "codec", None) if operand is not None else None
         if codec == "fp8" and kind in ("allreduce", "reduce_scatter") and \
                 dtype in (torch.float32, torch.bfloat16, torch.float16) and op is not None and \
                 not getattr(op, "is_custom", False) and op.code == OpCode.SUM and self.device.type == "cuda":
             return "fp8"
+        if forced in ("ipc1", "ipc2") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
+            return forced
         if op is not None and not self.rccl_ok(op, dtype):
             return "a2a"
         if forced in ("rccl", "a2a"):
             return forced
+        if kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
+            if nbytes <= self.ipc_oneshot_max:
+                return "ipc1"
+            if nbytes <= self.ipc_twoshot_max:
+                return "ipc2"
         if self.a2a_bytes and nbytes >= self.a2a_bytes:
             return "a2a"
         return "rccl"
@@ -199,8 +239,13 @@ class DeviceEngine:
         op = self._op(operator, view)
         algo = self.select("allreduce", view.numel() * view.element_size(), op, view.dtype, operand)
         self._count("allreduce." + algo)
+        if algo in ("ipc1", "ipc2") and self.ipc() is None:
+            algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
             dist.all_reduce(view, op=_RCCL_OPS[op.code], group=self.pg)
+        elif algo in ("ipc1", "ipc2"):
+            from .ipc import ONESHOT, TWOSHOT
+            self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT)
         elif algo == "fp8":
             self._allreduce_fp8(view)
         else:

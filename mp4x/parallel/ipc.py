@@ -1,0 +1,145 @@
+"""Host side of the custom xGMI allreduce (csrc/runtime/ipc.hip).
+
+Each rank allocates one fine-grained uncached data buffer (``MP4X_IPC_BYTES``, default
+64 MiB) plus a signal block, exports both with ``hipIpcGetMemHandle``, exchanges the handles
+through the master (``allgather_obj``) and maps every peer's pair with
+``hipIpcOpenMemHandle``.  A call copies the input into the own data buffer (stream ordered)
+and launches ONE kernel that synchronises with the peers' kernels through epoch flags and
+reduces straight out of peer HBM.  Messages larger than the buffer are processed in
+buffer-sized pieces.
+
+Only needs the mp4x control plane (no RCCL communicator), so it also runs with several
+processes sharing one GPU — which is how it is tested on a single-GPU box.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional
+
+import torch
+
+from ..exceptions import Mp4jException
+from ..operators import OpCode, dtype_of_torch
+from ..ops import native
+from ..ops.native import check, ptr_array, stream_ptr, c_int, c_int64, c_void_p, c_size_t, PP
+
+native.register_signatures({
+    "mp4x_ipc_signal_bytes": (c_size_t, []),
+    "mp4x_ipc_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
+    "mp4x_ipc_free": (c_int, [c_void_p]),
+    "mp4x_ipc_handle_size": (c_int, []),
+    "mp4x_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
+    "mp4x_ipc_open_handle": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "mp4x_ipc_close_handle": (c_int, [c_void_p]),
+    "mp4x_ipc_read_error": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
+                                   c_int, c_void_p]),
+})
+
+ONESHOT, TWOSHOT = 0, 1
+SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64}
+
+
+class IpcAllreduce:
+    def __init__(self, comm, nbytes: Optional[int] = None, tag: str = "default"):
+        self.comm = comm
+        self.rank = comm.rank
+        self.p = comm.slaveNum
+        if not (2 <= self.p <= 8):
+            raise Mp4jException("IPC allreduce supports 2..8 ranks")
+        self.lib = native.hip()
+        self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
+        self.nbytes = (self.nbytes + 4095) // 4096 * 4096
+        self.device = torch.cuda.current_device()
+        hs = self.lib.mp4x_ipc_handle_size()
+        self._data = c_void_p()
+        self._sig = c_void_p()
+        check(self.lib.mp4x_ipc_alloc(self.nbytes, ctypes.byref(self._data)), "ipc_alloc(data)")
+        check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)), "ipc_alloc(sig)")
+        hd = ctypes.create_string_buffer(hs)
+        hsg = ctypes.create_string_buffer(hs)
+        check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
+        check(self.lib.mp4x_ipc_get_handle(self._sig, hsg), "ipc_get_handle(sig)")
+        allh = comm.server.call("allgather_obj", self.rank, hd.raw + hsg.raw)
+        self.data_ptrs: List[int] = []
+        self.sig_ptrs: List[int] = []
+        self._opened: List[c_void_p] = []
+        err = None
+        try:
+            for r, blob in enumerate(allh):
+                if r == self.rank:
+                    self.data_ptrs.append(self._data.value)
+                    self.sig_ptrs.append(self._sig.value)
+                    continue
+                for i, lst in ((0, self.data_ptrs), (1, self.sig_ptrs)):
+                    h = ctypes.create_string_buffer(bytes(blob[i * hs:(i + 1) * hs]), hs)
+                    ptr = c_void_p()
+                    check(self.lib.mp4x_ipc_open_handle(h, ctypes.byref(ptr)), f"ipc_open_handle(rank {r})")
+                    self._opened.append(ptr)
+                    lst.append(ptr.value)
+        except Exception as e:   # decide collectively: every rank enables IPC or none does
+            err = str(e)
+        oks = comm.server.call("allgather_obj", self.rank, b"" if err is None else err.encode())
+        if any(oks):
+            self.close(sync=False)
+            bad = [(i, bytes(o).decode()) for i, o in enumerate(oks) if o]
+            raise Mp4jException(f"IPC peer mapping failed on ranks {bad}")
+        self._pp_data = ptr_array(self.data_ptrs)
+        self._pp_sig = ptr_array(self.sig_ptrs)
+        self.epoch = 0
+        # all ranks mapped before anyone launches
+        comm.server.call("barrier", self.rank)
+
+    def supports(self, t: torch.Tensor, op) -> bool:
+        if getattr(op, "is_custom", False) or t.dtype not in SUPPORTED_DTYPES:
+            return False
+        if op.code == OpCode.SUM:
+            return True
+        return op.code in (OpCode.MAX, OpCode.MIN) and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
+
+    def allreduce(self, view: torch.Tensor, op, algo: int = ONESHOT, out: Optional[torch.Tensor] = None,
+                  blocks: int = 0) -> torch.Tensor:
+        """In place (or into ``out``) allreduce of a contiguous device tensor."""
+        if out is None:
+            out = view
+        if not view.is_contiguous() or not out.is_contiguous():
+            raise Mp4jException("IPC allreduce needs contiguous tensors")
+        es = view.element_size()
+        total = view.numel() * es
+        if total % 16 or out.data_ptr() % 16:
+            raise Mp4jException("IPC allreduce needs 16-byte multiples")
+        dt = int(dtype_of_torch(view.dtype))
+        src = view.view(torch.uint8)
+        dst = out.view(torch.uint8)
+        piece = self.nbytes - self.nbytes % 16
+        off = 0
+        st = stream_ptr()
+        while off < total:
+            m = min(piece, total - off)
+            check(self.lib.mp4x_memcpy_async(self._data.value, src.data_ptr() + off, m, st), "ipc input copy")
+            self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+            check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0], self.rank,
+                                              self.p, m, dst.data_ptr() + off, self.epoch, blocks, st),
+                  "mp4x_ipc_allreduce")
+            off += m
+        return out
+
+    def error_word(self) -> int:
+        v = ctypes.c_uint32(0)
+        check(self.lib.mp4x_ipc_read_error(self._sig, ctypes.byref(v)), "ipc_read_error")
+        return int(v.value)
+
+    def close(self, sync: bool = True):
+        if sync:
+            torch.cuda.synchronize()
+        for ptr in self._opened:
+            self.lib.mp4x_ipc_close_handle(ptr)
+        self._opened = []
+        if self._data:
+            self.lib.mp4x_ipc_free(self._data)
+            self._data = c_void_p()
+        if self._sig:
+            self.lib.mp4x_ipc_free(self._sig)
+            self._sig = c_void_p()

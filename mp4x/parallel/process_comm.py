@@ -476,19 +476,40 @@ class ProcessCommSlave:
         return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._UNION)
 
     def allreduceSetUnion(self, setData, elementSerializer=None, elementType=None):
+        if _is_torch(setData):   # int64 id tensor → GPU K7 path
+            from .sparse import set_union
+            return setData if self.slaveNum == 1 else set_union(self.device, setData)
         return self.allreduceMapSetUnion({"key": setData}, elementSerializer, elementType).get("key")
 
     def allreduceMapSetIntersection(self, mapData: Dict, elementSerializer=None, elementType=None) -> Dict:
         return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._INTERSECT)
 
     def allreduceSetIntersection(self, setData, elementSerializer=None, elementType=None):
+        if _is_torch(setData):
+            from .sparse import set_intersection
+            return setData if self.slaveNum == 1 else set_intersection(self.device, setData)
         return self.allreduceMapSetIntersection({"key": setData}, elementSerializer, elementType).get("key")
 
     def allreduceMapListConcat(self, mapData: Dict, elementSerializer=None, elementType=None) -> Dict:
         return self.allreduceMap(mapData, self._set_operand(elementSerializer), self._CONCAT)
 
     def allreduceListConcat(self, listData, elementSerializer=None, elementType=None):
+        if _is_torch(listData):
+            from .sparse import list_concat
+            return listData if self.slaveNum == 1 else list_concat(self.device, listData)
         return self.allreduceMapListConcat({"key": listData}, elementSerializer, elementType).get("key")
+
+    def allreduceSparse(self, keys, vals, operator):
+        """Sparse allreduce of (int64 id, value-row) pairs on the device engine (extension).
+
+        Every rank returns ``(keys, vals)`` holding the op-reduction over all ranks of the rows
+        sharing an id (the tensor form of ``allreduceMap`` for ``Map<String, float[]>``).
+        """
+        self._tick("allreduceSparse")
+        if self.slaveNum == 1:
+            return keys, vals
+        from .sparse import allreduce_sparse
+        return allreduce_sparse(self.device, keys, vals, operator)
 
     # ================================================================ allreduce
     def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, out=None):
@@ -500,7 +521,13 @@ class ProcessCommSlave:
         self._tick("allreduceArray")
         if out is not None:
             CommUtils.isFromToLegal(frm, to)
-            if _is_torch(out):
+            if _is_device_tensor(out):
+                # the local data movement of an out-of-place allreduce runs through the K1 kernel
+                from ..ops.device_ops import reduce_
+                from ..operators import OpCode
+                if to > frm:
+                    reduce_(out.view(-1)[frm:to], [arrData.view(-1)[frm:to]], int(OpCode.SUM))
+            elif _is_torch(out):
                 out.view(-1)[frm:to].copy_(arrData.view(-1)[frm:to])
             else:
                 out[frm:to] = arrData[frm:to]
@@ -573,7 +600,7 @@ class ProcessCommSlave:
         self._tick("allreduceMap")
         if self.slaveNum == 1:
             return mapData
-        if mapData and _is_device_tensor(next(iter(mapData.values()))):
+        if mapData and _is_torch(next(iter(mapData.values()))):
             return self.device.allreduce_map(mapData, operator)
         mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)
         allb = self.engine.ring_allgather_maps(mine, operand)

@@ -1,0 +1,227 @@
+"""Sparse ``Map<String, T>`` collectives on the GPU (BASELINE config 4).
+
+Reference semantics: ``allreduceMap`` = hash partition → ring reduce-scatter of per-owner
+maps → ring allgather → merge (ProcessCommSlave.java:2053-2088); set/list specials on top
+(ProcessCommSlave.java:1583-1720, 2099-2230).
+
+Device design (one process per GPU):
+
+* string keys become stable 64-bit ids (xxh64, :mod:`mp4x.utils.hashing`); a per-communicator
+  :class:`KeyDictionary` maps ids back to strings.  Only keys a rank has never seen before
+  are exchanged (host allgather), so a steady-state embedding / histogram sync moves no
+  strings at all;
+* values live in one ``[n, dim]`` device tensor (``Map<String, float[]>`` rows);
+* owner of a key = ``id % p`` (kernel K4: owner + LDS histogram), rows are sorted by owner
+  with a stable hipCUB radix sort and exchanged with ONE ragged all-to-all over RCCL
+  (every link busy at once, no ring);
+* each owner reduces its rows with the deterministic reduce-by-key kernel K5 (stable sort
+  by id, one wave per key, rows combined in source-rank order);
+* owned results are all-gathered; ownership is disjoint, so the union needs no merge.
+
+The tensor-level entry points (``allreduce_sparse``, ``set_union``, ``set_intersection``)
+take int64 id tensors directly and are what a training loop should call.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..operators import OpCode, dtype_of_torch, for_dtype
+from ..utils.hashing import key_id
+
+
+class KeyDictionary:
+    """id <-> string dictionary shared (incrementally) by all ranks of a communicator."""
+
+    def __init__(self):
+        self.id2key: Dict[int, str] = {}
+        self.key2id: Dict[str, int] = {}
+
+    def ids_for(self, keys) -> Tuple[List[int], Dict[str, int]]:
+        ids = []
+        new = {}
+        for k in keys:
+            i = self.key2id.get(k)
+            if i is None:
+                i = key_id(k)
+                self.key2id[k] = i
+                other = self.id2key.get(i)
+                if other is not None and other != k:
+                    raise RuntimeError(f"64-bit key id collision: {k!r} vs {other!r}")
+                self.id2key[i] = k
+                new[k] = i
+            ids.append(i)
+        return ids, new
+
+    def learn(self, pairs: Dict[str, int]) -> None:
+        for k, i in pairs.items():
+            other = self.id2key.get(i)
+            if other is not None and other != k:
+                raise RuntimeError(f"64-bit key id collision: {k!r} vs {other!r}")
+            self.id2key[i] = k
+            self.key2id[k] = i
+
+
+def _dictionary(engine) -> KeyDictionary:
+    d = getattr(engine, "_keydict", None)
+    if d is None:
+        d = engine._keydict = KeyDictionary()
+    return d
+
+
+def _sync_new_keys(engine, new: Dict[str, int]) -> None:
+    """Host allgather of the (string, id) pairs some rank has not published yet."""
+    from ..operands import Operands
+    comm = engine.comm
+    blocks = comm.engine.ring_allgather_maps([new], Operands.LONG_OPERAND())
+    d = _dictionary(engine)
+    for r, blk in enumerate(blocks):
+        if r != comm.rank:
+            for m in blk:
+                d.learn(m)
+
+
+# ------------------------------------------------------------------ local kernels (GPU) / CPU twins
+def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op):
+    if keys.is_cuda:
+        from ..ops.device_ops import reduce_by_key
+        return reduce_by_key(keys, vals, int(op.code) if vals is not None else 0)
+    # CPU twin for the gloo test configuration only
+    uk, inv, cnt = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)
+    if vals is None:
+        return uk, None, cnt.to(torch.int32)
+    order = torch.argsort(inv, stable=True)
+    out = torch.empty((uk.numel(),) + tuple(vals.shape[1:]), dtype=vals.dtype)
+    vnp = vals.numpy()
+    inv_np = inv.numpy()
+    onp = out.numpy()
+    seen = np.zeros(uk.numel(), dtype=bool)
+    for j in order.numpy():
+        u = inv_np[j]
+        if not seen[u]:
+            onp[u] = vnp[j]
+            seen[u] = True
+        else:
+            row = np.array(onp[u], copy=True)
+            op.reduce_into(row.reshape(-1), vnp[j].reshape(-1))
+            onp[u] = row
+    return uk, out, cnt.to(torch.int32)
+
+
+def _owner_order(keys: torch.Tensor, p: int):
+    """(perm sorting rows by owner, per-owner counts) — kernels K4 + stable radix sort."""
+    if keys.is_cuda:
+        from ..ops.device_ops import key_owner, sort_pairs
+        dest, hist = key_owner(keys, p)
+        bits = max(1, int(p - 1).bit_length())
+        _, perm = sort_pairs(dest, end_bit=bits)
+        return perm, hist.to(torch.int64)
+    dest = torch.remainder(keys, p)
+    perm = torch.argsort(dest, stable=True)
+    return perm, torch.bincount(dest, minlength=p)
+
+
+def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    if x.is_cuda:
+        from ..ops.device_ops import gather_rows
+        return gather_rows(x.contiguous(), idx)
+    return x[idx]
+
+
+# ------------------------------------------------------------------ tensor-level API
+def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor]):
+    p = engine.p
+    perm, hist = _owner_order(keys, p)
+    skeys = _gather_rows(keys.view(-1, 1), perm).view(-1)
+    svals = _gather_rows(vals, perm) if vals is not None else None
+    recv_counts = torch.empty_like(hist)
+    dist.all_to_all_single(recv_counts, hist, group=engine.pg)
+    send = hist.tolist()
+    recv = recv_counts.tolist()
+    rkeys = torch.empty(sum(recv), dtype=keys.dtype, device=keys.device)
+    dist.all_to_all_single(rkeys, skeys, recv, send, group=engine.pg)
+    rvals = None
+    if vals is not None:
+        rvals = torch.empty((sum(recv),) + tuple(vals.shape[1:]), dtype=vals.dtype, device=vals.device)
+        dist.all_to_all_single(rvals, svals, recv, send, group=engine.pg)
+    return rkeys, rvals
+
+
+def _allgather_v(engine, t: torch.Tensor) -> torch.Tensor:
+    p = engine.p
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.empty_like(n) for _ in range(p)]
+    dist.all_gather(ns, n, group=engine.pg)
+    sizes = [int(x.item()) for x in ns]
+    m = max(sizes) if sizes else 0
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    if t.shape[0]:
+        pad[:t.shape[0]] = t
+    outs = [torch.empty_like(pad) for _ in range(p)]
+    dist.all_gather(outs, pad, group=engine.pg)
+    return torch.cat([o[:s] for o, s in zip(outs, sizes)], 0)
+
+
+def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator):
+    """All ranks end with the op-reduction of every rank's (key, row) pairs, keys ascending per owner.
+
+    ``keys`` int64 [n] (unique per rank), ``vals`` [n, dim] (or [n]).
+    """
+    squeeze = vals.dim() == 1
+    v2 = vals.view(-1, 1) if squeeze else vals
+    op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
+    rkeys, rvals = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op)
+    all_k = _allgather_v(engine, uk)
+    all_v = _allgather_v(engine, uv)
+    return all_k, (all_v.view(-1) if squeeze else all_v)
+
+
+def _set_counts(engine, ids: torch.Tensor):
+    ids = torch.unique(ids) if not ids.is_cuda else _reduce_by_key(ids, None, None)[0]
+    rkeys, _ = _exchange_by_owner(engine, ids, None)
+    return _reduce_by_key(rkeys, None, None)
+
+
+def set_union(engine, ids: torch.Tensor) -> torch.Tensor:
+    """K7 union of int64 id sets across ranks."""
+    uk, _, _ = _set_counts(engine, ids)
+    return _allgather_v(engine, uk)
+
+
+def set_intersection(engine, ids: torch.Tensor) -> torch.Tensor:
+    """K7 intersection: ids present on all p ranks (count == p after de-duplication)."""
+    uk, _, cnt = _set_counts(engine, ids)
+    return _allgather_v(engine, uk[cnt == engine.p])
+
+
+def list_concat(engine, ids: torch.Tensor) -> torch.Tensor:
+    """K7 concat = allgather-v in rank order."""
+    return _allgather_v(engine, ids)
+
+
+# ------------------------------------------------------------------ Map API
+def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
+    """``allreduceMap`` for ``Dict[str, torch.Tensor]`` values on the GPU."""
+    d = _dictionary(engine)
+    keys = list(mapData.keys())
+    ids, new = d.ids_for(keys)
+    _sync_new_keys(engine, new)
+    vals = list(mapData.values())
+    dev = vals[0].device if vals else engine.device
+    if vals:
+        v = torch.stack([x.reshape(-1) for x in vals])
+        shape = tuple(vals[0].shape)
+    else:
+        v = torch.empty((0, 1), device=dev)
+        shape = (1,)
+    k = torch.tensor(ids, dtype=torch.int64, device=dev)
+    rk, rv = allreduce_sparse(engine, k, v, operator)
+    out = {}
+    rk_l = rk.tolist()
+    for i, kid in enumerate(rk_l):
+        out[d.id2key[kid]] = rv[i].view(shape)
+    return out

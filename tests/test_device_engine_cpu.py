@@ -94,3 +94,33 @@ def test_device_engine_gloo(p, algo):
     assert st.get("allreduce.a2a", 0) >= 2      # bitwise + int16 always take the a2a schedule
     if algo == "rccl":
         assert st.get("allreduce.rccl", 0) >= 1
+
+
+def sparse_engine(comm):
+    p, r = comm.getSlaveNum(), comm.getRank()
+    # ids 0..29 shared, plus one unique id per rank; dim-3 float rows
+    ids = torch.tensor(list(range(30)) + [1000 + r], dtype=torch.int64)
+    vals = torch.ones(31, 3) * (r + 1)
+    k, v = comm.allreduceSparse(ids, vals, Operators.Float.SUM)
+    got = dict(zip(k.tolist(), v.tolist()))
+    assert len(got) == 30 + p
+    assert got[0] == [p * (p + 1) / 2] * 3 and got[1000 + r] == [r + 1.0] * 3
+    u = comm.allreduceSetUnion(torch.tensor([r, 100, 100], dtype=torch.int64))
+    assert sorted(u.tolist()) == sorted(set(range(p)) | {100})
+    i = comm.allreduceSetIntersection(torch.tensor([5, 6, 50 + r], dtype=torch.int64))
+    assert sorted(i.tolist()) == [5, 6]
+    c = comm.allreduceListConcat(torch.tensor([r, r], dtype=torch.int64))
+    assert c.tolist() == sum([[j, j] for j in range(p)], [])
+    # Map<String, float[]> with tensor values -> device map path
+    m = {f"feat{j}": torch.full((4,), float(r + 1)) for j in range(12)}
+    m[f"only{r}"] = torch.ones(4)
+    out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.SUM)
+    assert len(out) == 12 + p and torch.all(out["feat3"] == p * (p + 1) / 2) and torch.all(out[f"only{r}"] == 1)
+    out2 = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.MAX)   # keys known now: no string sync
+    assert torch.all(out2["feat0"] == p)
+    return "ok"
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_sparse_engine_gloo(p):
+    run_ranks(p, sparse_engine, timeout=120)

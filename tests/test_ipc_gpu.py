@@ -1,0 +1,97 @@
+"""Custom IPC allreduce (csrc/runtime/ipc.hip): p processes sharing ONE GPU.
+
+On a single-GPU box the peers' buffers are IPC mappings of memory on the same device, which
+exercises the whole protocol (handle exchange, epoch flags, per-block barriers, one-shot and
+two-shot schedules, piecewise large messages) except the xGMI hop itself.
+"""
+import multiprocessing as mp
+import os
+import tempfile
+import traceback
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _ipc_worker(port, q, sizes, dtype_name, algos, nbytes_buf):
+    try:
+        import torch
+        from mp4x import ProcessCommSlave, Operators
+        from mp4x.parallel.ipc import IpcAllreduce, ONESHOT, TWOSHOT
+        torch.cuda.set_device(0)
+        comm = ProcessCommSlave("t", "127.0.0.1", port, heartbeat=False)
+        r, p = comm.getRank(), comm.getSlaveNum()
+        dt = getattr(torch, dtype_name)
+        ipc = IpcAllreduce(comm, nbytes=nbytes_buf)
+        res = []
+        for n in sizes:
+            for algo in algos:
+                for op in ("SUM", "MAX"):
+                    g = torch.Generator(device="cuda").manual_seed(1000 + r)
+                    x = torch.randn(n, device="cuda", generator=g).to(dt)
+                    out = torch.empty_like(x)
+                    operator = getattr(Operators.Float, op)
+                    ipc.allreduce(x, operator, algo=algo, out=out)
+                    torch.cuda.synchronize()
+                    # reference: regenerate every rank's input locally
+                    xs = [torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(1000 + j)).to(dt)
+                          for j in range(p)]
+                    if op == "SUM":
+                        ref = xs[0].double()
+                        for j in range(1, p):
+                            ref = ref + xs[j].double()
+                    else:
+                        ref = xs[0].double()
+                        for j in range(1, p):
+                            ref = torch.maximum(ref, xs[j].double())
+                    err = (out.double() - ref).abs().max().item() if n else 0.0
+                    res.append((n, algo, op, err, ipc.error_word()))
+        comm.barrier()
+        ipc.close()
+        comm.close(0)
+        q.put((r, "ok", res))
+    except BaseException:
+        q.put((-1, "err", traceback.format_exc()))
+
+
+def _run(p, sizes, dtype_name="float32", algos=(0, 1), nbytes_buf=1 << 20):
+    from mp4x import CommMaster
+    m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ipc_worker, args=(m.port, q, sizes, dtype_name, algos, nbytes_buf)) for _ in range(p)]
+    for pr in procs:
+        pr.start()
+    out = {}
+    try:
+        for _ in range(p):
+            r, st, val = q.get(timeout=240)
+            assert st == "ok", val
+            out[r] = val
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+        m.stop(timeout=5)
+    return out
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_ipc_allreduce_f32(p):
+    # 64 elems (one vector per thread at most), ragged sizes, and > buffer (piecewise)
+    out = _run(p, [64, 4 * 1000, 3 * (1 << 18) + 4096])
+    for r, res in out.items():
+        for n, algo, op, err, ew in res:
+            assert ew == 0, f"rank {r}: barrier timeout flag {ew}"
+            assert err < 1e-4 * p, (r, n, algo, op, err)
+
+
+def test_ipc_allreduce_bf16():
+    out = _run(2, [8 * 4096], dtype_name="bfloat16")
+    for r, res in out.items():
+        for n, algo, op, err, ew in res:
+            assert ew == 0 and err < 0.05, (n, algo, op, err)
