@@ -23,7 +23,7 @@ def worker(port, q, sizes, iters):
     from mp4x.parallel.ipc import IpcAllreduce
     torch.cuda.set_device(0)
     comm = ProcessCommSlave("b", "127.0.0.1", port, heartbeat=False)
-    ipc = IpcAllreduce(comm, nbytes=64 << 20)
+    ipc = IpcAllreduce(comm, nbytes=64 << 20).prepare_graph()
     out = []
     for nbytes in sizes:
         x = torch.randn(nbytes // 4, device="cuda")
@@ -40,8 +40,23 @@ def worker(port, q, sizes, iters):
                 e[i].record()
             torch.cuda.synchronize()
             ts = sorted(a.elapsed_time(b) for a, b in zip(s, e))
+            # same call captured in a hipGraph (launch overhead removed)
+            gs = torch.cuda.Stream()
+            gs.wait_stream(torch.cuda.current_stream())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=gs):
+                ipc.allreduce(x, Operators.Float.SUM, algo=algo)
+            torch.cuda.synchronize()
+            comm.barrier()
+            for i in range(iters):
+                s[i].record()
+                g.replay()
+                e[i].record()
+            torch.cuda.synchronize()
+            tg = sorted(a.elapsed_time(b) for a, b in zip(s, e))
             out.append({"bytes": nbytes, "algo": ["oneshot", "twoshot"][algo], "p50_us": ts[len(ts) // 2] * 1e3,
-                        "p99_us": ts[min(len(ts) - 1, int(0.99 * len(ts)))] * 1e3, "err": ipc.error_word()})
+                        "p99_us": ts[min(len(ts) - 1, int(0.99 * len(ts)))] * 1e3,
+                        "graph_p50_us": tg[len(tg) // 2] * 1e3, "err": ipc.error_word()})
             comm.barrier()
     ipc.close()
     comm.close(0)

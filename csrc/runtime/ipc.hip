@@ -111,10 +111,23 @@ __device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v) {
 }
 
 // one-shot: out[v] = op over all ranks' data[v]
+__device__ __forceinline__ uint32_t resolve_epoch(uint32_t epoch, const uint32_t* epoch_dev) {
+  // graph mode: the epoch lives in device memory and is bumped by k_ipc_bump_epoch, the
+  // preceding node of the same graph, so every replay gets a fresh, rank-consistent epoch
+  return epoch_dev ? __hip_atomic_load(epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epoch;
+}
+
+__global__ void k_ipc_bump_epoch(uint32_t* epoch_dev) {
+  uint32_t e = *epoch_dev + 1;
+  *epoch_dev = e ? e : 1;
+}
+
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
-                                                              u32x4* __restrict__ out, uint32_t epoch) {
+                                                              u32x4* __restrict__ out, uint32_t epoch,
+                                                              const uint32_t* epoch_dev) {
   constexpr int p = NR;
+  epoch = resolve_epoch(epoch, epoch_dev);
   if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
   for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
@@ -125,8 +138,10 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* 
 // two-shot: direct reduce-scatter into own buffer chunk `rank`, then direct all-gather.
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
-                                                              u32x4* __restrict__ out, uint32_t epoch) {
+                                                              u32x4* __restrict__ out, uint32_t epoch,
+                                                              const uint32_t* epoch_dev) {
   constexpr int p = NR;
+  epoch = resolve_epoch(epoch, epoch_dev);
   if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t chunk = (nvec + p - 1) / p;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
@@ -152,15 +167,19 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
 }
 
+// set per call by mp4x_ipc_allreduce (host-side, single-threaded use per communicator)
+static thread_local const uint32_t* g_epoch_dev = nullptr;
+
 template <int DT, int OP, int NR>
 static int launch_nr(int algo, const IpcPtrs& P, Signal* self, int rank, int64_t nvec, void* out, uint32_t epoch,
                      int blocks, hipStream_t st) {
+  const uint32_t* edev = g_epoch_dev;
   if (algo == 0)
     hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch);
+                       (u32x4*)out, epoch, edev);
   else
     hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch);
+                       (u32x4*)out, epoch, edev);
   return (int)hipGetLastError();
 }
 
@@ -240,9 +259,17 @@ extern "C" int mp4x_ipc_read_error(void* signal, uint32_t* err) {
 // algo 0 = one-shot, 1 = two-shot.  data_ptrs / signal_ptrs: p entries (own rank included,
 // peers as mapped by mp4x_ipc_open_handle).  nbytes must be a multiple of 16; the caller has
 // already placed this rank's input in data_ptrs[rank] (stream-ordered before this launch).
+extern "C" int mp4x_ipc_bump_epoch(uint32_t* epoch_dev, void* stream) {
+  hipLaunchKernelGGL(k_ipc_bump_epoch, dim3(1), dim3(1), 0, (hipStream_t)stream, epoch_dev);
+  return (int)hipGetLastError();
+}
+
+// epoch_dev == NULL: `epoch` (host counter) is used.  epoch_dev != NULL: graph-capturable form,
+// the kernel reads the epoch from device memory (bump it with mp4x_ipc_bump_epoch first).
 extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                   int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
-                                  void* stream) {
+                                  const uint32_t* epoch_dev, void* stream) {
+  g_epoch_dev = epoch_dev;
   if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
   if (((uintptr_t)out & 15)) return MP4X_E_BADARG;
   IpcPtrs P;

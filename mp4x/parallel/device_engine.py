@@ -324,8 +324,7 @@ class DeviceEngine:
         padded[:n].copy_(view)
         q = torch.empty(p * c, dtype=torch.uint8, device=dev)
         s = torch.empty(p * nblk, dtype=torch.float32, device=dev)
-        for j in range(p):
-            K.quant_fp8(padded[j * c:(j + 1) * c], q[j * c:(j + 1) * c], s[j * nblk:(j + 1) * nblk])
+        K.quant_fp8(padded, q, s)     # one launch: chunks are whole quant blocks, so scales never straddle
         rq = torch.empty_like(q)
         rs = torch.empty_like(s)
         dist.all_to_all_single(rq, q, group=self.pg)

@@ -35,7 +35,8 @@ native.register_signatures({
     "mp4x_ipc_read_error": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
-                                   c_int, c_void_p]),
+                                   c_int, c_void_p, c_void_p]),
+    "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
 })
 
 ONESHOT, TWOSHOT = 0, 1
@@ -89,6 +90,7 @@ class IpcAllreduce:
         self._pp_data = ptr_array(self.data_ptrs)
         self._pp_sig = ptr_array(self.sig_ptrs)
         self.epoch = 0
+        self._epoch_dev = None     # device epoch counter for graph-captured calls (lazy)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -116,15 +118,32 @@ class IpcAllreduce:
         piece = self.nbytes - self.nbytes % 16
         off = 0
         st = stream_ptr()
+        # once prepare_graph() ran, EVERY call (eager or captured) takes its epoch from the device
+        # counter, so eager calls and graph replays can interleave without reusing an epoch
+        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+            raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
         while off < total:
             m = min(piece, total - off)
             check(self.lib.mp4x_memcpy_async(self._data.value, src.data_ptr() + off, m, st), "ipc input copy")
-            self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+            if edev is not None:
+                check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
+            else:
+                self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
             check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0], self.rank,
-                                              self.p, m, dst.data_ptr() + off, self.epoch, blocks, st),
+                                              self.p, m, dst.data_ptr() + off, self.epoch, blocks, edev, st),
                   "mp4x_ipc_allreduce")
             off += m
         return out
+
+    def prepare_graph(self):
+        """Move the epoch counter to device memory so hipGraph replays get fresh epochs.
+
+        Collective (every rank calls it at the same point in its call sequence)."""
+        if self._epoch_dev is None:
+            torch.cuda.synchronize()
+            self._epoch_dev = torch.full((1,), self.epoch, dtype=torch.int32, device="cuda")
+        return self
 
     def error_word(self) -> int:
         v = ctypes.c_uint32(0)

@@ -95,3 +95,63 @@ def test_ipc_allreduce_bf16():
     for r, res in out.items():
         for n, algo, op, err, ew in res:
             assert ew == 0 and err < 0.05, (n, algo, op, err)
+
+
+def _graph_worker(port, q, n, replays):
+    try:
+        import torch
+        from mp4x import ProcessCommSlave, Operators
+        from mp4x.parallel.ipc import IpcAllreduce, ONESHOT, TWOSHOT
+        torch.cuda.set_device(0)
+        comm = ProcessCommSlave("t", "127.0.0.1", port, heartbeat=False)
+        r, p = comm.getRank(), comm.getSlaveNum()
+        ipc = IpcAllreduce(comm, nbytes=1 << 20).prepare_graph()
+        x = torch.zeros(n, device="cuda")
+        y = torch.zeros(n, device="cuda")
+        ipc.allreduce(x, Operators.Float.SUM, algo=ONESHOT, out=y)      # eager call in graph mode
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            ipc.allreduce(x, Operators.Float.SUM, algo=TWOSHOT, out=y)
+        torch.cuda.synchronize()
+        bad = 0
+        for i in range(replays):
+            x.fill_(float(r + 1 + i))
+            g.replay()
+            torch.cuda.synchronize()
+            expect = sum(j + 1 + i for j in range(p))
+            bad += int((y != expect).sum().item())
+            if i % 5 == 0:   # interleave eager calls with replays
+                ipc.allreduce(x, Operators.Float.SUM, algo=ONESHOT, out=y)
+                torch.cuda.synchronize()
+                bad += int((y != expect).sum().item())
+        comm.barrier()
+        ew = ipc.error_word()
+        ipc.close()
+        comm.close(0)
+        q.put((r, "ok", (bad, ew)))
+    except BaseException:
+        q.put((-1, "err", traceback.format_exc()))
+
+
+def test_ipc_allreduce_hipgraph_replay():
+    from mp4x import CommMaster
+    p = 3
+    m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_graph_worker, args=(m.port, q, 4096 * 3, 20)) for _ in range(p)]
+    for pr in procs:
+        pr.start()
+    try:
+        for _ in range(p):
+            r, st, val = q.get(timeout=240)
+            assert st == "ok", val
+            assert val == (0, 0), (r, val)
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+        m.stop(timeout=5)
