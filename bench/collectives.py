@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""nccl-tests-style sweep of every mp4x collective on MI355X + the BASELINE.json configs.
+
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/collectives.py --sweep ref
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/collectives.py --config zero_bf16
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/collectives.py --config sparse_map
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench/collectives.py --config fp8_8gb
+
+``--sweep ref`` runs the reference's published table shape: double[] of
+1e5 ... 1e9 elements for gather / scatter / allgather / reduce-scatter / broadcast / reduce /
+allreduce, reporting algbw, busbw (nccl-tests factors) and p50/p99 per size,
+plus the reference's own time at that (p, size) for comparison.  One JSON line per row.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# README.md:341-352 of the reference (8 slaves, 1 GbE, ms) and :302-339 for 2/4/6
+REF_MS = {
+    2: {100000: [6, 6, 6, 7, 12, 12, 12], 1000000: [48, 43, 45, 38, 95, 105, 110],
+        10000000: [397, 355, 445, 447, 850, 840, 955], 100000000: [3526, 3555, 4667, 4611, 8002, 8061, 9547],
+        1000000000: [34228, 34464, 47179, 47361, 80846, 78442, 93624]},
+    4: {100000: [12, 8, 10, 11, 19, 20, 23], 1000000: [57, 56, 63, 65, 118, 121, 130],
+        10000000: [538, 534, 630, 618, 1149, 1237, 1230], 100000000: [5223, 5266, 6601, 7322, 11973, 11894, 13283],
+        1000000000: [51396, 52517, 65308, 62918, 117354, 118999, 129174]},
+    8: {100000: [16, 11, 15, 14, 24, 25, 28], 1000000: [69, 67, 92, 85, 152, 155, 183],
+        10000000: [645, 648, 741, 749, 1449, 1431, 1641], 100000000: [6050, 6143, 8716, 8931, 14800, 14561, 16332],
+        1000000000: [59974, 61426, 75464, 74495, 136574, 134260, 154090]},
+}
+OPS = ["gather", "scatter", "allgather", "reduce_scatter", "broadcast", "reduce", "allreduce"]
+
+
+def busfactor(op, p):
+    if op in ("gather", "scatter", "allgather", "reduce_scatter"):
+        return (p - 1) / p
+    if op in ("broadcast", "reduce"):
+        return 1.0
+    return 2.0 * (p - 1) / p
+
+
+def timed(fn, iters, warmup, sync):
+    import torch
+    for _ in range(warmup):
+        fn()
+    sync()
+    s = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    e = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
+    for i in range(iters):
+        s[i].record()
+        fn()
+        e[i].record()
+    sync()
+    ts = sorted(a.elapsed_time(b) for a, b in zip(s, e))
+    return ts[len(ts) // 2], ts[min(len(ts) - 1, int(0.99 * len(ts)))]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sweep", choices=["ref", "none"], default="none")
+    ap.add_argument("--config", choices=["none", "zero_bf16", "sparse_map", "fp8_8gb", "allreduce_1gb"],
+                    default="none")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--max-elems", type=float, default=1e9)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    from mp4x import CommUtils, Operands, Operators
+    from mp4x.launch import init_from_env
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    comm = init_from_env(heartbeat=False)
+    p, r = comm.getSlaveNum(), comm.getRank()
+    eng = comm.device if p > 1 else None
+
+    def sync():
+        torch.cuda.synchronize()
+        if eng is not None:
+            eng.barrier()
+            torch.cuda.synchronize()
+
+    def emit(rec):
+        if r == 0:
+            print(json.dumps(rec), flush=True)
+
+    if a.sweep == "ref":
+        D = Operands.DOUBLE_OPERAND()
+        for n in (100000, 1000000, 10000000, 100000000, 1000000000):
+            if n > a.max_elems:
+                break
+            buf = torch.randn(n, device="cuda", dtype=torch.float64)
+            froms = CommUtils.createProcessArrayFroms(n, p)
+            tos = CommUtils.createProcessArrayTos(n, p)
+            counts = [t - f for f, t in zip(froms, tos)]
+            fns = {
+                "gather": lambda: comm.gatherArray(buf, D, froms, tos, 0),
+                "scatter": lambda: comm.scatterArray(buf, D, froms, tos, 0),
+                "allgather": lambda: comm.allgatherArray(buf, D, froms, tos),
+                "reduce_scatter": lambda: comm.reduceScatterArray(buf, D, Operators.Double.SUM, 0, counts),
+                "broadcast": lambda: comm.broadcastArray(buf, D, 0, n, 0),
+                "reduce": lambda: comm.reduceArray(buf, D, Operators.Double.SUM, 0, n, 0),
+                "allreduce": lambda: comm.allreduceArray(buf, D, Operators.Double.SUM, 0, n),
+            }
+            for k, op in enumerate(OPS):
+                p50, p99 = timed(fns[op], a.iters, a.warmup, sync)
+                nb = n * 8
+                algbw = nb / (p50 * 1e-3) / 1e9
+                ref = REF_MS.get(p, {}).get(n)
+                emit({"op": op, "p": p, "elements": n, "bytes": nb, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
+                      "algbw_GBps": round(algbw, 3), "busbw_GBps": round(algbw * busfactor(op, p), 3),
+                      "ref_ms_1GbE": ref[k] if ref else None,
+                      "speedup_vs_ref": round(ref[k] / p50, 1) if ref else None})
+            del buf
+    if a.config == "zero_bf16":   # BASELINE config 3: RS + AG of a 4 GB bf16 tensor
+        n = 2_000_000_000 // p * p
+        x = torch.randn(n, device="cuda").to(torch.bfloat16)
+        B = Operands.BF16_OPERAND()
+        counts = [n // p] * p
+        froms = CommUtils.getFromsFromCount(0, counts, p)
+        tos = CommUtils.getTosFromCount(0, counts, p)
+
+        def step():
+            comm.reduceScatterArray(x, B, Operators.BFloat16.SUM, 0, counts)
+            comm.allgatherArray(x, B, froms, tos)
+        p50, p99 = timed(step, a.iters, a.warmup, sync)
+        nb = n * 2
+        emit({"config": "reduceScatter + allgather of 4 GB bf16 (ZeRO)", "p": p, "p50_ms": p50, "p99_ms": p99,
+              "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None})
+    if a.config == "sparse_map":  # BASELINE config 4: sparse Map<String, float[]> allreduce
+        dim, nkeys = 64, 200_000
+        shared = nkeys // 2
+        ids = torch.cat([torch.arange(shared), 10_000_000 + r * nkeys + torch.arange(nkeys - shared)]).cuda()
+        vals = torch.randn(nkeys, dim, device="cuda")
+        fn = (lambda: comm.allreduceSparse(ids, vals, Operators.Float.SUM)) if p > 1 else (lambda: None)
+        p50, p99 = timed(fn, a.iters, a.warmup, sync)
+        m = {f"feat{i}": vals[i] for i in range(2000)}
+        t0 = time.perf_counter()
+        if p > 1:
+            comm.allreduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.SUM)
+        t_map = time.perf_counter() - t0
+        emit({"config": "sparse allreduce, 200k keys x float[64] per rank (50% shared)", "p": p,
+              "p50_ms": p50, "p99_ms": p99, "map_api_2000_keys_ms": t_map * 1e3})
+    if a.config in ("fp8_8gb", "allreduce_1gb"):   # BASELINE configs 5 / 2
+        nbytes = 8_000_000_000 if a.config == "fp8_8gb" else 1_000_000_000
+        n = nbytes // 4
+        x = torch.randn(n, device="cuda")
+        for codec in ([None, "fp8"] if a.config == "fp8_8gb" else [None]):
+            F = Operands.FLOAT_OPERAND(codec=codec)
+            p50, p99 = timed(lambda: comm.allreduceArray(x, F, Operators.Float.SUM, 0, n), a.iters, a.warmup, sync)
+            emit({"config": f"allreduce {nbytes/1e9:.0f} GB f32", "codec": codec or "none", "p": p,
+                  "p50_ms": p50, "p99_ms": p99,
+                  "busbw_GBps": round(nbytes / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None})
+    comm.close(0)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

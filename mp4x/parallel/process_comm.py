@@ -127,6 +127,8 @@ class ProcessCommSlave:
         self.engine = HostEngine(self.transport, self.rank, self.slaveNum)
         self._fault = _FaultInjector(self.rank)
         self.stats: Dict[str, Any] = {"calls": {}, "bytes": 0}
+        from ..utils.trace import Tracer
+        self.tracer = Tracer(self.rank)
 
         pid = os.getpid()
         host = self.transport.advertise_host
@@ -624,6 +626,45 @@ class ProcessCommSlave:
         opnd = operand or Operands.FLOAT_OPERAND()
         self.allreduceArray(flat, opnd, op, 0, flat.shape[0])
         return tensor
+
+
+def _nbytes(x) -> int:
+    if isinstance(x, np.ndarray):
+        return int(x.nbytes)
+    if _is_torch(x):
+        return int(x.numel() * x.element_size())
+    if isinstance(x, (list, dict, set)):
+        return len(x)
+    return 0
+
+
+def _traced(name, fn):
+    def wrapper(self, *args, **kwargs):
+        a0 = args[0] if args else None
+        with self.tracer.span(name, _nbytes(a0), a0 if _is_device_tensor(a0) else None):
+            return fn(self, *args, **kwargs)
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    wrapper.__wrapped__ = fn
+    return wrapper
+
+
+_TRACED = ["gatherArray", "gatherMap", "allgatherArray", "allgatherMap", "broadcastArray", "broadcastMap",
+           "scatterArray", "scatterMap", "reduceScatterArray", "reduceScatterMap", "reduceArray", "reduceMap",
+           "allreduceArray", "allreduceArrayRpc", "allreduceMap", "allreduceSparse", "barrier"]
+for _n in _TRACED:
+    setattr(ProcessCommSlave, _n, _traced(_n, getattr(ProcessCommSlave, _n)))
+
+
+def _trace_report(self):
+    """Per-collective calls / bytes / host ms (+ device ms and algorithm mix with MP4X_TRACE=1)."""
+    rep = self.tracer.report()
+    if self._device_engine is not None:
+        rep["_device_algorithms"] = dict(self._device_engine.stats)
+    return rep
+
+
+ProcessCommSlave.trace_report = _trace_report
 
 
 # snake_case aliases --------------------------------------------------------------

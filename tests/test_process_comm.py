@@ -266,3 +266,16 @@ def big_ring(comm):
 def test_large_allreduce_4_ranks():
     res, _, _ = run_ranks(4, big_ring, timeout=180)
     assert all(v == 4 * 3_000_007 for v in res.values())
+
+
+def traced(comm):
+    a = np.ones(100)
+    comm.allreduceArray(a, Operands.DOUBLE_OPERAND(), Operators.Double.SUM, 0, 100)
+    comm.allreduce_array(a, Operands.DOUBLE_OPERAND(), Operators.Double.SUM, 0, 100)   # snake_case alias
+    rep = comm.trace_report()
+    return rep["allreduceArray"]["calls"], rep["allreduceArray"]["bytes"]
+
+
+def test_trace_report_counts_calls():
+    res, _, _ = run_ranks(2, traced, env={"MP4X_TRACE": "1"})
+    assert all(v == (2, 1600) for v in res.values())
