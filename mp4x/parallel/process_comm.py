@@ -49,6 +49,8 @@ HEARTBEAT_DELAY = float(os.environ.get("MP4X_HEARTBEAT_DELAY", 5.0))
 HEARTBEAT_PERIOD = float(os.environ.get("MP4X_HEARTBEAT_PERIOD", 15.0))
 HEARTBEAT_MAX_FAIL = int(os.environ.get("MP4X_HEARTBEAT_MAX_FAIL", 4))
 BCAST_TREE_BYTES = int(os.environ.get("MP4X_BCAST_TREE_BYTES", 1 << 16))
+SHM_ON = os.environ.get("MP4X_SHM", "1") == "1"
+SHM_MIN_BYTES = 1 << 20     # below this the TCP mesh wins (shm barrier round trips dominate)
 
 
 def _is_device_tensor(x) -> bool:
@@ -110,6 +112,7 @@ class ProcessCommSlave:
         self.closed = False
         self._device_engine = None
         self._device_index = device
+        self._shm = None
         LOG.info("master host:%s, master port:%s", masterHost, masterPort)
         self.server = MasterClient(masterHost, masterPort)
         loop = masterHost in ("127.0.0.1", "localhost", "::1")
@@ -182,6 +185,8 @@ class ProcessCommSlave:
                     self._device_engine.shutdown()
                 except Exception:
                     pass
+            if self._shm is not None:
+                self._shm.close()
             self.transport.close()
             self.server.close()
             if self._hb_client is not None:
@@ -237,6 +242,24 @@ class ProcessCommSlave:
             self._device_engine = DeviceEngine(self, self._device_index)
         return self._device_engine
 
+    def _shm_engine(self, buf, operand: Operand, operator, nelems: int):
+        """The shared-memory engine when this call qualifies (decision identical on every rank)."""
+        if os.environ.get("MP4X_SHM", "1") != "1" or self.slaveNum == 1 or not operand.is_primitive \
+                or operand.compress:
+            return None
+        if not isinstance(buf, np.ndarray) or buf.dtype != operand.np_dtype:
+            return None
+        if operator is not None and (getattr(operator, "is_custom", False) or operator.dtype != operand.dtype):
+            return None
+        if nelems * buf.itemsize < int(os.environ.get("MP4X_SHM_MIN_BYTES", SHM_MIN_BYTES)):
+            return None
+        from .shm import ShmEngine, same_host
+        if not same_host(self.addresses):
+            return None
+        if self._shm is None:
+            self._shm = ShmEngine(self)
+        return self._shm
+
     def _tick(self, name: str):
         self._fault.tick(name)
         c = self.stats["calls"]
@@ -280,6 +303,10 @@ class ProcessCommSlave:
         if _is_device_tensor(arrData):
             return self.device.allgather(arrData, list(froms), list(tos))
         buf = _host_view(arrData, operand)
+        shm = self._shm_engine(buf, operand, None, tos[-1] - froms[0])
+        if shm is not None and buf.flags.c_contiguous:
+            shm.allgather(buf, froms, tos)
+            return arrData
         self.engine.ring_allgather(buf, froms, tos, operand)
         return arrData
 
@@ -300,6 +327,10 @@ class ProcessCommSlave:
         if _is_device_tensor(arrData):
             return self.device.broadcast(arrData, frm, to, rootRank)
         buf = _host_view(arrData, operand)
+        shm = self._shm_engine(buf, operand, None, to - frm)
+        if shm is not None and buf.flags.c_contiguous:
+            shm.broadcast(buf, frm, to, rootRank)
+            return arrData
         nbytes = (to - frm) * (operand.np_dtype.itemsize if operand.is_primitive else 64)
         if nbytes <= BCAST_TREE_BYTES or (to - frm) < self.slaveNum:
             self.engine.tree_bcast(buf, frm, to, operand, rootRank)
@@ -386,6 +417,10 @@ class ProcessCommSlave:
         if _is_device_tensor(arrData):
             return self.device.reduce_scatter(arrData, froms, tos, operator, operand)
         buf = _host_view(arrData, operand)
+        shm = self._shm_engine(buf, operand, operator, tos[-1] - froms[0])
+        if shm is not None and buf.flags.c_contiguous:
+            shm.reduce_scatter(buf, froms, tos, int(operand.dtype), int(operator.code))
+            return arrData
         self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
         return arrData
 
@@ -415,6 +450,11 @@ class ProcessCommSlave:
         if _is_device_tensor(arrData):
             return self.device.reduce(arrData, frm, to, operator, operand, rootRank)
         buf = _host_view(arrData, operand)
+        shm = self._shm_engine(buf, operand, operator, to - frm)
+        if shm is not None and buf.flags.c_contiguous:
+            # non-root results are unspecified by contract; the shm allreduce serves the root
+            shm.allreduce(buf, frm, to, int(operand.dtype), int(operator.code))
+            return arrData
         froms, tos, counts = CommUtils.even_split(frm, to, self.slaveNum)
         self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
         self.engine.tree_gather(buf, froms, tos, operand, rootRank)
@@ -542,6 +582,10 @@ class ProcessCommSlave:
         if _is_device_tensor(arrData):
             return self.device.allreduce(arrData, frm, to, operator, operand)
         buf = _host_view(arrData, operand)
+        shm = self._shm_engine(buf, operand, operator, to - frm)
+        if shm is not None and buf.flags.c_contiguous:
+            shm.allreduce(buf, frm, to, int(operand.dtype), int(operator.code))
+            return arrData
         froms, tos, _ = CommUtils.even_split(frm, to, self.slaveNum)
         self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
         self.engine.ring_allgather(buf, froms, tos, operand)

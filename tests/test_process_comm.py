@@ -279,3 +279,22 @@ def traced(comm):
 def test_trace_report_counts_calls():
     res, _, _ = run_ranks(2, traced, env={"MP4X_TRACE": "1"})
     assert all(v == (2, 1600) for v in res.values())
+
+
+@pytest.mark.parametrize("p", [2, 3, 4])
+@pytest.mark.parametrize("kind", ["double", "int", "byte"])
+def test_primitive_matrix_shared_memory_engine(p, kind):
+    """Same matrix with the /dev/shm engine (C++ host runtime) forced on for every size."""
+    res, code, _ = run_ranks(p, prim_matrix, (kind, False, 1001), env={"MP4X_SHM_MIN_BYTES": "0"})
+    assert code == 0
+
+
+def shm_used(comm):
+    a = np.ones(300_000)
+    comm.allreduceArray(a, Operands.DOUBLE_OPERAND(), Operators.Double.SUM, 0, len(a))
+    return comm._shm is not None and bool((a == comm.getSlaveNum()).all())
+
+
+def test_shm_engine_selected_for_large_same_host_arrays():
+    res, _, _ = run_ranks(3, shm_used)
+    assert all(res.values())

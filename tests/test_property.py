@@ -91,3 +91,9 @@ def random_cases(comm, seed, cases):
 def test_random_collectives_match_numpy(p, seed):
     res, code, _ = run_ranks(p, random_cases, (seed, 60), timeout=240)
     assert code == 0 and all(v == 60 for v in res.values())
+
+
+@pytest.mark.parametrize("p,seed", [(3, 21), (8, 22)])
+def test_random_collectives_shared_memory(p, seed):
+    res, code, _ = run_ranks(p, random_cases, (seed, 40), timeout=240, env={"MP4X_SHM_MIN_BYTES": "0"})
+    assert code == 0

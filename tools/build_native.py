@@ -112,7 +112,7 @@ def build_host(jobs):
 
     def comp(so):
         s, o = so
-        run(["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-Wall", "-fopenmp", "-pthread",
+        run(["g++", "-O3", "-march=x86-64-v3", "-std=c++17", "-fPIC", "-Wall", "-pthread",
              "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
         return s
 
@@ -121,7 +121,7 @@ def build_host(jobs):
             print("  g++  ", os.path.relpath(s, ROOT))
     out = os.path.join(OUT, "libmp4x_host.so")
     if todo or not os.path.exists(out):
-        run(["g++", "-shared", "-fPIC", "-fopenmp", "-pthread", "-o", out] + objs)
+        run(["g++", "-shared", "-fPIC", "-pthread", "-o", out] + objs)
         print("  link ", os.path.relpath(out, ROOT))
     return out
 
