@@ -166,3 +166,37 @@ def test_baseline_config1_two_threads():
     """BASELINE config 1: 2-thread in-process float[1024] allreduceArray on CPU."""
     res, code, _ = run_ranks(1, config1, kind="thread", threads=2)
     assert res[0] == [(3.0, 3.0), (3.0, 3.0)]
+
+
+def stress(tc, iters):
+    """Race screen: many back-to-back mixed collectives from every thread (no sleeps)."""
+    p, r, T = tc.getSlaveNum(), tc.getRank(), tc.getThreadNum()
+
+    def body(t):
+        rng = np.random.default_rng(1234)          # same op sequence on every thread / rank
+        for it in range(iters):
+            k = int(rng.integers(4))
+            n = int(rng.integers(1, 64))
+            if k == 0:
+                a = np.full(n, float(it + t), np.float64)
+                tc.allreduceArray(a, Operands.DOUBLE_OPERAND(), Operators.Double.SUM, 0, n)
+                assert (a == sum(it + j for j in range(T)) * p).all()
+            elif k == 1:
+                v = tc.allreduce(it * 10 + t + r, Operands.INT_OPERAND(), Operators.Int.MAX)
+                assert v == it * 10 + (T - 1) + (p - 1)
+            elif k == 2:
+                m = tc.allreduceMap({"k": 1, f"t{t}r{r}": it}, Operands.INT_OPERAND(), Operators.Int.SUM)
+                assert m["k"] == p * T and len(m) == 1 + p * T
+            else:
+                a = np.full(n, -1.0)
+                a[:] = 5.0 if (r == 0 and t == 0) else -1.0
+                tc.broadcastArray(a, Operands.DOUBLE_OPERAND(), 0, n, 0, 0)
+                assert (a == 5.0).all()
+        return True
+
+    return _run_threads(tc, body)
+
+
+def test_thread_stress_interleaved_collectives():
+    res, code, _ = run_ranks(2, stress, (150,), kind="thread", threads=4, timeout=240)
+    assert code == 0 and all(all(v) for v in res.values())

@@ -98,7 +98,8 @@ def build_hip(jobs):
 
 
 def build_host(jobs):
-    srcs = sorted(glob.glob(os.path.join(CSRC, "host", "*.cpp")))
+    srcs = sorted(f for f in glob.glob(os.path.join(CSRC, "host", "*.cpp"))
+                  if not os.path.basename(f).startswith("test_"))   # test_*.cpp are standalone test programs
     if not srcs:
         return None
     deps = headers()
