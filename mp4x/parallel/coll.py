@@ -1,0 +1,212 @@
+"""Collective back-ends used by the device engine.
+
+``TorchColl``    the production path: ``torch.distributed`` with the ``nccl`` backend, i.e.
+                 RCCL over xGMI (gloo for CPU tensors in tests).
+``LoopbackColl`` an in-process fake: p "virtual ranks" are threads of ONE process that share
+                 a hub; every collective is computed from the ranks' published tensors.  It
+                 lets the whole device engine (two-shot a2a schedule, fp8 / bf16 codecs,
+                 sparse map exchange, p2p gather/scatter) run with real HIP kernels on a
+                 single GPU — RCCL refuses two ranks on one device — and without any GPU on
+                 CPU tensors (the "fake backend" SURVEY §4 asks for).
+"""
+from __future__ import annotations
+
+import threading
+from collections import defaultdict
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from ..operators import OpCode
+
+_RCCL_OPS = {OpCode.SUM: dist.ReduceOp.SUM, OpCode.MAX: dist.ReduceOp.MAX,
+             OpCode.MIN: dist.ReduceOp.MIN, OpCode.PROD: dist.ReduceOp.PRODUCT}
+
+
+class TorchColl:
+    def __init__(self, pg, backend: str):
+        self.pg = pg
+        self.backend = backend
+        self.gather_into_tensor_ok = backend != "gloo"
+        self.reduce_scatter_ok = backend != "gloo"
+
+    def all_reduce(self, t, code):
+        dist.all_reduce(t, op=_RCCL_OPS[code], group=self.pg)
+
+    def reduce(self, t, dst, code):
+        dist.reduce(t, dst=dst, op=_RCCL_OPS[code], group=self.pg)
+
+    def broadcast(self, t, src):
+        dist.broadcast(t, src=src, group=self.pg)
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.pg)
+
+    def all_gather_into_tensor(self, out, inp):
+        dist.all_gather_into_tensor(out, inp, group=self.pg)
+
+    def all_gather(self, outs, t):
+        dist.all_gather(outs, t, group=self.pg)
+
+    def reduce_scatter_tensor(self, out, inp, code):
+        dist.reduce_scatter_tensor(out, inp, op=_RCCL_OPS[code], group=self.pg)
+
+    def p2p(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
+        ops = [dist.P2POp(dist.isend, t, j, group=self.pg) for t, j in sends]
+        ops += [dist.P2POp(dist.irecv, t, j, group=self.pg) for t, j in recvs]
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+
+    def barrier(self):
+        dist.barrier(group=self.pg)
+
+
+class LoopbackHub:
+    """Shared state of p virtual ranks living in one process."""
+
+    def __init__(self, p: int):
+        self.p = p
+        self.bar = threading.Barrier(p)
+        self.slots: List[object] = [None] * p
+        self.box = {}
+        self.cv = threading.Condition()
+
+    def coll(self, rank: int) -> "LoopbackColl":
+        return LoopbackColl(self, rank)
+
+
+def _combine(code, a, b):
+    if code == OpCode.SUM:
+        return a + b
+    if code == OpCode.MAX:
+        return torch.maximum(a, b)
+    if code == OpCode.MIN:
+        return torch.minimum(a, b)
+    if code == OpCode.PROD:
+        return a * b
+    raise ValueError(code)
+
+
+class LoopbackColl:
+    gather_into_tensor_ok = True
+    reduce_scatter_ok = True
+    backend = "loopback"
+
+    def __init__(self, hub: LoopbackHub, rank: int):
+        self.hub = hub
+        self.rank = rank
+        self.p = hub.p
+        self._seq = defaultdict(int)
+
+    def _sync(self, t=None):
+        if (t is not None and t.is_cuda) or torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+    def _exchange(self, obj):
+        """Publish obj, return every rank's object (after all published)."""
+        self._sync()
+        self.hub.slots[self.rank] = obj
+        self.hub.bar.wait()
+        out = list(self.hub.slots)
+        self.hub.bar.wait()
+        return out
+
+    def all_reduce(self, t, code):
+        xs = self._exchange(t.clone())
+        acc = xs[0].clone()
+        for x in xs[1:]:
+            acc = _combine(code, acc, x)
+        t.copy_(acc)
+        self._sync()
+
+    def reduce(self, t, dst, code):
+        xs = self._exchange(t.clone())
+        if self.rank == dst:
+            acc = xs[0].clone()
+            for x in xs[1:]:
+                acc = _combine(code, acc, x)
+            t.copy_(acc)
+        self._sync()
+
+    def broadcast(self, t, src):
+        xs = self._exchange(t.clone() if self.rank == src else None)
+        if self.rank != src:
+            t.copy_(xs[src])
+        self._sync()
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        p = self.p
+        if in_splits is None:
+            in_splits = [inp.shape[0] // p] * p
+        offs = [0]
+        for s in in_splits:
+            offs.append(offs[-1] + s)
+        pieces = [inp[offs[j]:offs[j + 1]].clone() for j in range(p)]
+        allp = self._exchange(pieces)
+        got = [allp[j][self.rank] for j in range(p)]
+        o = 0
+        for g in got:
+            out[o:o + g.shape[0]].copy_(g)
+            o += g.shape[0]
+        self._sync()
+
+    def all_gather_into_tensor(self, out, inp):
+        xs = self._exchange(inp.clone())
+        torch.cat([x.reshape(-1) for x in xs]).view(-1)
+        out.view(-1).copy_(torch.cat([x.reshape(-1) for x in xs]))
+        self._sync()
+
+    def all_gather(self, outs, t):
+        xs = self._exchange(t.clone())
+        for o, x in zip(outs, xs):
+            o.copy_(x)
+        self._sync()
+
+    def reduce_scatter_tensor(self, out, inp, code):
+        xs = self._exchange(inp.clone())
+        n = out.numel()
+        acc = xs[0][self.rank * n:(self.rank + 1) * n].clone()
+        for x in xs[1:]:
+            acc = _combine(code, acc, x[self.rank * n:(self.rank + 1) * n])
+        out.copy_(acc.view_as(out))
+        self._sync()
+
+    def p2p(self, sends, recvs):
+        self._sync()
+        with self.hub.cv:
+            for t, j in sends:
+                k = (self.rank, j, self._seq[("s", j)])
+                self._seq[("s", j)] += 1
+                self.hub.box[k] = t.clone()
+            self.hub.cv.notify_all()
+        for t, j in recvs:
+            k = (j, self.rank, self._seq[("r", j)])
+            self._seq[("r", j)] += 1
+            with self.hub.cv:
+                while k not in self.hub.box:
+                    self.hub.cv.wait(1.0)
+                v = self.hub.box.pop(k)
+            t.copy_(v)
+        self._sync()
+
+    def barrier(self):
+        self.hub.bar.wait()
+
+
+class _FakeComm:
+    """Minimal communicator facade for a loopback virtual rank."""
+
+    def __init__(self, rank: int, p: int):
+        self.rank = rank
+        self.slaveNum = p
+        self.server = None
+        self.transport = None
+
+
+def loopback_engines(p: int, device=None):
+    """p DeviceEngines sharing one LoopbackHub (drive each from its own thread)."""
+    from .device_engine import DeviceEngine
+    hub = LoopbackHub(p)
+    return [DeviceEngine(_FakeComm(r, p), coll=hub.coll(r), device=device) for r in range(p)]

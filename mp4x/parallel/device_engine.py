@@ -89,35 +89,50 @@ def local_reduce(out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: i
 
 
 class DeviceEngine:
-    def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None):
+    def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
+                 device=None):
         self.comm = comm
         self.rank = comm.rank
         self.p = comm.slaveNum
         self.stats: Dict[str, int] = {}
         use_cuda = torch.cuda.is_available()
-        self.backend = backend or os.environ.get("MP4X_DEVICE_BACKEND") or ("nccl" if use_cuda else "gloo")
-        if use_cuda:
-            if device_index is None:
-                lr = os.environ.get("LOCAL_RANK")
-                device_index = int(lr) if lr is not None else self.rank % torch.cuda.device_count()
-            torch.cuda.set_device(device_index)
-            self.device = torch.device("cuda", device_index)
-            from ..ops import native
-            native.hip()   # fail loudly here if the kernels are missing on a GPU box
-        else:
-            self.device = torch.device("cpu")
         self._owns_pg = False
-        if dist.is_initialized():
-            if dist.get_world_size() != self.p or dist.get_rank() != self.rank:
-                raise Mp4jException(f"torch.distributed already initialised with world={dist.get_world_size()} "
-                                    f"rank={dist.get_rank()} but mp4x has p={self.p} rank={self.rank}")
-            self.pg = dist.group.WORLD
+        self.pg = None
+        if coll is not None:
+            # injected back-end (LoopbackColl: p virtual ranks in one process)
+            self.coll = coll
+            self.backend = coll.backend
+            self.device = torch.device(device) if device is not None else \
+                (torch.device("cuda", torch.cuda.current_device()) if use_cuda else torch.device("cpu"))
+            if self.device.type == "cuda":
+                from ..ops import native
+                native.hip()
         else:
-            self._init_pg()
+            self.backend = backend or os.environ.get("MP4X_DEVICE_BACKEND") or ("nccl" if use_cuda else "gloo")
+            if use_cuda:
+                if device_index is None:
+                    lr = os.environ.get("LOCAL_RANK")
+                    device_index = int(lr) if lr is not None else self.rank % torch.cuda.device_count()
+                torch.cuda.set_device(device_index)
+                self.device = torch.device("cuda", device_index)
+                from ..ops import native
+                native.hip()   # fail loudly here if the kernels are missing on a GPU box
+            else:
+                self.device = torch.device("cpu")
+            if dist.is_initialized():
+                if dist.get_world_size() != self.p or dist.get_rank() != self.rank:
+                    raise Mp4jException(f"torch.distributed already initialised with world={dist.get_world_size()} "
+                                        f"rank={dist.get_rank()} but mp4x has p={self.p} rank={self.rank}")
+                self.pg = dist.group.WORLD
+            else:
+                self._init_pg()
+            from .coll import TorchColl
+            self.coll = TorchColl(self.pg, self.backend)
         self.algo = _env_algo()
         self.a2a_bytes = int(os.environ.get("MP4X_A2A_MIN_BYTES", 0))
         # custom xGMI IPC allreduce (csrc/runtime/ipc.hip) below these sizes
-        self.ipc_enabled = os.environ.get("MP4X_IPC", "1") == "1" and self.device.type == "cuda" and 2 <= self.p <= 8
+        self.ipc_enabled = os.environ.get("MP4X_IPC", "1") == "1" and self.device.type == "cuda" and 2 <= self.p <= 8 \
+            and coll is None
         self.ipc_oneshot_max = int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))
         self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
         self._ipc_obj = None
@@ -176,7 +191,7 @@ class DeviceEngine:
     def rccl_ok(self, op, dtype) -> bool:
         if getattr(op, "is_custom", False):
             return False
-        if self.backend == "gloo":
+        if self.backend in ("gloo", "loopback"):
             return op.code in _RCCL_OPS and dtype not in (torch.bfloat16, torch.float16, torch.int16)
         return op.code in _RCCL_OPS and dtype in _RCCL_DTYPES
 
@@ -205,10 +220,11 @@ class DeviceEngine:
         """Per-call algorithm choice (size tiers, dtype/op support, MP4X_DEVICE_ALGO override)."""
         forced = self.algo
         codec = getattr(operand, "codec", None) if operand is not None else None
-        if codec == "fp8" and kind in ("allreduce", "reduce_scatter") and \
-                dtype in (torch.float32, torch.bfloat16, torch.float16) and op is not None and \
-                not getattr(op, "is_custom", False) and op.code == OpCode.SUM and self.device.type == "cuda":
-            return "fp8"
+        if codec in ("fp8", "bf16") and kind == "allreduce" and \
+                dtype in ((torch.float32, torch.bfloat16, torch.float16) if codec == "fp8" else (torch.float32,)) \
+                and op is not None and not getattr(op, "is_custom", False) and op.code == OpCode.SUM \
+                and self.device.type == "cuda":
+            return codec
         if forced in ("ipc1", "ipc2") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             return forced
         if op is not None and not self.rccl_ok(op, dtype):
@@ -242,12 +258,18 @@ class DeviceEngine:
         if algo in ("ipc1", "ipc2") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
-            dist.all_reduce(view, op=_RCCL_OPS[op.code], group=self.pg)
+            self.coll.all_reduce(view, op.code)
         elif algo in ("ipc1", "ipc2"):
             from .ipc import ONESHOT, TWOSHOT
             self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT)
         elif algo == "fp8":
             self._allreduce_fp8(view)
+        elif algo == "bf16":
+            # 2x-compressed wire: bf16 all-to-all, f32 accumulation inside the K1 kernel
+            # (bf16 inputs, one rounding), bf16 all-gather, widened back in place
+            w = view.to(torch.bfloat16)
+            self._allreduce_a2a(w, for_dtype(op, DType.BF16))
+            view.copy_(w)
         else:
             self._allreduce_a2a(view, op)
         return arr
@@ -276,8 +298,7 @@ class DeviceEngine:
         bsrc = src.view(torch.uint8) if src.dtype in (torch.int16,) else src
         brecv = recv.view(torch.uint8) if recv.dtype in (torch.int16,) else recv
         es = 2 if src.dtype in (torch.int16,) else 1
-        dist.all_to_all_single(brecv, bsrc, output_split_sizes=[cr * es] * p,
-                               input_split_sizes=[c * es for c in counts], group=self.pg)
+        self.coll.all_to_all_single(brecv, bsrc, [cr * es] * p, [c * es for c in counts])
         out = view[froms[r]:tos[r]]
         if cr:
             self._reduce_into(out, [recv[j * cr:(j + 1) * cr] for j in range(p)], op)
@@ -286,10 +307,10 @@ class DeviceEngine:
     def _allgather_any(self, view: torch.Tensor, froms, tos):
         counts = [t - f for f, t in zip(froms, tos)]
         contiguous = all(froms[i + 1] == tos[i] for i in range(self.p - 1))
-        if contiguous and len(set(counts)) == 1 and counts[0] > 0 and self.backend != "gloo":
+        if contiguous and len(set(counts)) == 1 and counts[0] > 0 and self.coll.gather_into_tensor_ok:
             whole = view[froms[0]:tos[-1]]
             mine = view[froms[self.rank]:tos[self.rank]]
-            dist.all_gather_into_tensor(whole, mine, group=self.pg)
+            self.coll.all_gather_into_tensor(whole, mine)
             return view
         self._allgather_p2p(view, froms, tos)
         return view
@@ -297,18 +318,10 @@ class DeviceEngine:
     def _allgather_p2p(self, view: torch.Tensor, froms, tos):
         """Direct allgather-v over the full mesh: one grouped launch of p-1 sends + p-1 recvs."""
         p, r = self.p, self.rank
-        ops = []
         mine = view[froms[r]:tos[r]]
-        for j in range(p):
-            if j == r:
-                continue
-            if tos[r] > froms[r]:
-                ops.append(dist.P2POp(dist.isend, mine, j, group=self.pg))
-            if tos[j] > froms[j]:
-                ops.append(dist.P2POp(dist.irecv, view[froms[j]:tos[j]], j, group=self.pg))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+        sends = [(mine, j) for j in range(p) if j != r and tos[r] > froms[r]]
+        recvs = [(view[froms[j]:tos[j]], j) for j in range(p) if j != r and tos[j] > froms[j]]
+        self.coll.p2p(sends, recvs)
 
     def _allreduce_fp8(self, view: torch.Tensor):
         """Compressed two-shot allreduce (K6 codec on the wire, f32 accumulation)."""
@@ -327,8 +340,8 @@ class DeviceEngine:
         K.quant_fp8(padded, q, s)     # one launch: chunks are whole quant blocks, so scales never straddle
         rq = torch.empty_like(q)
         rs = torch.empty_like(s)
-        dist.all_to_all_single(rq, q, group=self.pg)
-        dist.all_to_all_single(rs, s, group=self.pg)
+        self.coll.all_to_all_single(rq, q)
+        self.coll.all_to_all_single(rs, s)
         # reduce my chunk in f32 and re-quantise for the all-gather leg (one fused kernel)
         mine_q = torch.empty(c, dtype=torch.uint8, device=dev)
         mine_s = torch.empty(nblk, dtype=torch.float32, device=dev)
@@ -337,8 +350,8 @@ class DeviceEngine:
                              q_out=mine_q, s_out=mine_s, out_dtype=torch.float32)
         gq = torch.empty(p * c, dtype=torch.uint8, device=dev)
         gs = torch.empty(p * nblk, dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(gq, mine_q, group=self.pg)
-        dist.all_gather_into_tensor(gs, mine_s, group=self.pg)
+        self.coll.all_gather_into_tensor(gq, mine_q)
+        self.coll.all_gather_into_tensor(gs, mine_s)
         K.dequant_fp8(gq, gs, p * c, padded)
         view.copy_(padded[:n])
         return view
@@ -358,16 +371,16 @@ class DeviceEngine:
             algo = "a2a"    # exact path for ragged RS; fp8 RS is used inside the compressed allreduce
         self._count("reduce_scatter." + algo)
         equal = len(set(counts)) == 1
-        if algo == "rccl" and equal and self.backend != "gloo":
-            dist.reduce_scatter_tensor(flat[froms[r]:tos[r]], whole, op=_RCCL_OPS[op.code], group=self.pg)
-        elif algo == "rccl" and self.backend != "gloo":
+        if algo == "rccl" and equal and self.coll.reduce_scatter_ok:
+            self.coll.reduce_scatter_tensor(flat[froms[r]:tos[r]], whole, op.code)
+        elif algo == "rccl" and self.coll.reduce_scatter_ok:
             cmax = max(counts)
             stage = torch.zeros(self.p * cmax, dtype=whole.dtype, device=whole.device)
             for j in range(self.p):
                 if counts[j]:
                     stage[j * cmax:j * cmax + counts[j]].copy_(flat[froms[j]:tos[j]])
             out = torch.empty(cmax, dtype=whole.dtype, device=whole.device)
-            dist.reduce_scatter_tensor(out, stage, op=_RCCL_OPS[op.code], group=self.pg)
+            self.coll.reduce_scatter_tensor(out, stage, op.code)
             if counts[r]:
                 flat[froms[r]:tos[r]].copy_(out[:counts[r]])
         else:
@@ -386,7 +399,7 @@ class DeviceEngine:
         flat = self._flat(arr)
         if to > frm:
             self._count("broadcast")
-            dist.broadcast(flat[frm:to], src=root, group=self.pg)
+            self.coll.broadcast(flat[frm:to], root)
         return arr
 
     def reduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand, root: int):
@@ -397,7 +410,7 @@ class DeviceEngine:
         op = self._op(operator, view)
         if self.select("reduce", view.numel() * view.element_size(), op, view.dtype) == "rccl":
             self._count("reduce.rccl")
-            dist.reduce(view, dst=root, op=_RCCL_OPS[op.code], group=self.pg)
+            self.coll.reduce(view, root, op.code)
         else:   # reduce-scatter + gather (reference reduceArray composition, ProcessCommSlave.java:1390-1421)
             self._count("reduce.a2a")
             froms, tos, _ = CommUtils.even_split(frm, to, self.p)
@@ -410,32 +423,20 @@ class DeviceEngine:
         flat = self._flat(arr)
         r = self.rank
         self._count("gather")
-        ops = []
         if r == root:
-            for j in range(self.p):
-                if j != r and tos[j] > froms[j]:
-                    ops.append(dist.P2POp(dist.irecv, flat[froms[j]:tos[j]], j, group=self.pg))
+            self.coll.p2p([], [(flat[froms[j]:tos[j]], j) for j in range(self.p) if j != r and tos[j] > froms[j]])
         elif tos[r] > froms[r]:
-            ops.append(dist.P2POp(dist.isend, flat[froms[r]:tos[r]], root, group=self.pg))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            self.coll.p2p([(flat[froms[r]:tos[r]], root)], [])
         return arr
 
     def scatter(self, arr: torch.Tensor, froms, tos, root: int):
         flat = self._flat(arr)
         r = self.rank
         self._count("scatter")
-        ops = []
         if r == root:
-            for j in range(self.p):
-                if j != r and tos[j] > froms[j]:
-                    ops.append(dist.P2POp(dist.isend, flat[froms[j]:tos[j]], j, group=self.pg))
+            self.coll.p2p([(flat[froms[j]:tos[j]], j) for j in range(self.p) if j != r and tos[j] > froms[j]], [])
         elif tos[r] > froms[r]:
-            ops.append(dist.P2POp(dist.irecv, flat[froms[r]:tos[r]], root, group=self.pg))
-        if ops:
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
+            self.coll.p2p([], [(flat[froms[r]:tos[r]], root)])
         return arr
 
     # ================================================================== sparse map
@@ -445,4 +446,10 @@ class DeviceEngine:
         return allreduce_map_device(self, mapData, operator)
 
     def barrier(self):
-        dist.barrier(group=self.pg)
+        self.coll.barrier()
+
+    def all_gather_object(self, obj) -> List:
+        """Small host objects from every rank (rank order) — key dictionaries, handles."""
+        if hasattr(self.coll, "_exchange"):
+            return self.coll._exchange(obj)
+        return self.comm.server.call("allgather_obj", self.rank, obj)

@@ -73,15 +73,12 @@ def _dictionary(engine) -> KeyDictionary:
 
 
 def _sync_new_keys(engine, new: Dict[str, int]) -> None:
-    """Host allgather of the (string, id) pairs some rank has not published yet."""
-    from ..operands import Operands
-    comm = engine.comm
-    blocks = comm.engine.ring_allgather_maps([new], Operands.LONG_OPERAND())
+    """Allgather (through the control plane) of the (string, id) pairs not published yet."""
+    blocks = engine.all_gather_object(new)
     d = _dictionary(engine)
-    for r, blk in enumerate(blocks):
-        if r != comm.rank:
-            for m in blk:
-                d.learn(m)
+    for r, m in enumerate(blocks):
+        if r != engine.rank and m:
+            d.learn(m)
 
 
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins
@@ -138,15 +135,15 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     skeys = _gather_rows(keys.view(-1, 1), perm).view(-1)
     svals = _gather_rows(vals, perm) if vals is not None else None
     recv_counts = torch.empty_like(hist)
-    dist.all_to_all_single(recv_counts, hist, group=engine.pg)
+    engine.coll.all_to_all_single(recv_counts, hist)
     send = hist.tolist()
     recv = recv_counts.tolist()
     rkeys = torch.empty(sum(recv), dtype=keys.dtype, device=keys.device)
-    dist.all_to_all_single(rkeys, skeys, recv, send, group=engine.pg)
+    engine.coll.all_to_all_single(rkeys, skeys, recv, send)
     rvals = None
     if vals is not None:
         rvals = torch.empty((sum(recv),) + tuple(vals.shape[1:]), dtype=vals.dtype, device=vals.device)
-        dist.all_to_all_single(rvals, svals, recv, send, group=engine.pg)
+        engine.coll.all_to_all_single(rvals, svals, recv, send)
     return rkeys, rvals
 
 
@@ -154,14 +151,14 @@ def _allgather_v(engine, t: torch.Tensor) -> torch.Tensor:
     p = engine.p
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     ns = [torch.empty_like(n) for _ in range(p)]
-    dist.all_gather(ns, n, group=engine.pg)
+    engine.coll.all_gather(ns, n)
     sizes = [int(x.item()) for x in ns]
     m = max(sizes) if sizes else 0
     pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     if t.shape[0]:
         pad[:t.shape[0]] = t
     outs = [torch.empty_like(pad) for _ in range(p)]
-    dist.all_gather(outs, pad, group=engine.pg)
+    engine.coll.all_gather(outs, pad)
     return torch.cat([o[:s] for o, s in zip(outs, sizes)], 0)
 
 

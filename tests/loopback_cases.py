@@ -1,0 +1,130 @@
+"""Device-engine scenarios driven by p virtual ranks (threads) over LoopbackColl.
+
+Shared by tests/test_loopback_cpu.py (CPU tensors) and tests/test_loopback_gpu.py (one MI355X,
+real HIP kernels): a2a two-shot with rank-ordered reduce, fp8 / bf16 codecs, p2p
+gather/scatter/allgather-v, RCCL-shaped paths, sparse map / set ops.
+"""
+import threading
+
+import torch
+
+from mp4x import CommUtils, Operators
+from mp4x.operands import Operands
+from mp4x.operators import CustomOperator
+from mp4x.parallel.coll import loopback_engines
+
+
+def run_virtual(p, fn, device="cpu"):
+    engines = loopback_engines(p, device=device)
+    out = [None] * p
+    errs = []
+
+    def body(r):
+        try:
+            if device != "cpu":
+                torch.cuda.set_device(torch.device(device))
+            out[r] = fn(engines[r], r, p)
+        except BaseException as e:  # noqa
+            import traceback
+            errs.append(traceback.format_exc())
+            engines[r].coll.hub.bar.abort()
+
+    ths = [threading.Thread(target=body, args=(r,)) for r in range(p)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    if errs:
+        raise AssertionError(errs[0])
+    return out
+
+
+def dense_cases(eng, r, p):
+    dev = eng.device
+    n = 4099
+    for algo in ("rccl", "a2a"):
+        eng.algo = algo
+        t = torch.full((n,), float(r + 1), device=dev)
+        eng.allreduce(t, 2, n - 3, Operators.Float.SUM)
+        assert torch.all(t[2:n - 3] == p * (p + 1) / 2) and t[0] == r + 1
+    eng.algo = "auto"
+    x = torch.full((n,), 1 << r, dtype=torch.int16, device=dev)
+    eng.allreduce(x, 0, n, Operators.Short.BITS_OR)
+    assert torch.all(x == (1 << p) - 1)
+    # rank-ordered non-commutative op
+    op = CustomOperator(lambda a, b: a * 10 + b, vectorized=True)
+    t = torch.full((p * 5,), float(r + 1), dtype=torch.float64, device=dev)
+    eng.allreduce(t, 0, p * 5, op)
+    e = 1.0
+    for i in range(1, p):
+        e = e * 10 + (i + 1)
+    assert torch.all(t == e)
+    # ragged reduce-scatter / allgather, gather / scatter / broadcast / reduce
+    counts = [300 + 17 * i for i in range(p)]
+    fr = CommUtils.getFromsFromCount(1, counts, p)
+    to = CommUtils.getTosFromCount(1, counts, p)
+    t = torch.zeros(2 + sum(counts), device=dev)
+    for i in range(p):
+        t[fr[i]:to[i]] = i + 1
+    eng.reduce_scatter(t, fr, to, Operators.Float.SUM)
+    assert torch.all(t[fr[r]:to[r]] == (r + 1) * p)
+    t = torch.full((2 + sum(counts),), -1.0, device=dev)
+    t[fr[r]:to[r]] = r
+    eng.allgather(t, fr, to)
+    for i in range(p):
+        assert torch.all(t[fr[i]:to[i]] == i)
+    root = p - 1
+    t = torch.full((2 + sum(counts),), -1.0, device=dev)
+    t[fr[r]:to[r]] = r
+    eng.gather(t, fr, to, root)
+    if r == root:
+        for i in range(p):
+            assert torch.all(t[fr[i]:to[i]] == i)
+    t = torch.full((2 + sum(counts),), -1.0, device=dev)
+    if r == root:
+        for i in range(p):
+            t[fr[i]:to[i]] = i
+    eng.scatter(t, fr, to, root)
+    assert torch.all(t[fr[r]:to[r]] == r)
+    t = torch.full((n,), 7.0 if r == 0 else 0.0, device=dev)
+    eng.broadcast(t, 0, n, 0)
+    assert torch.all(t == 7)
+    t = torch.full((n,), 1 << r, dtype=torch.int64, device=dev)
+    eng.reduce(t, 0, n, Operators.Long.BITS_XOR, None, root)
+    if r == root:
+        assert torch.all(t == (1 << p) - 1)
+    return True
+
+
+def codec_cases(eng, r, p):
+    dev = eng.device
+    n = 256 * 40 + 64
+    g = torch.Generator(device=dev).manual_seed(100 + r)
+    x = torch.randn(n, device=dev, generator=g)
+    xs = [torch.randn(n, device=dev, generator=torch.Generator(device=dev).manual_seed(100 + j)) for j in range(p)]
+    ref = sum(xs)
+    y = x.clone()
+    eng.allreduce(y, 0, n, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="fp8"))
+    assert eng.stats.get("allreduce.fp8", 0) == 1
+    err = (y - ref).abs().max().item()
+    assert err < 0.25 * p, err                   # e4m3: ~2^-4 relative per block, twice quantised
+    z = x.clone()
+    eng.allreduce(z, 0, n, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="bf16"))
+    assert (z - ref).abs().max().item() < 0.05 * p
+    return True
+
+
+def sparse_cases(eng, r, p):
+    from mp4x.parallel.sparse import allreduce_sparse, set_intersection, set_union, allreduce_map_device
+    dev = eng.device
+    ids = torch.tensor(list(range(50)) + [10_000 + r], dtype=torch.int64, device=dev)
+    vals = torch.ones(51, 8, device=dev) * (r + 1)
+    k, v = allreduce_sparse(eng, ids, vals, Operators.Float.SUM)
+    got = dict(zip(k.tolist(), v[:, 0].tolist()))
+    assert len(got) == 50 + p and got[3] == p * (p + 1) / 2 and got[10_000 + r] == r + 1
+    u = set_union(eng, torch.tensor([r, 99, 99], dtype=torch.int64, device=dev))
+    assert sorted(u.tolist()) == sorted(set(range(p)) | {99})
+    i = set_intersection(eng, torch.tensor([4, 5, 77 + r], dtype=torch.int64, device=dev))
+    assert sorted(i.tolist()) == [4, 5]
+    m = {f"w{j}": torch.full((3,), float(r), device=dev) for j in range(20)}
+    out = allreduce_map_device(eng, m, Operators.Float.MAX)
+    assert len(out) == 20 and torch.all(out["w7"] == p - 1)
+    return True
