@@ -97,6 +97,10 @@ __device__ __forceinline__ void quant_block(const float (&x)[4], uint32_t* q, fl
   if (lane == 0) scales[blk] = scale;
 }
 
+// One wave per quant block; QU consecutive blocks per wave iteration so each lane keeps QU
+// 16-byte loads in flight before the first amax reduction.
+constexpr int QU = 4;
+
 template <int DT>
 __global__ __launch_bounds__(kBlock) void k_quant(const void* __restrict__ in, int64_t n, uint32_t* __restrict__ q,
                                                   float* __restrict__ scales) {
@@ -104,10 +108,14 @@ __global__ __launch_bounds__(kBlock) void k_quant(const void* __restrict__ in, i
   const int64_t nblk = (n + kQBlock - 1) / kQBlock;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t b = wave; b < nblk; b += nwaves) {
-    float x[4];
-    load4<DT>(in, b * kQBlock + lane * 4, n, x);
-    quant_block(x, q, scales, b, lane);
+  for (int64_t b0 = wave * QU; b0 < nblk; b0 += nwaves * QU) {
+    float x[QU][4];
+#pragma unroll
+    for (int u = 0; u < QU; ++u)
+      if (b0 + u < nblk) load4<DT>(in, (b0 + u) * kQBlock + lane * 4, n, x[u]);
+#pragma unroll
+    for (int u = 0; u < QU; ++u)
+      if (b0 + u < nblk) quant_block(x[u], q, scales, b0 + u, lane);
   }
 }
 

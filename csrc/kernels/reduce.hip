@@ -198,13 +198,19 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
       int g = grid_for(nvec > 0 ? nvec : 1, 2);
       hipLaunchKernelGGL((k_reduce_vec<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, nvec, n);
     } else {
-      // U vectors per lane: keep ~4-8 16-B loads in flight per lane
-      constexpr int U = NIN >= 4 ? 1 : (NIN == 1 ? 4 : 2);
-      int64_t per_block = (int64_t)kBlock * U;
+      // U vectors per lane: keep ~4-8 16-B loads in flight per lane (variant 3: ~8-16)
+      // measured (tools/bench_kernels.py --variants, profiles/r1/k1_variants2.txt): 4 vectors per
+      // lane for 1-2 inputs (6.1 / 6.4 TB/s), 1 vector per lane from 4 inputs up
+      constexpr int U = NIN >= 4 ? 1 : (NIN == 3 ? 2 : 4);
+      constexpr int U2 = NIN >= 8 ? 1 : (NIN >= 4 ? 2 : 4);
+      const int u = var == 3 ? U2 : U;
+      int64_t per_block = (int64_t)kBlock * u;
       int64_t g = (nvec + per_block - 1) / per_block;
       if (g < 1) g = 1;
       if (var == 1)
         hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, false>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
+      else if (var == 3)
+        hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U2, true>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
       else
         hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, true>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
     }

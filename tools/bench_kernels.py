@@ -50,10 +50,10 @@ def main():
     if a.variants:
         from mp4x.ops import native
         lib = native.hip()
-        names = {0: "gridstride_u2", 1: "tile", 2: "tile_nt"}
+        names = {0: "gridstride_u2", 1: "tile", 2: "tile_nt", 3: "tile_nt_u2x"}
         rounds = {}
         for rnd in range(3):
-            for v in (0, 1, 2):
+            for v in (2, 3):
                 lib.mp4x_set_k1_variant(v)
                 for nin in (1, 2, 4, 8):
                     ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
@@ -88,6 +88,14 @@ def main():
     ss = [s] * 8
     ms = timeit(lambda: K.dequant_reduce_fp8(out, qs, ss, n), a.iters)
     res["k6_dequant_reduce_fp8_nin8"] = {"ms": ms, "GBps": (8 * n + n * 4) / ms / 1e6}
+    # sparse K4/K5 pipeline: 8 ranks' worth of rows (1.6M x 64 f32) reduced by key
+    keys = torch.randint(0, 400_000, (1_600_000,), device=dev, dtype=torch.int64)
+    vals = torch.randn(1_600_000, 64, device=dev)
+    ms = timeit(lambda: K.reduce_by_key(keys, vals, int(OpCode.SUM)), max(3, a.iters // 4))
+    res["k5_reduce_by_key_1.6Mx64"] = {"ms": ms, "GBps": (vals.numel() * 4 * 2 + keys.numel() * 8 * 4) / ms / 1e6}
+    idx = torch.randperm(1_600_000, device=dev)
+    ms = timeit(lambda: K.gather_rows(vals, idx), a.iters)
+    res["k3_gather_rows_1.6Mx64"] = {"ms": ms, "GBps": vals.numel() * 4 * 2 / ms / 1e6}
     print(json.dumps(res, indent=1))
 
 
