@@ -111,7 +111,7 @@ class DeviceEngine:
             self.backend = backend or os.environ.get("MP4X_DEVICE_BACKEND") or ("nccl" if use_cuda else "gloo")
             if use_cuda:
                 if device_index is None:
-                    lr = os.environ.get("LOCAL_RANK")
+                    lr = os.environ.get("MP4X_DEVICE_INDEX", os.environ.get("LOCAL_RANK"))
                     device_index = int(lr) if lr is not None else self.rank % torch.cuda.device_count()
                 torch.cuda.set_device(device_index)
                 self.device = torch.device("cuda", device_index)
