@@ -132,7 +132,7 @@ def main():
     factor = 2.0 * (p - 1) / p if p > 1 else 1.0
     busbw = algbw * factor
     ref = REF_BUSBW_MBPS.get(p)
-    algo = "copy" if p == 1 else ("host-tcp" if args.cpu else
+    algo = "k1_copy (out-of-place, 1 rank)" if p == 1 else ("host-tcp" if args.cpu else
                                   comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand))
     if rank == 0:
         rec = {

@@ -32,7 +32,25 @@ __global__ __launch_bounds__(kBlock) void k_segment_copy(char* __restrict__ dst,
   }
 }
 
-// One wave64 per row; lanes move 16-byte words.
+// Lane groups: a row of V 16-byte vectors is moved by G = min(64, pow2 >= V) lanes, so a
+// wave moves 64/G rows at once (256-B rows: 4 rows / wave-instruction, every lane busy).
+__global__ __launch_bounds__(kBlock) void k_gather_rows_vec(u32x4* __restrict__ out, const u32x4* __restrict__ in,
+                                                            const int64_t* __restrict__ idx, int64_t nrows, int64_t V,
+                                                            int G) {
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / G, sub = lane % G, R = 64 / G;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t r0 = wave * R; r0 < nrows; r0 += nwaves * R) {
+    const int64_t r = r0 + grp;
+    if (r >= nrows) continue;
+    const u32x4* s = in + idx[r] * V;
+    u32x4* d = out + r * V;
+    for (int64_t v = sub; v < V; v += G) __builtin_nontemporal_store(s[v], d + v);
+  }
+}
+
+// One wave64 per row; lanes move 16-byte words (fallback for unaligned / odd-sized rows).
 __global__ __launch_bounds__(kBlock) void k_gather_rows(char* __restrict__ out, const char* __restrict__ in,
                                                         const int64_t* __restrict__ idx, int64_t nrows,
                                                         int64_t row_bytes) {
@@ -71,6 +89,16 @@ extern "C" int mp4x_segment_copy(void* dst, const void* src, const int64_t* dev_
 extern "C" int mp4x_gather_rows(void* out, const void* in, const int64_t* idx, int64_t nrows, int64_t row_bytes,
                                 void* stream) {
   if (nrows <= 0 || row_bytes <= 0) return 0;
+  if ((row_bytes & 15) == 0 && ((((uintptr_t)out | (uintptr_t)in) & 15) == 0)) {
+    const int64_t V = row_bytes / 16;
+    int G = 1;
+    while (G < V && G < 64) G <<= 1;
+    const int64_t waves = (nrows * G + 63) / 64;
+    int g = grid_for(waves * 64, 1);
+    hipLaunchKernelGGL(k_gather_rows_vec, dim3(g), dim3(kBlock), 0, (hipStream_t)stream, (u32x4*)out,
+                       (const u32x4*)in, idx, nrows, V, G);
+    return (int)hipGetLastError();
+  }
   int g = grid_for(nrows * 64, 1);
   hipLaunchKernelGGL(k_gather_rows, dim3(g), dim3(kBlock), 0, (hipStream_t)stream, (char*)out, (const char*)in, idx,
                      nrows, row_bytes);

@@ -74,6 +74,68 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce(const int64_t* __rest
   }
 }
 
+// Vectorised form: rows of V 16-byte vectors, G lanes per run (64/G runs per wave), each lane
+// accumulates one 16-byte vector of the row across the run's rows (2 rows per step in flight).
+template <int DT, int OP>
+__global__ __launch_bounds__(kBlock) void k_segment_reduce_vec(const int64_t* __restrict__ sk,
+                                                               const int64_t* __restrict__ perm,
+                                                               const int64_t* __restrict__ starts,
+                                                               const int64_t* __restrict__ nruns_dev, int64_t n,
+                                                               const u32x4* __restrict__ vals, int64_t V, int G,
+                                                               int64_t* __restrict__ out_keys,
+                                                               u32x4* __restrict__ out_vals,
+                                                               int32_t* __restrict__ out_count) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  using A = typename E::A;
+  constexpr int W = 16 / sizeof(S);
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / G, sub = lane % G, R = 64 / G;
+  const int64_t nruns = *nruns_dev;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t u0 = wave * R; u0 < nruns; u0 += nwaves * R) {
+    const int64_t u = u0 + grp;
+    if (u >= nruns) continue;
+    const int64_t s = starts[u];
+    const int64_t e = (u + 1 < nruns) ? starts[u + 1] : n;
+    if (sub == 0) {
+      out_keys[u] = sk[s];
+      if (out_count) out_count[u] = (int32_t)(e - s);
+    }
+    for (int64_t v = sub; v < V; v += G) {
+      S x[W];
+      u32x4 t = vals[perm[s] * V + v];
+      __builtin_memcpy(x, &t, 16);
+      A acc[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = E::load(x[j]);
+      int64_t j = s + 1;
+      for (; j + 1 < e; j += 2) {          // two rows in flight
+        u32x4 t0 = vals[perm[j] * V + v];
+        u32x4 t1 = vals[perm[j + 1] * V + v];
+        S y0[W], y1[W];
+        __builtin_memcpy(y0, &t0, 16);
+        __builtin_memcpy(y1, &t1, 16);
+#pragma unroll
+        for (int q = 0; q < W; ++q) acc[q] = combine<DT, OP>(combine<DT, OP>(acc[q], E::load(y0[q])), E::load(y1[q]));
+      }
+      if (j < e) {
+        u32x4 t0 = vals[perm[j] * V + v];
+        S y0[W];
+        __builtin_memcpy(y0, &t0, 16);
+#pragma unroll
+        for (int q = 0; q < W; ++q) acc[q] = combine<DT, OP>(acc[q], E::load(y0[q]));
+      }
+#pragma unroll
+      for (int q = 0; q < W; ++q) x[q] = E::store(acc[q]);
+      u32x4 o;
+      __builtin_memcpy(&o, x, 16);
+      out_vals[u * V + v] = o;
+    }
+  }
+}
+
 template <int DT, int OP>
 static int launch_sr(const int64_t* sk, const int64_t* perm, const int64_t* starts, const int64_t* nr, int64_t n,
                      int64_t max_runs, const void* vals, int64_t dim, int64_t* ok, void* ov, int32_t* oc,
@@ -81,6 +143,17 @@ static int launch_sr(const int64_t* sk, const int64_t* perm, const int64_t* star
   if constexpr (!op_valid<DT, OP>()) {
     return MP4X_E_UNSUPPORTED;
   } else {
+    using S = typename Elem<DT>::S;
+    const int64_t row_bytes = dim * (int64_t)sizeof(S);
+    if (vals && (row_bytes & 15) == 0 && ((((uintptr_t)vals | (uintptr_t)ov) & 15) == 0)) {
+      const int64_t V = row_bytes / 16;
+      int G = 1;
+      while (G < V && G < 64) G <<= 1;
+      int g = grid_for((max_runs * G + 63) / 64 * 64, 1);
+      hipLaunchKernelGGL((k_segment_reduce_vec<DT, OP>), dim3(g), dim3(kBlock), 0, st, sk, perm, starts, nr, n,
+                         (const u32x4*)vals, V, G, ok, (u32x4*)ov, oc);
+      return (int)hipGetLastError();
+    }
     int g = grid_for(max_runs * 64, 1);
     hipLaunchKernelGGL((k_segment_reduce<DT, OP>), dim3(g), dim3(kBlock), 0, st, sk, perm, starts, nr, n, vals, dim,
                        ok, ov, oc);
