@@ -176,6 +176,98 @@ static int sr_dt(int op, const int64_t* sk, const int64_t* perm, const int64_t* 
   }
 }
 
+
+// K4b — fused owner partition + pack (LDS multisplit).  Replaces owner -> radix sort by
+// owner -> two row gathers with three passes over the keys and ONE pass over the rows:
+//   k_pack_hist     per-256-key tile LDS histogram -> hist[d * nblk + tile] (no global atomics)
+//   DeviceScan      exclusive sum over (owner-major, tile-minor) -> every (owner, tile) base
+//   k_pack_scatter  per wave, a ballot "match" loop ranks lanes that share an owner (stable:
+//                   lane order), per-wave counts go through LDS for the block prefix; keys
+//                   scatter directly, destination row offsets are staged in LDS and the rows
+//                   then move with lane groups (contiguous 16-B loads, nontemporal stores).
+// The result is exactly the stable sort by owner (same layout as the radix-sort path) with
+// no contended atomics: deterministic run to run.
+constexpr int kPackMaxP = 2048;
+
+__device__ __forceinline__ int owner_of(int64_t k, int p) { return (int)((uint64_t)k % (uint64_t)p); }
+
+__global__ __launch_bounds__(kBlock) void k_pack_hist(const int64_t* __restrict__ keys, int64_t n, int p, int64_t nblk,
+                                                      int64_t* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) int32_t lh[];
+  for (int i = threadIdx.x; i < p; i += kBlock) lh[i] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) atomicAdd(&lh[owner_of(keys[i], p)], 1);
+  __syncthreads();
+  for (int d = threadIdx.x; d < p; d += kBlock) hist[(int64_t)d * nblk + blockIdx.x] = lh[d];
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restrict__ keys,
+                                                         const u32x4* __restrict__ vals, int64_t n, int64_t V,
+                                                         int G, int p, int64_t nblk,
+                                                         const int64_t* __restrict__ off,
+                                                         const int64_t* __restrict__ hist,
+                                                         int64_t* __restrict__ out_keys,
+                                                         u32x4* __restrict__ out_vals,
+                                                         int64_t* __restrict__ out_perm,
+                                                         int64_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int32_t* wcnt = reinterpret_cast<int32_t*>(smem);                         // [4][p]
+  int64_t* pos = reinterpret_cast<int64_t*>(smem + ((4 * p * 4 + 15) & ~15));  // [kBlock]
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int64_t b = blockIdx.x, t0 = b * kBlock, i = t0 + tid;
+  const bool valid = i < n;
+  for (int j = tid; j < 4 * p; j += kBlock) wcnt[j] = 0;
+  __syncthreads();
+  const int64_t k = valid ? keys[i] : 0;
+  const int d = valid ? owner_of(k, p) : -1;
+  uint64_t active = __ballot(valid);
+  int rank = 0;
+  while (active) {                       // wave-uniform: one trip per distinct owner in the wave
+    const int leader = __ffsll((unsigned long long)active) - 1;
+    const int ld = __shfl(d, leader);
+    const uint64_t m = __ballot(d == ld) & active;
+    if (d == ld) rank = __popcll(m & ((1ull << lane) - 1));
+    if (lane == leader) wcnt[w * p + ld] = __popcll(m);
+    active &= ~m;
+  }
+  __syncthreads();
+  if (valid) {
+    int inb = rank;
+    for (int q = 0; q < w; ++q) inb += wcnt[q * p + d];
+    const int64_t ps = off[(int64_t)d * nblk + b] + inb;
+    out_keys[ps] = k;
+    if (out_perm) out_perm[ps] = i;
+    pos[tid] = ps;
+  }
+  if (b == 0 && counts)
+    for (int q = tid; q < p; q += kBlock) {
+      const int64_t last = (int64_t)p * nblk - 1;
+      const int64_t end = (q + 1 < p) ? off[(int64_t)(q + 1) * nblk] : off[last] + hist[last];
+      counts[q] = end - off[(int64_t)q * nblk];
+    }
+  if (!vals) return;
+  __syncthreads();
+  const int64_t rows = (n - t0) < kBlock ? (n - t0) : kBlock;
+  const int grp = lane / G, sub = lane % G, R = 64 / G;
+  constexpr int UNR = 4;
+  for (int r0 = w * R + grp; r0 < rows; r0 += 4 * R * UNR) {
+    for (int64_t v = sub; v < V; v += G) {
+      u32x4 x[UNR];
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * 4 * R;
+        if (r < rows) x[u] = __builtin_nontemporal_load(vals + (t0 + r) * V + v);
+      }
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * 4 * R;
+        if (r < rows) __builtin_nontemporal_store(x[u], out_vals + pos[r] * V + v);
+      }
+    }
+  }
+}
+
 }  // namespace mp4x
 
 using namespace mp4x;
@@ -249,4 +341,47 @@ extern "C" int mp4x_segment_reduce_rows(int dtype, int op, const int64_t* sk, co
     case MP4X_F16: return sr_dt<MP4X_F16>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
     default: return MP4X_E_UNSUPPORTED;
   }
+}
+
+static size_t pack_align(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p) {
+  const int64_t nblk = (n + kBlock - 1) / kBlock;
+  const int64_t m = (int64_t)p * (nblk < 1 ? 1 : nblk);
+  size_t cub_bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)m,
+                                         (hipStream_t)0);
+  return 2 * pack_align(m * sizeof(int64_t)) + pack_align(cub_bytes);
+}
+
+// keys[n] (+ rows vals[n][row_bytes]) -> stable-by-owner layout out_keys / out_vals, optional
+// out_perm (source index of every output slot) and counts[p] (rows per owner).
+extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
+                                   int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts,
+                                   void* scratch, size_t scratch_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (p < 1 || p > kPackMaxP) return MP4X_E_BADARG;
+  if (n <= 0) return counts ? (int)hipMemsetAsync(counts, 0, p * sizeof(int64_t), st) : 0;
+  if (n > INT32_MAX / 2) return MP4X_E_BADARG;
+  if (vals && ((row_bytes & 15) || ((((uintptr_t)vals | (uintptr_t)out_vals) & 15)))) return MP4X_E_BADARG;
+  if (scratch_bytes < mp4x_partition_pack_scratch_bytes(n, p)) return MP4X_E_BADARG;
+  const int64_t nblk = (n + kBlock - 1) / kBlock;
+  const int64_t m = (int64_t)p * nblk;
+  char* sc = (char*)scratch;
+  int64_t* hist = (int64_t*)sc;
+  int64_t* off = (int64_t*)(sc + pack_align(m * sizeof(int64_t)));
+  void* temp = sc + 2 * pack_align(m * sizeof(int64_t));
+  size_t temp_bytes = scratch_bytes - 2 * pack_align(m * sizeof(int64_t));
+  hipLaunchKernelGGL(k_pack_hist, dim3(nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, nblk, hist);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, off, (int)m, st);
+  if (e) return e;
+  const int64_t V = vals ? row_bytes / 16 : 0;
+  int G = 1;
+  while (G < V && G < 64) G <<= 1;
+  const size_t lds = ((4 * p * 4 + 15) & ~15) + kBlock * sizeof(int64_t);
+  hipLaunchKernelGGL(k_pack_scatter, dim3(nblk), dim3(kBlock), lds, st, keys, (const u32x4*)vals, n, V, G, p, nblk,
+                     off, hist, out_keys, (u32x4*)out_vals, out_perm, counts);
+  return (int)hipGetLastError();
 }

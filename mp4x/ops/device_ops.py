@@ -179,6 +179,50 @@ def key_owner(keys: torch.Tensor, p: int, stream=None):
     return dest, hist
 
 
+PACK_MAX_P = 2048
+
+
+def partition_pack(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, want_perm: bool = False,
+                   stream=None):
+    """Fused K4b stable partition by owner ``(uint64)key % p``.
+
+    Returns ``(out_keys, out_vals, counts int64[p], perm)``; ``out_vals`` is None when
+    ``vals`` is None, ``perm`` (source row of each slot) only with ``want_perm``.  Rows whose
+    size is not a multiple of 16 bytes are packed with :func:`gather_rows` through ``perm``.
+    """
+    _dev_check(keys, vals)
+    if keys.dtype != torch.int64:
+        raise ValueError("partition_pack: keys must be int64")
+    if not 1 <= p <= PACK_MAX_P:
+        raise ValueError(f"partition_pack: p must be in [1, {PACK_MAX_P}]")
+    n = keys.numel()
+    dev = keys.device
+    keys = keys.contiguous()
+    row_bytes = 0
+    fused_rows = False
+    if vals is not None:
+        if vals.shape[0] != n:
+            raise ValueError("partition_pack: vals rows != keys")
+        vals = vals.contiguous()
+        row_bytes = (vals[0].numel() if n else 0) * vals.element_size()
+        fused_rows = row_bytes % 16 == 0 and row_bytes > 0
+    need_perm = want_perm or (vals is not None and not fused_rows)
+    out_keys = torch.empty(n, dtype=torch.int64, device=dev)
+    out_vals = torch.empty_like(vals) if vals is not None else None
+    perm = torch.empty(n, dtype=torch.int64, device=dev) if need_perm else None
+    counts = torch.empty(p, dtype=torch.int64, device=dev)
+    lib = native.hip()
+    sb = lib.mp4x_partition_pack_scratch_bytes(n, p)
+    scratch = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
+    check(lib.mp4x_partition_pack(keys.data_ptr(), vals.data_ptr() if fused_rows else None, n, row_bytes, p,
+                                  out_keys.data_ptr(), out_vals.data_ptr() if fused_rows else None,
+                                  perm.data_ptr() if perm is not None else None, counts.data_ptr(),
+                                  scratch.data_ptr(), sb, stream_ptr(stream)), "mp4x_partition_pack")
+    if vals is not None and not fused_rows and n:
+        gather_rows(vals.view(n, -1), perm, out=out_vals.view(n, -1), stream=stream)
+    return out_keys, out_vals, counts, perm
+
+
 def sort_pairs(keys: torch.Tensor, idx: Optional[torch.Tensor] = None, end_bit: Optional[int] = None, stream=None):
     """Stable radix sort of int64 (or int32) keys with an int64 payload (default arange)."""
     _dev_check(keys)

@@ -12,7 +12,12 @@ Algorithms follow the reference's schedules (Thakur/Rabenseifner/Gropp):
 * gather on the same tree reversed — deterministic, no master pairing (the
   reference's ``dynamicBinaryTreeGather`` pairs ranks through the master's
   Exchanger, ProcessCommSlave.java:440-520);
-* map variants of all of the above with per-key merge/reduce.
+* map variants of all of the above with per-key merge/reduce;
+* recursive halving / doubling allreduce (Rabenseifner) for built-in operators: 2·log2(p)
+  message rounds instead of the ring's 2(p−1), with the same bandwidth-optimal
+  2(p−1)/p·S bytes per rank when p is a power of two; other p fold the excess ranks into
+  their neighbours first.  ``ProcessCommSlave`` picks it by size and p
+  (:func:`choose_allreduce`).
 
 All routines work in place on the caller's array and are tag-matched, so no
 master barrier is needed after every collective (the reference ends each ring
@@ -43,6 +48,29 @@ def _write_segment(arr, f: int, t: int, data) -> None:
         arr[f:t] = data
     else:
         arr[f:t] = list(data)
+
+
+RHD_MAX_BYTES_DEFAULT = 64 << 10
+
+
+def choose_allreduce(p: int, nbytes: int, custom: bool) -> str:
+    """``ring`` or ``rhd`` for a host allreduce of ``nbytes`` on ``p`` ranks.
+
+    Custom (possibly non-commutative) operators keep the reference's ring.  Power-of-two p:
+    RHD always (fewer rounds, same bytes).  Otherwise RHD only below ``MP4X_RHD_MAX_BYTES``
+    (default 64 KiB; measured crossover for p = 6 lies between 8 and 256 KiB), where latency dominates the fold's extra full-message transfer.
+    ``MP4X_HOST_ALGO=ring|rhd`` forces one.
+    """
+    import os
+    forced = os.environ.get("MP4X_HOST_ALGO", "").lower()
+    if forced in ("ring", "rhd"):
+        return forced
+    if custom or p <= 2:
+        return "ring" if custom else "rhd"
+    if p & (p - 1) == 0:
+        return "rhd"
+    lim = int(os.environ.get("MP4X_RHD_MAX_BYTES", RHD_MAX_BYTES_DEFAULT))
+    return "rhd" if nbytes <= lim else "ring"
 
 
 class HostEngine:
@@ -87,6 +115,66 @@ class HostEngine:
                 _reduce_segment(arr, f, t, data, op)
             if step < p - 1:
                 self.t.send(nxt, tag, wire.pack_segments(arr, [(r, froms[b], tos[b])], operand))
+        return arr
+
+    def rhd_allreduce(self, arr, frm: int, to: int, operand: Operand, op):
+        """Recursive-halving reduce-scatter + recursive-doubling allgather on [frm, to).
+
+        Ranks fold to the largest power of two p2 <= p: for r < 2(p − p2), odd r hands its
+        range to r − 1 first and receives the result last.  Every block is reduced by exactly
+        one rank and copied to the others, so all ranks end bit-identical.
+        """
+        p, r = self.p, self.rank
+        if p == 1 or to <= frm:
+            return arr
+        t_fold, t_rs, t_ag = self.next_tag(), self.next_tag(), self.next_tag()
+        p2 = 1 << (p.bit_length() - 1)
+        rem = p - p2
+
+        def real(v):
+            return 2 * v if v < rem else v + rem
+
+        def send(dst, tag, f, t):
+            self.t.send(dst, tag, wire.pack_segments(arr, [(r, f, t)], operand))
+
+        def recv(src, tag, reduce):
+            for _, f, t, data in wire.unpack_segments(self.t.recv(src, tag), operand):
+                if reduce:
+                    _reduce_segment(arr, f, t, data, op)
+                else:
+                    _write_segment(arr, f, t, data)
+
+        if r < 2 * rem:
+            if r % 2:
+                send(r - 1, t_fold, frm, to)
+                recv(r - 1, t_fold, False)
+                return arr
+            recv(r + 1, t_fold, True)
+            vr = r // 2
+        else:
+            vr = r - rem
+        lo, hi = frm, to
+        mask = p2 >> 1
+        steps = []
+        while mask:
+            partner = real(vr ^ mask)
+            mid = lo + (hi - lo) // 2
+            keep, give = ((lo, mid), (mid, hi)) if not vr & mask else ((mid, hi), (lo, mid))
+            if give[1] > give[0]:
+                send(partner, t_rs, *give)
+            if keep[1] > keep[0]:
+                recv(partner, t_rs, True)
+            steps.append((partner, give))
+            lo, hi = keep
+            mask >>= 1
+        for partner, give in reversed(steps):
+            if hi > lo:
+                send(partner, t_ag, lo, hi)
+            if give[1] > give[0]:
+                recv(partner, t_ag, False)
+            lo, hi = min(lo, give[0]), max(hi, give[1])
+        if r < 2 * rem:
+            send(r + 1, t_fold, frm, to)
         return arr
 
     def tree_scatter(self, arr, froms, tos, operand: Operand, root: int):

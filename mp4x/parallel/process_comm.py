@@ -39,7 +39,7 @@ from ..operands import Operand, Operands, Serializer, DEFAULT_SERIALIZER
 from ..operators import CustomOperator, DType, Operator, dtype_of_numpy
 from ..utils.commutils import CommUtils
 from ..utils.hashing import owner_of
-from .host_engine import HostEngine
+from .host_engine import HostEngine, choose_allreduce
 from .transport import HostTransport
 from . import wire
 
@@ -585,6 +585,10 @@ class ProcessCommSlave:
         shm = self._shm_engine(buf, operand, operator, to - frm)
         if shm is not None and buf.flags.c_contiguous:
             shm.allreduce(buf, frm, to, int(operand.dtype), int(operator.code))
+            return arrData
+        nbytes = (to - frm) * (buf.itemsize if isinstance(buf, np.ndarray) else 64)
+        if choose_allreduce(self.slaveNum, nbytes, getattr(operator, "is_custom", False)) == "rhd":
+            self.engine.rhd_allreduce(buf, frm, to, operand, operator)
             return arrData
         froms, tos, _ = CommUtils.even_split(frm, to, self.slaveNum)
         self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)

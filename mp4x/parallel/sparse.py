@@ -11,9 +11,10 @@ Device design (one process per GPU):
   are exchanged (host allgather), so a steady-state embedding / histogram sync moves no
   strings at all;
 * values live in one ``[n, dim]`` device tensor (``Map<String, float[]>`` rows);
-* owner of a key = ``id % p`` (kernel K4: owner + LDS histogram), rows are sorted by owner
-  with a stable hipCUB radix sort and exchanged with ONE ragged all-to-all over RCCL
-  (every link busy at once, no ring);
+* owner of a key = ``(uint64)id % p``; kernel K4b partitions keys AND rows by owner in one
+  fused LDS-multisplit pass (stable, deterministic; the hipCUB radix-sort K4 path remains
+  as the fallback) and they are exchanged with ONE ragged all-to-all over RCCL (every link
+  busy at once, no ring);
 * each owner reduces its rows with the deterministic reduce-by-key kernel K5 (stable sort
   by id, one wave per key, rows combined in source-rank order);
 * owned results are all-gathered; ownership is disjoint, so the union needs no merge.
@@ -108,6 +109,15 @@ def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op):
     return uk, out, cnt.to(torch.int32)
 
 
+def _owner(keys: torch.Tensor, p: int) -> torch.Tensor:
+    """CPU twin of the device owner ``(uint64)id % p`` (ids are int64 two's complement)."""
+    dest = torch.remainder(keys, p)
+    wrap = (1 << 64) % p
+    if wrap:
+        dest = torch.where(keys < 0, torch.remainder(dest + wrap, p), dest)
+    return dest
+
+
 def _owner_order(keys: torch.Tensor, p: int):
     """(perm sorting rows by owner, per-owner counts) — kernels K4 + stable radix sort."""
     if keys.is_cuda:
@@ -116,9 +126,26 @@ def _owner_order(keys: torch.Tensor, p: int):
         bits = max(1, int(p - 1).bit_length())
         _, perm = sort_pairs(dest, end_bit=bits)
         return perm, hist.to(torch.int64)
-    dest = torch.remainder(keys, p)
+    dest = _owner(keys, p)
     perm = torch.argsort(dest, stable=True)
     return perm, torch.bincount(dest, minlength=p)
+
+
+def _pack_by_owner(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int):
+    """(keys, rows) in stable owner-major order + per-owner counts.
+
+    GPU: one fused K4b launch chain (LDS multisplit, :func:`mp4x.ops.device_ops.partition_pack`);
+    the sort-based K4 path remains for p beyond the fused kernel's LDS budget and on CPU.
+    """
+    if keys.is_cuda:
+        from ..ops.device_ops import PACK_MAX_P, partition_pack
+        if p <= PACK_MAX_P:
+            sk, sv, counts, _ = partition_pack(keys, vals, p)
+            return sk, sv, counts
+    perm, hist = _owner_order(keys, p)
+    skeys = _gather_rows(keys.view(-1, 1), perm).view(-1)
+    svals = _gather_rows(vals, perm) if vals is not None else None
+    return skeys, svals, hist
 
 
 def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
@@ -131,9 +158,7 @@ def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 # ------------------------------------------------------------------ tensor-level API
 def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor]):
     p = engine.p
-    perm, hist = _owner_order(keys, p)
-    skeys = _gather_rows(keys.view(-1, 1), perm).view(-1)
-    svals = _gather_rows(vals, perm) if vals is not None else None
+    skeys, svals, hist = _pack_by_owner(keys, vals, p)
     recv_counts = torch.empty_like(hist)
     engine.coll.all_to_all_single(recv_counts, hist)
     send = hist.tolist()

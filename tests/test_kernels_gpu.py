@@ -205,3 +205,40 @@ def test_key_owner_hist():
     dest, hist = K.key_owner(keys, 7)
     assert torch.equal(dest.long(), keys % 7)
     assert torch.equal(hist.long(), torch.bincount(keys % 7, minlength=7))
+
+
+def _owner_ref(keys, p):
+    from mp4x.parallel.sparse import _owner
+    return _owner(keys.cpu(), p).to(keys.device)
+
+
+@pytest.mark.parametrize("p", [1, 3, 8, 1000])
+@pytest.mark.parametrize("n", [0, 1, 255, 257, 70_001])
+@pytest.mark.parametrize("dim,dtype", [(64, torch.float32), (3, torch.float32), (8, torch.bfloat16), (0, None)])
+def test_partition_pack_is_stable_sort_by_owner(p, n, dim, dtype):
+    """K4b fused LDS multisplit == stable argsort by (uint64)key % p (negative ids included)."""
+    K = _native()
+    g = torch.Generator(device="cpu").manual_seed(n * 31 + p)
+    keys = torch.randint(-(1 << 62), 1 << 62, (n,), generator=g, dtype=torch.int64).to(DEV)
+    vals = torch.randn(n, dim, generator=g).to(DEV, dtype) if dim else None
+    sk, sv, counts, perm = K.partition_pack(keys, vals, p, want_perm=True)
+    dest = _owner_ref(keys, p)
+    ref = torch.argsort(dest, stable=True)
+    assert torch.equal(perm, ref)
+    assert torch.equal(sk, keys[ref])
+    assert torch.equal(counts, torch.bincount(dest, minlength=p))
+    if vals is not None:
+        assert torch.equal(sv, vals[ref])
+    else:
+        assert sv is None
+
+
+def test_partition_pack_matches_sort_path():
+    K = _native()
+    keys = torch.randint(0, 1 << 62, (100_000,), device=DEV, dtype=torch.int64)
+    vals = torch.randn(100_000, 16, device=DEV)
+    dest, hist = K.key_owner(keys, 8)
+    _, perm = K.sort_pairs(dest, end_bit=3)
+    sk, sv, counts, _ = K.partition_pack(keys, vals, 8)
+    assert torch.equal(sk, keys[perm]) and torch.equal(sv, vals[perm])
+    assert torch.equal(counts, hist.long())

@@ -97,3 +97,25 @@ def test_random_collectives_match_numpy(p, seed):
 def test_random_collectives_shared_memory(p, seed):
     res, code, _ = run_ranks(p, random_cases, (seed, 40), timeout=240, env={"MP4X_SHM_MIN_BYTES": "0"})
     assert code == 0
+
+
+@pytest.mark.parametrize("algo,p,seed", [("ring", 4, 31), ("rhd", 3, 32), ("rhd", 6, 33), ("rhd", 7, 34),
+                                         ("ring", 7, 35)])
+def test_random_collectives_forced_host_allreduce_algo(algo, p, seed):
+    """Both host allreduce schedules (ring / recursive halving-doubling with fold) vs NumPy."""
+    res, code, _ = run_ranks(p, random_cases, (seed, 30), timeout=240, env={"MP4X_HOST_ALGO": algo})
+    assert code == 0 and all(v == 30 for v in res.values())
+
+
+def _float_allreduce_digest(comm, n):
+    import hashlib
+    r = comm.getRank()
+    a = np.random.default_rng(r).standard_normal(n)
+    comm.allreduceArray(a, Operands.DOUBLE_OPERAND(), Operators.Double.SUM, 0, n)
+    return hashlib.sha1(a.tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("algo,p", [("rhd", 5), ("rhd", 8), ("ring", 5)])
+def test_host_allreduce_bit_identical_across_ranks(algo, p):
+    res, code, _ = run_ranks(p, _float_allreduce_digest, (10_001,), timeout=120, env={"MP4X_HOST_ALGO": algo})
+    assert code == 0 and len(set(res.values())) == 1

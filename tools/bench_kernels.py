@@ -96,6 +96,20 @@ def main():
     idx = torch.randperm(1_600_000, device=dev)
     ms = timeit(lambda: K.gather_rows(vals, idx), a.iters)
     res["k3_gather_rows_1.6Mx64"] = {"ms": ms, "GBps": vals.numel() * 4 * 2 / ms / 1e6}
+    # K4 owner partition of one rank's map (200k keys x 64 f32) for p = 8: sort path vs fused K4b
+    pk = torch.randint(0, 1 << 62, (200_000,), device=dev, dtype=torch.int64)
+    pv = torch.randn(200_000, 64, device=dev)
+
+    def sort_path():
+        dest, _ = K.key_owner(pk, 8)
+        _, perm = K.sort_pairs(dest, end_bit=3)
+        K.gather_rows(pk.view(-1, 1), perm)
+        K.gather_rows(pv, perm)
+
+    ms = timeit(sort_path, a.iters)
+    res["k4_owner_sort_gather_200kx64_p8"] = {"ms": ms, "GBps": pv.numel() * 4 * 2 / ms / 1e6}
+    ms = timeit(lambda: K.partition_pack(pk, pv, 8), a.iters)
+    res["k4b_partition_pack_200kx64_p8"] = {"ms": ms, "GBps": pv.numel() * 4 * 2 / ms / 1e6}
     print(json.dumps(res, indent=1))
 
 
