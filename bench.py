@@ -8,8 +8,10 @@ per GPU with ``torch.distributed.run``.  Every step is ONE public-API call
 
 on a 1e9-byte float32 array (250,000,000 elements, synthetic random data) resident on the
 rank's MI355X, i.e. the reference's ``ProcessCommSlave.allreduceArray`` on the BASELINE
-config.  Timing: W untimed warmup calls, barrier + device sync, K timed calls with a
-hipEvent pair around each (p50 / p99), barrier + sync; MAX over ranks.
+config.  For N>1 the warm-up first autotunes the schedule (RCCL, IPC two-shot over xGMI,
+a2a two-shot; MAX time over ranks, on a scratch tensor).  Timing: W untimed warmup calls,
+barrier + device sync, K timed calls with a hipEvent pair around each (p50 / p99),
+barrier + sync; MAX over ranks.
 
 busbw follows the nccl-tests convention used in BASELINE.md: algbw = bytes / t,
 busbw = algbw * 2(p-1)/p.  ``value`` is the whole-job aggregate ``N * busbw``.
@@ -53,6 +55,8 @@ def main():
     ap.add_argument("--algo", default=None, help="force device algorithm: rccl | a2a")
     ap.add_argument("--codec", default=None, help="wire codec for the fp8-compressed config: fp8")
     ap.add_argument("--cpu", action="store_true", help="dry run of the launch/rendezvous path on CPU (gloo)")
+    ap.add_argument("--no-autotune", action="store_true",
+                    help="skip the warm-up schedule autotune (RCCL vs IPC two-shot vs a2a) for N>1")
     args = ap.parse_args()
     if args.algo:
         os.environ["MP4X_DEVICE_ALGO"] = args.algo
@@ -98,8 +102,14 @@ def main():
             comm.peer_barrier() if args.cpu else comm.device.barrier()
             torch.cuda.synchronize()
 
+    tuned = None
     if p > 1 and not args.cpu:
         comm.device  # bring up the RCCL communicator before timing
+        if not (args.no_autotune or args.algo or args.codec):
+            # untimed: measure every applicable schedule on a scratch tensor of this shape and
+            # pin the fastest (all ranks agree: MAX over ranks); the timed steps run it in full
+            tuned = {k: round(v * 1e3, 3) for k, v in
+                     comm.device.autotune_allreduce(buf, op, iters=2).items()}
     for _ in range(args.warmup):
         step()
     sync_all()
@@ -151,7 +161,7 @@ def main():
             "config": {"model": "allreduceArray float[250000000] (1e9 bytes), Operators.Float.SUM",
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
                        "payload_bytes": nbytes, "algo": algo,
-                       "in_place": p > 1},
+                       "in_place": p > 1, "autotune_ms": tuned},
             "busbw_gbps_per_rank": round(busbw, 3),
             "algbw_gbps": round(algbw, 3),
             "p50_ms": round(p50, 4),

@@ -17,17 +17,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(port, q, sizes, iters):
+def worker(port, q, sizes, iters, buf_bytes=64 << 20, algos=(0, 1)):
     import torch
     from mp4x import ProcessCommSlave, Operators
     from mp4x.parallel.ipc import IpcAllreduce
     torch.cuda.set_device(0)
     comm = ProcessCommSlave("b", "127.0.0.1", port, heartbeat=False)
-    ipc = IpcAllreduce(comm, nbytes=64 << 20).prepare_graph()
+    ipc = IpcAllreduce(comm, nbytes=buf_bytes).prepare_graph()
     out = []
     for nbytes in sizes:
         x = torch.randn(nbytes // 4, device="cuda")
-        for algo in (0, 1):
+        for algo in algos:
             for _ in range(5):
                 ipc.allreduce(x, Operators.Float.SUM, algo=algo)
             torch.cuda.synchronize()
@@ -67,13 +67,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--procs", type=int, default=4)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--sizes", default="4096,65536,262144,1048576,8388608,33554432", help="message bytes, comma list")
+    ap.add_argument("--buf-mib", type=int, default=64, help="IPC buffer size (larger messages go in pieces)")
+    ap.add_argument("--algos", default="0,1", help="0 = one-shot, 1 = two-shot")
     a = ap.parse_args()
     from mp4x import CommMaster
     m = CommMaster(a.procs, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
-    sizes = [4096, 65536, 262144, 1 << 20, 8 << 20, 32 << 20]
+    sizes = [int(x) for x in a.sizes.split(",")]
+    algos = tuple(int(x) for x in a.algos.split(","))
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters)) for _ in range(a.procs)]
+    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters, a.buf_mib << 20, algos)) for _ in range(a.procs)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=600) for _ in range(a.procs))
     [p.join(timeout=30) for p in ps]

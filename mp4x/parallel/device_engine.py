@@ -88,6 +88,10 @@ def local_reduce(out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: i
     return out
 
 
+def _tune_key(dtype, op, nbytes: int) -> tuple:
+    return (dtype, int(op.code), max(0, int(nbytes) - 1).bit_length())   # ceil(log2(nbytes))
+
+
 class DeviceEngine:
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
@@ -136,6 +140,9 @@ class DeviceEngine:
         self.ipc_oneshot_max = int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))
         self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
         self._ipc_obj = None
+        self._ipc_large = None
+        # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
+        self._tuned: Dict[tuple, str] = {}
 
     # ------------------------------------------------------------------ bootstrap
     def _init_pg(self):
@@ -160,12 +167,14 @@ class DeviceEngine:
         LOG.info("rank %d: device communicator up (%s, %s)", self.rank, self.backend, self.device)
 
     def shutdown(self):
-        if self._ipc_obj is not None:
-            try:
-                self._ipc_obj.close()
-            except Exception:
-                pass
-            self._ipc_obj = None
+        for name in ("_ipc_obj", "_ipc_large"):
+            obj = getattr(self, name)
+            if obj is not None:
+                try:
+                    obj.close()
+                except Exception:
+                    pass
+                setattr(self, name, None)
         if self._owns_pg and dist.is_initialized():
             try:
                 dist.destroy_process_group()
@@ -206,6 +215,20 @@ class DeviceEngine:
                 self.ipc_enabled = False
         return self._ipc_obj
 
+    def ipc_large(self):
+        """Second IPC instance with a large buffer (``MP4X_IPC_LARGE_BYTES``, default 256 MiB)
+        for messages above the two-shot tier, when autotuning (or ``MP4X_DEVICE_ALGO=ipc2``)
+        routes them to IPC.  Collective, lazily created."""
+        if self._ipc_large is None and self.ipc() is not None:
+            try:
+                from .ipc import IpcAllreduce
+                self._ipc_large = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
+                                               tag="large")
+            except Exception as e:
+                LOG.warning("large-message IPC allreduce disabled: %s", e)
+                return self._ipc_obj
+        return self._ipc_large or self._ipc_obj
+
     def _ipc_ok(self, op, dtype, nbytes) -> bool:
         if not self.ipc_enabled or nbytes % 16 or getattr(op, "is_custom", False):
             return False
@@ -225,8 +248,12 @@ class DeviceEngine:
                 and op is not None and not getattr(op, "is_custom", False) and op.code == OpCode.SUM \
                 and self.device.type == "cuda":
             return codec
-        if forced in ("ipc1", "ipc2") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
+        if forced in ("ipc1", "ipc2", "ipc2p") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             return forced
+        if kind == "allreduce" and op is not None and forced in ("", "auto") and self._tuned:
+            t = self._tuned.get(_tune_key(dtype, op, nbytes))
+            if t is not None and self._algo_valid(t, op, dtype, nbytes):
+                return t
         if op is not None and not self.rccl_ok(op, dtype):
             return "a2a"
         if forced in ("rccl", "a2a"):
@@ -255,13 +282,20 @@ class DeviceEngine:
         op = self._op(operator, view)
         algo = self.select("allreduce", view.numel() * view.element_size(), op, view.dtype, operand)
         self._count("allreduce." + algo)
-        if algo in ("ipc1", "ipc2") and self.ipc() is None:
+        self._run_allreduce(algo, view, op)
+        return arr
+
+    def _run_allreduce(self, algo: str, view: torch.Tensor, op) -> None:
+        if algo in ("ipc1", "ipc2", "ipc2p") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
             self.coll.all_reduce(view, op.code)
-        elif algo in ("ipc1", "ipc2"):
+        elif algo in ("ipc1", "ipc2", "ipc2p"):
             from .ipc import ONESHOT, TWOSHOT
-            self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT)
+            nbytes = view.numel() * view.element_size()
+            inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
+            inst.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT,
+                           overlap=True if algo == "ipc2p" else None)
         elif algo == "fp8":
             self._allreduce_fp8(view)
         elif algo == "bf16":
@@ -272,7 +306,72 @@ class DeviceEngine:
             view.copy_(w)
         else:
             self._allreduce_a2a(view, op)
-        return arr
+
+    # ------------------------------------------------------------------ autotuning
+    def _algo_valid(self, algo: str, op, dtype, nbytes: int) -> bool:
+        if algo == "rccl":
+            return self.rccl_ok(op, dtype)
+        if algo in ("ipc1", "ipc2", "ipc2p"):
+            return self._ipc_ok(op, dtype, nbytes)
+        return algo == "a2a"
+
+    def allreduce_candidates(self, nbytes: int, op, dtype) -> List[str]:
+        c = []
+        if self.rccl_ok(op, dtype):
+            c.append("rccl")
+        if self._ipc_ok(op, dtype, nbytes) and self.device.type == "cuda":
+            if nbytes <= (4 << 20):
+                c.append("ipc1")
+            c.append("ipc2")
+            if nbytes > self.ipc_twoshot_max:
+                c.append("ipc2p")     # pipelined pieces: input copies overlap the xGMI-bound kernel
+        c.append("a2a")
+        return c
+
+    def autotune_allreduce(self, like: torch.Tensor, operator, candidates: Optional[Sequence[str]] = None,
+                           iters: int = 3) -> Dict[str, float]:
+        """Time every applicable allreduce schedule on a scratch tensor shaped like ``like`` and
+        pin the fastest for this (dtype, op, size class).  Collective: every rank calls it with
+        the same shape; the decision uses the MAX time over ranks, so all ranks agree.
+
+        Returns {algo: seconds per call} (inf for a schedule that failed on any rank)."""
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        op = self._op(operator, view)
+        nbytes = view.numel() * view.element_size()
+        cands = [c for c in (candidates or self.allreduce_candidates(nbytes, op, view.dtype))
+                 if self._algo_valid(c, op, view.dtype, nbytes)]
+        times = []
+        for c in cands:
+            ok = True
+            dt = float("inf")
+            try:
+                self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
+                self._sync()
+                self.barrier()
+                t0 = time.perf_counter()
+                for _ in range(max(1, iters)):
+                    self._run_allreduce(c, view, op)
+                self._sync()
+                dt = (time.perf_counter() - t0) / max(1, iters)
+                if c.startswith("ipc"):
+                    for inst in (self._ipc_obj, self._ipc_large):
+                        if inst is not None and inst.error_word():
+                            ok = False
+            except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
+                LOG.warning("autotune: %s failed: %s", c, e)
+                ok = False
+            times.append(dt if ok else float("inf"))
+        tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        self.coll.all_reduce(tt, OpCode.MAX)
+        res = dict(zip(cands, tt.cpu().tolist()))
+        best = min(res, key=res.get) if res else None
+        if best is not None and res[best] != float("inf"):
+            self._tuned[_tune_key(view.dtype, op, nbytes)] = best
+        return res
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def _chunking(self, n: int):
         froms, tos, counts = CommUtils.even_split(0, n, self.p)

@@ -6,7 +6,7 @@ through the master (``allgather_obj``) and maps every peer's pair with
 ``hipIpcOpenMemHandle``.  A call copies the input into the own data buffer (stream ordered)
 and launches ONE kernel that synchronises with the peers' kernels through epoch flags and
 reduces straight out of peer HBM.  Messages larger than the buffer are processed in
-buffer-sized pieces.
+half-buffer pieces whose input copies (side stream) overlap the previous piece's kernel.
 
 Only needs the mp4x control plane (no RCCL communicator), so it also runs with several
 processes sharing one GPU — which is how it is tested on a single-GPU box.
@@ -90,6 +90,8 @@ class IpcAllreduce:
         self._pp_data = ptr_array(self.data_ptrs)
         self._pp_sig = ptr_array(self.sig_ptrs)
         self.epoch = 0
+        self._pp_hi = None         # peer pointers of the upper half-buffers (pipelined large path)
+        self._copy_stream = None
         self._epoch_dev = None     # device epoch counter for graph-captured calls (lazy)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
@@ -102,8 +104,13 @@ class IpcAllreduce:
         return op.code in (OpCode.MAX, OpCode.MIN) and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
 
     def allreduce(self, view: torch.Tensor, op, algo: int = ONESHOT, out: Optional[torch.Tensor] = None,
-                  blocks: int = 0) -> torch.Tensor:
-        """In place (or into ``out``) allreduce of a contiguous device tensor."""
+                  blocks: int = 0, overlap: Optional[bool] = None) -> torch.Tensor:
+        """In place (or into ``out``) allreduce of a contiguous device tensor.
+
+        ``overlap`` (messages larger than the buffer): pipeline half-buffer pieces with the
+        input copies on a side stream; default from ``MP4X_IPC_OVERLAP`` (0).  It pays when the
+        kernel is xGMI-bound; on a GPU shared by all ranks (single-GPU rehearsal) the copies
+        compete for the same HBM and it measured 2x slower (profiles/r1/ipc_large_shared_gpu.jsonl)."""
         if out is None:
             out = view
         if not view.is_contiguous() or not out.is_contiguous():
@@ -115,6 +122,10 @@ class IpcAllreduce:
         dt = int(dtype_of_torch(view.dtype))
         src = view.view(torch.uint8)
         dst = out.view(torch.uint8)
+        if overlap is None:
+            overlap = os.environ.get("MP4X_IPC_OVERLAP", "0") == "1"
+        if total > self.nbytes and overlap and not torch.cuda.is_current_stream_capturing():
+            return self._allreduce_pipelined(src, dst, total, dt, op, algo, blocks, out)
         piece = self.nbytes - self.nbytes % 16
         off = 0
         st = stream_ptr()
@@ -134,6 +145,51 @@ class IpcAllreduce:
                                               self.p, m, dst.data_ptr() + off, self.epoch, blocks, edev, st),
                   "mp4x_ipc_allreduce")
             off += m
+        return out
+
+    def _allreduce_pipelined(self, src, dst, total, dt, op, algo, blocks, out):
+        """Messages larger than the buffer: two half-buffers, the input copy of piece i+1 (side
+        stream, HBM-bound) overlaps the xGMI-bound kernel of piece i.
+
+        A half is refilled only after the kernel that last used it completed on THIS rank; that
+        kernel's end barrier already guarantees every peer finished reading it.
+        """
+        half = (self.nbytes // 2) // 4096 * 4096
+        if self._pp_hi is None:
+            self._pp_hi = ptr_array([d + half for d in self.data_ptrs])
+            self._copy_stream = torch.cuda.Stream()
+        main = torch.cuda.current_stream()
+        cs = self._copy_stream
+        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
+        cs.wait_stream(main)            # the input was produced on the caller's stream
+        kdone = [None, None]
+        ms = stream_ptr(main)
+        css = stream_ptr(cs)
+        off = 0
+        i = 0
+        while off < total:
+            m = min(half, total - off)
+            slot = i & 1
+            if kdone[slot] is not None:
+                cs.wait_event(kdone[slot])
+            check(self.lib.mp4x_memcpy_async(self.data_ptrs[self.rank] + slot * half, src.data_ptr() + off, m, css),
+                  "ipc input copy")
+            ev = torch.cuda.Event()
+            ev.record(cs)
+            main.wait_event(ev)
+            if edev is not None:
+                check(self.lib.mp4x_ipc_bump_epoch(edev, ms), "ipc_bump_epoch")
+            else:
+                self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+            pp = self._pp_hi[0] if slot else self._pp_data[0]
+            check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
+                                              dst.data_ptr() + off, self.epoch, blocks, edev, ms),
+                  "mp4x_ipc_allreduce")
+            kd = torch.cuda.Event()
+            kd.record(main)
+            kdone[slot] = kd
+            off += m
+            i += 1
         return out
 
     def prepare_graph(self):

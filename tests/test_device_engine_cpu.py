@@ -124,3 +124,28 @@ def sparse_engine(comm):
 @pytest.mark.parametrize("p", [2, 3])
 def test_sparse_engine_gloo(p):
     run_ranks(p, sparse_engine, timeout=120)
+
+
+def autotune_job(comm):
+    eng = comm.device
+    assert eng.algo == "auto"
+    t = torch.ones(4096, dtype=torch.float32)
+    res = eng.autotune_allreduce(t, Operators.Float.SUM, iters=2)
+    assert set(res) == {"rccl", "a2a"} and all(v > 0 for v in res.values())
+    best = min(res, key=res.get)
+    eng.stats.clear()
+    x = torch.full((3000,), float(comm.getRank() + 1))     # same log2 size class as 4096 floats
+    eng.allreduce(x, 0, 3000, Operators.Float.SUM)
+    p = comm.getSlaveNum()
+    assert torch.all(x == p * (p + 1) / 2)
+    return best, dict(eng.stats)
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_autotune_pins_fastest_schedule_consistently(p):
+    res, code, _ = run_ranks(p, autotune_job, timeout=120)
+    assert code == 0
+    bests = {b for b, _ in res.values()}
+    assert len(bests) == 1                      # every rank made the same decision
+    best = bests.pop()
+    assert all(st.get("allreduce." + best) == 1 for _, st in res.values())

@@ -90,6 +90,17 @@ def test_ipc_allreduce_f32(p):
             assert err < 1e-4 * p, (r, n, algo, op, err)
 
 
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_ipc_allreduce_large_pipelined(overlap, monkeypatch):
+    """10 MiB messages through a 1 MiB buffer: half-buffer pieces with the input copy of the
+    next piece overlapped on a side stream (MP4X_IPC_OVERLAP=1) or serial pieces (0)."""
+    monkeypatch.setenv("MP4X_IPC_OVERLAP", overlap)
+    out = _run(2, [(10 << 20) // 4 + 64], algos=(1,))
+    for r, res in out.items():
+        for n, algo, op, err, ew in res:
+            assert ew == 0 and err < 1e-4 * 2, (r, n, algo, op, err)
+
+
 def test_ipc_allreduce_bf16():
     out = _run(2, [8 * 4096], dtype_name="bfloat16")
     for r, res in out.items():
