@@ -157,12 +157,21 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
     }
   }
   if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
-  for (int c = 1; c < p; ++c) {
-    const int src = (rank + c) % p;            // stagger peers so links load evenly
-    const u32x4* pd = reinterpret_cast<const u32x4*>(P.data[src]);
-    const int64_t b = (int64_t)src * chunk;
-    const int64_t e = b + chunk < nvec ? b + chunk : nvec;
-    for (int64_t v = b + off0; v < e; v += stride) out[v] = pd[v];
+  // all-gather: every thread pulls the same chunk offset from ALL p-1 peers at once, so all
+  // xGMI links stream concurrently (peer after peer would leave one link busy at a time).
+  // k is a compile-time index: no dynamic indexing of the kernarg pointer table.
+  for (int64_t v = off0; v < chunk; v += stride) {
+    u32x4 x[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec) x[k] = reinterpret_cast<const u32x4*>(P.data[k])[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec) out[idx] = x[k];
+    }
   }
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
 }
@@ -281,7 +290,10 @@ extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data
   int64_t nvec = nbytes / 16;
   if (blocks <= 0) {
     int64_t b = (nvec + kIpcThreads - 1) / kIpcThreads;
-    blocks = (int)(b < 1 ? 1 : (b > 128 ? 128 : b));
+    // one-shot (latency tier): up to 128 blocks; two-shot: up to one block per CU so large
+    // messages keep enough remote requests in flight on every link
+    const int64_t cap = algo == 0 ? 128 : kIpcMaxBlocks;
+    blocks = (int)(b < 1 ? 1 : (b > cap ? cap : b));
   }
   if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
   Signal* self = (Signal*)signal_ptrs[rank];
