@@ -70,10 +70,11 @@ def reduce_into(out: torch.Tensor, ins: Sequence[torch.Tensor], op) -> None:
     if out.is_cuda:
         from ..ops.device_ops import reduce_
         reduce_(out, list(ins), int(op.code))
-    else:   # CPU tensors: only the gloo test configuration reaches this
-        acc = ins[0].numpy().copy()
+    else:   # CPU tensors: only the gloo / loopback test configurations reach this
+        half = ins[0].dtype in (torch.bfloat16, torch.float16)   # K1 accumulates these in f32
+        acc = (ins[0].float() if half else ins[0]).numpy().copy()
         for x in ins[1:]:
-            op.reduce_into(acc, x.numpy())
+            op.reduce_into(acc, (x.float() if half else x).numpy())
         out.copy_(torch.from_numpy(acc))
 
 
@@ -166,6 +167,22 @@ class DeviceEngine:
         self._owns_pg = True
         LOG.info("rank %d: device communicator up (%s, %s)", self.rank, self.backend, self.device)
 
+    def abort(self):
+        """Fail-stop teardown (``ncclCommAbort``): a rank blocked in a collective with a dead
+        peer returns instead of hanging.  Called by ``ProcessCommSlave.close(code != 0)``."""
+        for name in ("_ipc_obj", "_ipc_large"):
+            setattr(self, name, None)          # peers may be gone: no synchronising close
+        if self._owns_pg and dist.is_initialized():
+            try:
+                from torch.distributed.distributed_c10d import _abort_process_group
+                _abort_process_group(self.pg)
+            except Exception:
+                try:
+                    self.pg.abort()
+                except Exception:
+                    pass
+            self._owns_pg = False
+
     def shutdown(self):
         for name in ("_ipc_obj", "_ipc_large"):
             obj = getattr(self, name)
@@ -250,6 +267,8 @@ class DeviceEngine:
             return codec
         if forced in ("ipc1", "ipc2", "ipc2p") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             return forced
+        if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
+            return forced     # (custom operators may be non-commutative: rank-ordered a2a only)
         if kind == "allreduce" and op is not None and forced in ("", "auto") and self._tuned:
             t = self._tuned.get(_tune_key(dtype, op, nbytes))
             if t is not None and self._algo_valid(t, op, dtype, nbytes):
@@ -296,6 +315,8 @@ class DeviceEngine:
             inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
             inst.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT,
                            overlap=True if algo == "ipc2p" else None)
+        elif algo == "rhd":
+            self._allreduce_rhd(view, op)
         elif algo == "fp8":
             self._allreduce_fp8(view)
         elif algo == "bf16":
@@ -313,6 +334,8 @@ class DeviceEngine:
             return self.rccl_ok(op, dtype)
         if algo in ("ipc1", "ipc2", "ipc2p"):
             return self._ipc_ok(op, dtype, nbytes)
+        if algo == "rhd":
+            return not getattr(op, "is_custom", False)
         return algo == "a2a"
 
     def allreduce_candidates(self, nbytes: int, op, dtype) -> List[str]:
@@ -326,6 +349,8 @@ class DeviceEngine:
             if nbytes > self.ipc_twoshot_max:
                 c.append("ipc2p")     # pipelined pieces: input copies overlap the xGMI-bound kernel
         c.append("a2a")
+        if nbytes <= (64 << 20):
+            c.append("rhd")
         return c
 
     def autotune_allreduce(self, like: torch.Tensor, operator, candidates: Optional[Sequence[str]] = None,
@@ -372,6 +397,62 @@ class DeviceEngine:
     def _sync(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
+
+    def _allreduce_rhd(self, view: torch.Tensor, op):
+        """Recursive halving (reduce-scatter) + recursive doubling (all-gather), Rabenseifner.
+
+        2·log2(p) pairwise rounds over grouped send/recv; each received half is combined by
+        ONE K1 launch (local first).  Every element is reduced by exactly one rank per round
+        and then copied, so all ranks end bit-identical.  Non-power-of-two p: odd ranks below
+        2(p − p2) fold into their even neighbour first and get the result back last.  On a
+        full xGMI mesh the direct two-shot is usually faster (all links per round, 2 sync
+        points); this schedule is the latency/bandwidth middle tier for topologies without
+        IPC (autotune decides).  Host twin: ``HostEngine.rhd_allreduce``.
+        """
+        p, r = self.p, self.rank
+        n = view.numel()
+        p2 = 1 << (p.bit_length() - 1)
+        rem = p - p2
+
+        def real(v):
+            return 2 * v if v < rem else v + rem
+
+        tmp = torch.empty(max(1, (n + 1) // 2 if r >= 2 * rem else n), dtype=view.dtype, device=view.device)
+        if r < 2 * rem:
+            if r % 2:
+                self.coll.p2p([(view, r - 1)], [])
+                self.coll.p2p([], [(view, r - 1)])
+                return view
+            self.coll.p2p([], [(tmp[:n], r + 1)])
+            self._reduce_into(view, [view, tmp[:n]], op)
+            vr = r // 2
+        else:
+            vr = r - rem
+        lo, hi = 0, n
+        mask = p2 >> 1
+        steps = []
+        while mask:
+            partner = real(vr ^ mask)
+            mid = lo + (hi - lo) // 2
+            keep, give = ((lo, mid), (mid, hi)) if not vr & mask else ((mid, hi), (lo, mid))
+            kn = keep[1] - keep[0]
+            sends = [(view[give[0]:give[1]], partner)] if give[1] > give[0] else []
+            recvs = [(tmp[:kn], partner)] if kn else []
+            self.coll.p2p(sends, recvs)
+            if kn:
+                k = view[keep[0]:keep[1]]
+                self._reduce_into(k, [k, tmp[:kn]], op)
+            steps.append((partner, give))
+            lo, hi = keep
+            mask >>= 1
+        for partner, give in reversed(steps):
+            sends = [(view[lo:hi], partner)] if hi > lo else []
+            recvs = [(view[give[0]:give[1]], partner)] if give[1] > give[0] else []
+            self.coll.p2p(sends, recvs)
+            lo, hi = min(lo, give[0]), max(hi, give[1])
+        if r < 2 * rem:
+            self.coll.p2p([(view, r + 1)], [])
+        return view
 
     def _chunking(self, n: int):
         froms, tos, counts = CommUtils.even_split(0, n, self.p)

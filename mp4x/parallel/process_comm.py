@@ -182,7 +182,10 @@ class ProcessCommSlave:
             self._hb_stop.set()
             if self._device_engine is not None:
                 try:
-                    self._device_engine.shutdown()
+                    if code:
+                        self._device_engine.abort()      # fail-stop: never block on a dead peer
+                    else:
+                        self._device_engine.shutdown()
                 except Exception:
                     pass
             if self._shm is not None:

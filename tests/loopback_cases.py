@@ -40,11 +40,19 @@ def run_virtual(p, fn, device="cpu"):
 def dense_cases(eng, r, p):
     dev = eng.device
     n = 4099
-    for algo in ("rccl", "a2a"):
+    for algo in ("rccl", "a2a", "rhd"):
         eng.algo = algo
         t = torch.full((n,), float(r + 1), device=dev)
         eng.allreduce(t, 2, n - 3, Operators.Float.SUM)
         assert torch.all(t[2:n - 3] == p * (p + 1) / 2) and t[0] == r + 1
+    # recursive halving/doubling with ops / dtypes RCCL lacks (K1 combines every round)
+    eng.algo = "rhd"
+    x = torch.full((n,), 1 << r, dtype=torch.int16, device=dev)
+    eng.allreduce(x, 0, n, Operators.Short.BITS_OR)
+    assert torch.all(x == (1 << p) - 1)
+    b = torch.full((7,), float(r + 1), dtype=torch.bfloat16, device=dev)
+    eng.allreduce(b, 0, 7, Operators.BFloat16.MAX)
+    assert torch.all(b == p)
     eng.algo = "auto"
     x = torch.full((n,), 1 << r, dtype=torch.int16, device=dev)
     eng.allreduce(x, 0, n, Operators.Short.BITS_OR)

@@ -87,10 +87,13 @@ def engine_matrix(comm, algo):
 
 
 @pytest.mark.parametrize("p", [2, 3, 4])
-@pytest.mark.parametrize("algo", ["rccl", "a2a"])
+@pytest.mark.parametrize("algo", ["rccl", "a2a", "rhd"])
 def test_device_engine_gloo(p, algo):
     res, code, _ = run_ranks(p, engine_matrix, (algo,), timeout=180)
     st = res[0]
+    if algo == "rhd":                            # forced RHD takes every op (K1 combines)
+        assert st.get("allreduce.rhd", 0) >= 3
+        return
     assert st.get("allreduce.a2a", 0) >= 2      # bitwise + int16 always take the a2a schedule
     if algo == "rccl":
         assert st.get("allreduce.rccl", 0) >= 1
@@ -131,7 +134,7 @@ def autotune_job(comm):
     assert eng.algo == "auto"
     t = torch.ones(4096, dtype=torch.float32)
     res = eng.autotune_allreduce(t, Operators.Float.SUM, iters=2)
-    assert set(res) == {"rccl", "a2a"} and all(v > 0 for v in res.values())
+    assert set(res) == {"rccl", "a2a", "rhd"} and all(v > 0 for v in res.values())
     best = min(res, key=res.get)
     eng.stats.clear()
     x = torch.full((3000,), float(comm.getRank() + 1))     # same log2 size class as 4096 floats
@@ -149,3 +152,20 @@ def test_autotune_pins_fastest_schedule_consistently(p):
     assert len(bests) == 1                      # every rank made the same decision
     best = bests.pop()
     assert all(st.get("allreduce." + best) == 1 for _, st in res.values())
+
+
+def _abort_job(comm):
+    t = torch.ones(64)
+    comm.device.allreduce(t, 0, 64, Operators.Float.SUM)
+    assert torch.all(t == comm.getSlaveNum())
+    if comm.getRank() == 0:
+        comm.close(1)                 # failure close: the device communicator is aborted
+        assert not comm.device._owns_pg
+        return "aborted"
+    return "ok"
+
+
+def test_failure_close_aborts_device_communicator():
+    res, code, errs = run_ranks(2, _abort_job, timeout=60, expect_fail=True)
+    assert res.get(0) == "aborted" and not errs
+    assert code == 1                  # the master aggregates the non-zero close
