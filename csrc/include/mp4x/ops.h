@@ -25,6 +25,7 @@ enum mp4x_op {
   MP4X_BAND = 4, MP4X_BOR = 5, MP4X_BXOR = 6,
   MP4X_FMAXLOC = 7, MP4X_FMINLOC = 8,   // f64 word: f32 value in hi 32 bits, int32 loc in lo 32 bits
   MP4X_IMAXLOC = 9, MP4X_IMINLOC = 10,  // i64 word: i32 value in hi 32 bits, int32 loc in lo 32 bits
+  MP4X_FIRST = 11,                      // keep the first value (K8 map merge / dedupe-by-key; sparse only)
 };
 
 enum { MP4X_E_BADARG = 1001, MP4X_E_UNSUPPORTED = 1002 };

@@ -68,7 +68,7 @@ template <int DT> constexpr bool is_float_dt() {
 
 // Which (dtype, op) pairs exist (mirrors the reference operator table + 16-bit floats).
 template <int DT, int OP> constexpr bool op_valid() {
-  if (OP == MP4X_SUM || OP == MP4X_MAX || OP == MP4X_MIN || OP == MP4X_PROD) return true;
+  if (OP == MP4X_SUM || OP == MP4X_MAX || OP == MP4X_MIN || OP == MP4X_PROD || OP == MP4X_FIRST) return true;
   if (OP == MP4X_BAND || OP == MP4X_BOR || OP == MP4X_BXOR) return !is_float_dt<DT>();
   if (OP == MP4X_FMAXLOC || OP == MP4X_FMINLOC) return DT == MP4X_F64;
   if (OP == MP4X_IMAXLOC || OP == MP4X_IMINLOC) return DT == MP4X_I64;
@@ -86,7 +86,10 @@ template <> struct Unsigned<int8_t> { using U = uint8_t; };
 template <int DT, int OP>
 __device__ __forceinline__ typename Elem<DT>::A combine(typename Elem<DT>::A a, typename Elem<DT>::A b) {
   using A = typename Elem<DT>::A;
-  if constexpr (OP == MP4X_SUM) {
+  if constexpr (OP == MP4X_FIRST) {
+    (void)b;
+    return a;
+  } else if constexpr (OP == MP4X_SUM) {
     if constexpr (is_float_dt<DT>()) return a + b;
     else { using U = typename Unsigned<A>::U; return (A)((U)a + (U)b); }
   } else if constexpr (OP == MP4X_PROD) {

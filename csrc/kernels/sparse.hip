@@ -11,6 +11,8 @@
 //       head flags + DeviceSelect give run starts, then one wave per run reduces its rows
 //       (lanes over `dim`) in run order => deterministic, no float atomics.
 //   K7  set union / intersection / concat reuse the same runs (count == p for intersection).
+//   K8  map merge (gather / allgather map): the same runs with OP = FIRST keep the first
+//       row of every key in rank order (dedupe-by-key).
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
@@ -68,7 +70,8 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce(const int64_t* __rest
     if (!vals) continue;
     for (int64_t d = lane; d < dim; d += 64) {
       A acc = E::load(vals[perm[s] * dim + d]);
-      for (int64_t j = s + 1; j < e; ++j) acc = combine<DT, OP>(acc, E::load(vals[perm[j] * dim + d]));
+      if constexpr (OP != MP4X_FIRST)
+        for (int64_t j = s + 1; j < e; ++j) acc = combine<DT, OP>(acc, E::load(vals[perm[j] * dim + d]));
       out_vals[u * dim + d] = E::store(acc);
     }
   }
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce_vec(const int64_t* __
       A acc[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) acc[j] = E::load(x[j]);
-      int64_t j = s + 1;
+      int64_t j = (OP == MP4X_FIRST) ? e : s + 1;   // FIRST (K8 dedupe): the run's first row only
       for (; j + 1 < e; j += 2) {          // two rows in flight
         u32x4 t0 = vals[perm[j] * V + v];
         u32x4 t1 = vals[perm[j + 1] * V + v];
@@ -172,6 +175,7 @@ static int sr_dt(int op, const int64_t* sk, const int64_t* perm, const int64_t* 
     case MP4X_BAND: return launch_sr<DT, MP4X_BAND>(sk, perm, starts, nr, n, mr, vals, dim, ok, ov, oc, st);
     case MP4X_BOR: return launch_sr<DT, MP4X_BOR>(sk, perm, starts, nr, n, mr, vals, dim, ok, ov, oc, st);
     case MP4X_BXOR: return launch_sr<DT, MP4X_BXOR>(sk, perm, starts, nr, n, mr, vals, dim, ok, ov, oc, st);
+    case MP4X_FIRST: return launch_sr<DT, MP4X_FIRST>(sk, perm, starts, nr, n, mr, vals, dim, ok, ov, oc, st);
     default: return MP4X_E_UNSUPPORTED;
   }
 }
@@ -339,6 +343,9 @@ extern "C" int mp4x_segment_reduce_rows(int dtype, int op, const int64_t* sk, co
     case MP4X_I32: return sr_dt<MP4X_I32>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
     case MP4X_BF16: return sr_dt<MP4X_BF16>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
     case MP4X_F16: return sr_dt<MP4X_F16>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
+    case MP4X_I16: return sr_dt<MP4X_I16>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
+    case MP4X_I8: return sr_dt<MP4X_I8>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
+    case MP4X_U8: return sr_dt<MP4X_U8>(op, sk, perm, starts, nruns_dev, n, max_runs, vals, dim, out_keys, out_vals, out_count, st);
     default: return MP4X_E_UNSUPPORTED;
   }
 }

@@ -625,6 +625,43 @@ class DeviceEngine:
         self._count("allreduce_map")
         return allreduce_map_device(self, mapData, operator)
 
+    def all_to_all_v(self, send: torch.Tensor, send_counts: List[int], recv: Optional[torch.Tensor] = None):
+        """Ragged all-to-all over rows of ``send`` (rows grouped by destination)."""
+        self._count("all_to_all_v")
+        if sum(send_counts) != send.shape[0]:
+            raise Mp4jException(f"sendCounts sum {sum(send_counts)} != rows {send.shape[0]}")
+        sc = torch.tensor(send_counts, dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
+        rc = torch.empty_like(sc)
+        self.coll.all_to_all_single(rc, sc)
+        recv_counts = [int(x) for x in rc.tolist()]
+        shape = (sum(recv_counts),) + tuple(send.shape[1:])
+        if recv is None:
+            recv = torch.empty(shape, dtype=send.dtype, device=send.device)
+        elif tuple(recv.shape) != shape:
+            raise Mp4jException(f"recvData shape {tuple(recv.shape)} != {shape}")
+        self.coll.all_to_all_single(recv, send.contiguous(), recv_counts, list(send_counts))
+        return recv, recv_counts
+
+    def reduce_map(self, mapData: Dict, operator, root: int):
+        from .sparse import reduce_map_device
+        self._count("reduce_map")
+        return reduce_map_device(self, mapData, operator, root)
+
+    def gather_map(self, mapData: Dict, root: int):
+        from .sparse import gather_map_device
+        self._count("gather_map")
+        return gather_map_device(self, mapData, root)
+
+    def allgather_map(self, mapData: Dict):
+        from .sparse import allgather_map_device
+        self._count("allgather_map")
+        return allgather_map_device(self, mapData)
+
+    def broadcast_map(self, mapData: Dict, root: int):
+        from .sparse import broadcast_map_device
+        self._count("broadcast_map")
+        return broadcast_map_device(self, mapData, root)
+
     def barrier(self):
         self.coll.barrier()
 

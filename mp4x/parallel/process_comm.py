@@ -288,11 +288,20 @@ class ProcessCommSlave:
         self.engine.tree_gather(buf, sendfroms, sendtos, operand, rootRank)
         return arrData
 
+    def _map_on_device(self, mapData: Dict) -> bool:
+        """Do this map collective's values live on the GPU?  A rank with an empty map cannot
+        tell, so the ranks agree over the control plane (one small RPC)."""
+        mine = -1 if not mapData else int(_is_torch(next(iter(mapData.values()))))
+        flags = self.server.call("allgather_obj", self.rank, mine)
+        return any(f == 1 for f in flags)
+
     def gatherMap(self, mapData: Dict, operand: Operand, rootRank: int) -> Dict:
         self._tick("gatherMap")
         if self.slaveNum == 1:
             return mapData
         self._check_root(rootRank)
+        if self._map_on_device(mapData):
+            return self.device.gather_map(mapData, rootRank)
         return self.engine.tree_gather_map(mapData, operand, rootRank)
 
     # ================================================================ allgather
@@ -317,6 +326,8 @@ class ProcessCommSlave:
         self._tick("allgatherMap")
         if self.slaveNum == 1:
             return [mapData]
+        if self._map_on_device(mapData):
+            return self.device.allgather_map(mapData)
         blocks = self.engine.ring_allgather_maps([mapData], operand)
         return [b[0] for b in blocks]
 
@@ -358,6 +369,8 @@ class ProcessCommSlave:
         if self.slaveNum == 1:
             return mapData
         self._check_root(rootRank)
+        if self._map_on_device(mapData if self.rank == rootRank else {}):
+            return self.device.broadcast_map(mapData, rootRank)
         p = self.slaveNum
         blocks = None
         if self.rank == rootRank:
@@ -484,6 +497,8 @@ class ProcessCommSlave:
         if self.slaveNum == 1:
             return mapData
         self._check_root(rootRank)
+        if self._map_on_device(mapData):
+            return self.device.reduce_map(mapData, operator, rootRank)
         mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)[0]
         return self.engine.tree_gather_map(mine, operand, rootRank)
 
@@ -555,6 +570,52 @@ class ProcessCommSlave:
             return keys, vals
         from .sparse import allreduce_sparse
         return allreduce_sparse(self.device, keys, vals, operator)
+
+    def reduceSparse(self, keys, vals, operator, rootRank: int):
+        """Tensor form of ``reduceMap``: root gets the op-reduced union (others: their owned share)."""
+        self._tick("reduceSparse")
+        if self.slaveNum == 1:
+            return keys, vals
+        self._check_root(rootRank)
+        from .sparse import reduce_sparse
+        return reduce_sparse(self.device, keys, vals, operator, rootRank)
+
+    def gatherSparse(self, keys, vals, rootRank: int):
+        """Tensor form of ``gatherMap``: union at root, duplicate ids keep the lowest rank's row (K8)."""
+        self._tick("gatherSparse")
+        if self.slaveNum == 1:
+            return keys, vals
+        self._check_root(rootRank)
+        from .sparse import gather_sparse
+        return gather_sparse(self.device, keys, vals, rootRank)
+
+    def allgatherSparse(self, keys, vals):
+        """Tensor form of ``allgatherMap``: (keys, rows, per-rank counts) concatenated in rank order."""
+        self._tick("allgatherSparse")
+        if self.slaveNum == 1:
+            return keys, vals, [int(keys.shape[0])]
+        from .sparse import allgather_sparse
+        return allgather_sparse(self.device, keys, vals)
+
+    def broadcastSparse(self, keys, vals, rootRank: int):
+        """Tensor form of ``broadcastMap``: root's (keys, rows) everywhere (non-root inputs may be None)."""
+        self._tick("broadcastSparse")
+        if self.slaveNum == 1:
+            return keys, vals
+        self._check_root(rootRank)
+        from .sparse import broadcast_sparse
+        return broadcast_sparse(self.device, keys, vals, rootRank)
+
+    def alltoallArray(self, sendData, sendCounts: Sequence[int], recvData=None):
+        """Ragged all-to-all of a device tensor (extension; the exchange behind the sparse map
+        collectives, exposed for expert-parallel style routing).  ``sendData`` rows are grouped
+        by destination rank with ``sendCounts[j]`` rows for rank j.  Returns ``(recv, recvCounts)``
+        with rows grouped by source rank (RCCL all-to-all, every link at once)."""
+        self._tick("alltoallArray")
+        self._check_len(sendCounts, "sendCounts")
+        if not _is_torch(sendData):
+            raise Mp4jException("alltoallArray needs a torch tensor (device engine)")
+        return self.device.all_to_all_v(sendData, list(sendCounts), recvData)
 
     # ================================================================ allreduce
     def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, out=None):
@@ -653,7 +714,7 @@ class ProcessCommSlave:
         self._tick("allreduceMap")
         if self.slaveNum == 1:
             return mapData
-        if mapData and _is_torch(next(iter(mapData.values()))):
+        if self._map_on_device(mapData):
             return self.device.allreduce_map(mapData, operator)
         mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)
         allb = self.engine.ring_allgather_maps(mine, operand)

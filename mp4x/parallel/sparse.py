@@ -172,12 +172,17 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     return rkeys, rvals
 
 
-def _allgather_v(engine, t: torch.Tensor) -> torch.Tensor:
+def _row_counts(engine, n: int, device) -> List[int]:
+    t = torch.tensor([n], dtype=torch.int64, device=device)
+    ts = [torch.empty_like(t) for _ in range(engine.p)]
+    engine.coll.all_gather(ts, t)
+    return [int(x.item()) for x in ts]
+
+
+def _allgather_v(engine, t: torch.Tensor, sizes: Optional[List[int]] = None) -> torch.Tensor:
     p = engine.p
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    ns = [torch.empty_like(n) for _ in range(p)]
-    engine.coll.all_gather(ns, n)
-    sizes = [int(x.item()) for x in ns]
+    if sizes is None:
+        sizes = _row_counts(engine, t.shape[0], t.device)
     m = max(sizes) if sizes else 0
     pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
     if t.shape[0]:
@@ -200,6 +205,83 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator):
     all_k = _allgather_v(engine, uk)
     all_v = _allgather_v(engine, uv)
     return all_k, (all_v.view(-1) if squeeze else all_v)
+
+
+OP_FIRST = 11     # native MP4X_FIRST: keep the first row of every key (K8 map merge)
+
+
+def _dedupe_first(keys: torch.Tensor, vals: Optional[torch.Tensor]):
+    """K8: unique keys ascending, each with its FIRST row in input (= rank) order."""
+    if keys.is_cuda:
+        from ..ops.device_ops import reduce_by_key
+        uk, uv, _ = reduce_by_key(keys, vals, OP_FIRST)
+        return uk, uv
+    uk, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    first = torch.full((uk.numel(),), keys.numel(), dtype=torch.int64)
+    first.scatter_reduce_(0, inv, torch.arange(keys.numel()), "amin")
+    return uk, (vals[first] if vals is not None else None)
+
+
+def allgather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor):
+    """Every rank's (keys, rows) concatenated in rank order + the per-rank row counts."""
+    sizes = _row_counts(engine, keys.shape[0], keys.device)
+    return _allgather_v(engine, keys, sizes), _allgather_v(engine, vals, sizes), sizes
+
+
+def gather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, root: int):
+    """Root receives every rank's pairs (grouped p2p, all links at once) and merges them with
+    K8 (duplicate key: the lowest rank's row survives).  Non-root ranks get their input back."""
+    sizes = _row_counts(engine, keys.shape[0], keys.device)
+    r = engine.rank
+    if r != root:
+        sends = [(keys, root)] + ([(vals, root)] if vals.numel() else []) if sizes[r] else []
+        engine.coll.p2p(sends, [])
+        return keys, vals
+    tail = tuple(vals.shape[1:])
+    ks, vs, recvs = [], [], []
+    for j in range(engine.p):
+        if j == root:
+            ks.append(keys)
+            vs.append(vals)
+            continue
+        kb = torch.empty(sizes[j], dtype=keys.dtype, device=keys.device)
+        vb = torch.empty((sizes[j],) + tail, dtype=vals.dtype, device=vals.device)
+        ks.append(kb)
+        vs.append(vb)
+        if sizes[j]:
+            recvs.append((kb, j))
+            if vb.numel():
+                recvs.append((vb, j))
+    engine.coll.p2p([], recvs)
+    return _dedupe_first(torch.cat(ks), torch.cat(vs))
+
+
+def broadcast_sparse(engine, keys: Optional[torch.Tensor], vals: Optional[torch.Tensor], root: int):
+    """Root's (keys, rows) on every rank (shape/dtype travel over the control plane)."""
+    meta = engine.all_gather_object(
+        (int(keys.shape[0]), tuple(vals.shape[1:]), str(vals.dtype).replace("torch.", ""))
+        if engine.rank == root else None)[root]
+    n, tail, dt = meta
+    dev = engine.device
+    if engine.rank != root:
+        keys = torch.empty(n, dtype=torch.int64, device=dev)
+        vals = torch.empty((n,) + tuple(tail), dtype=getattr(torch, dt), device=dev)
+    if n:
+        engine.coll.broadcast(keys, root)
+        if vals.numel():
+            engine.coll.broadcast(vals, root)
+    return keys, vals
+
+
+def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root: int):
+    """Owner exchange + K5 reduce-by-key, then the owner-disjoint pieces go to ``root``."""
+    squeeze = vals.dim() == 1
+    v2 = vals.view(-1, 1) if squeeze else vals
+    op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
+    rkeys, rvals = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op)
+    gk, gv = gather_sparse(engine, uk, uv, root)    # disjoint owners: K8 dedupe is a no-op
+    return gk, (gv.view(-1) if squeeze else gv)
 
 
 def _set_counts(engine, ids: torch.Tensor):
@@ -226,8 +308,8 @@ def list_concat(engine, ids: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ Map API
-def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
-    """``allreduceMap`` for ``Dict[str, torch.Tensor]`` values on the GPU."""
+def _map_tensors(engine, mapData: Dict):
+    """Dict[str, Tensor] -> (ids int64[n], rows [n, numel], value shape); syncs new keys."""
     d = _dictionary(engine)
     keys = list(mapData.keys())
     ids, new = d.ids_for(keys)
@@ -240,10 +322,53 @@ def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
     else:
         v = torch.empty((0, 1), device=dev)
         shape = (1,)
-    k = torch.tensor(ids, dtype=torch.int64, device=dev)
+    return torch.tensor(ids, dtype=torch.int64, device=dev), v, shape
+
+
+def _tensors_map(engine, k: torch.Tensor, v: torch.Tensor, shape) -> Dict:
+    d = _dictionary(engine)
+    return {d.id2key[kid]: v[i].view(shape) for i, kid in enumerate(k.tolist())}
+
+
+def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
+    """``allreduceMap`` for ``Dict[str, torch.Tensor]`` values on the GPU."""
+    k, v, shape = _map_tensors(engine, mapData)
     rk, rv = allreduce_sparse(engine, k, v, operator)
-    out = {}
-    rk_l = rk.tolist()
-    for i, kid in enumerate(rk_l):
-        out[d.id2key[kid]] = rv[i].view(shape)
+    return _tensors_map(engine, rk, rv, shape)
+
+
+def reduce_map_device(engine, mapData: Dict, operator, root: int) -> Dict:
+    """``reduceMap``: the op-reduced union at ``root`` (non-root: its owned share)."""
+    k, v, shape = _map_tensors(engine, mapData)
+    rk, rv = reduce_sparse(engine, k, v, operator, root)
+    return _tensors_map(engine, rk, rv, shape)
+
+
+def gather_map_device(engine, mapData: Dict, root: int) -> Dict:
+    """``gatherMap``: union at root, duplicate keys keep the lowest rank's value (K8)."""
+    k, v, shape = _map_tensors(engine, mapData)
+    gk, gv = gather_sparse(engine, k, v, root)
+    return _tensors_map(engine, gk, gv, shape) if engine.rank == root else mapData
+
+
+def allgather_map_device(engine, mapData: Dict) -> List[Dict]:
+    """``allgatherMap``: every rank's map, indexed by rank."""
+    k, v, shape = _map_tensors(engine, mapData)
+    ak, av, sizes = allgather_sparse(engine, k, v)
+    out, off = [], 0
+    for n in sizes:
+        out.append(_tensors_map(engine, ak[off:off + n], av[off:off + n], shape))
+        off += n
     return out
+
+
+def broadcast_map_device(engine, mapData: Dict, root: int) -> Dict:
+    """``broadcastMap``: root's map on every rank."""
+    if engine.rank == root:
+        k, v, shape = _map_tensors(engine, mapData)
+    else:
+        _sync_new_keys(engine, {})
+        k = v = None
+    bk, bv = broadcast_sparse(engine, k, v, root)
+    shape = engine.all_gather_object(shape if engine.rank == root else None)[root]
+    return _tensors_map(engine, bk, bv, shape)

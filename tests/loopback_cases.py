@@ -135,4 +135,49 @@ def sparse_cases(eng, r, p):
     m = {f"w{j}": torch.full((3,), float(r), device=dev) for j in range(20)}
     out = allreduce_map_device(eng, m, Operators.Float.MAX)
     assert len(out) == 20 and torch.all(out["w7"] == p - 1)
+    map_family_cases(eng, r, p)
     return True
+
+
+def map_family_cases(eng, r, p):
+    """reduce / gather (K8 dedupe) / allgather / broadcast maps and their tensor forms, ragged
+    and empty inputs, every value dtype the segment kernels take."""
+    from mp4x.parallel import sparse as S
+    dev = eng.device
+    root = p - 1
+    # reduceMap: union reduced at root; rank r contributes keys 0..r (rank 0: a single key)
+    m = {f"k{j}": torch.full((2,), float(j + r), device=dev) for j in range(r + 1)}
+    out = S.reduce_map_device(eng, m, Operators.Float.SUM, root)
+    if r == root:
+        assert len(out) == p
+        for j in range(p):   # key j is present on ranks j..p-1
+            assert torch.all(out[f"k{j}"] == sum(j + q for q in range(j, p)))
+    # gatherMap: duplicate key "dup" keeps the lowest rank's value; rank 1 sends an empty map
+    g = {} if r == 1 else {"dup": torch.tensor([float(r)], device=dev), f"own{r}": torch.ones(1, device=dev)}
+    got = S.gather_map_device(eng, g, root)
+    if r == root:
+        expect_dup = 0.0
+        assert float(got["dup"]) == expect_dup and len(got) == 1 + sum(1 for q in range(p) if q != 1)
+    # allgatherMap: list indexed by rank
+    lst = S.allgather_map_device(eng, {f"a{r}": torch.full((4,), r, dtype=torch.int16, device=dev)})
+    assert len(lst) == p and all(int(lst[q][f"a{q}"][0]) == q for q in range(p))
+    # broadcastMap: non-root ranks start empty
+    b = {"x": torch.arange(6, dtype=torch.float64, device=dev).view(2, 3)} if r == 0 else {}
+    bb = S.broadcast_map_device(eng, b, 0)
+    assert list(bb) == ["x"] and bb["x"].shape == (2, 3) and float(bb["x"][1, 2]) == 5.0
+    # tensor forms: gather with int8 rows (scalar segment kernel), allgather counts
+    keys = torch.tensor([7, 100 + r], dtype=torch.int64, device=dev)
+    vals = torch.full((2, 3), r, dtype=torch.int8, device=dev)
+    gk, gv = S.gather_sparse(eng, keys, vals, 0)
+    if r == 0:
+        d = dict(zip(gk.tolist(), gv[:, 0].tolist()))
+        assert d[7] == 0 and len(d) == 1 + p and d[100 + p - 1] == p - 1
+    ak, av, sizes = S.allgather_sparse(eng, keys, vals)
+    assert sizes == [2] * p and ak.tolist()[2 * r + 1] == 100 + r
+    # ragged all-to-all (EP-style routing): rank r sends j+1 rows to rank j
+    counts = [j + 1 for j in range(p)]
+    send = torch.cat([torch.full((j + 1, 2), float(r * 10 + j), device=dev) for j in range(p)])
+    recv, rc = eng.all_to_all_v(send, counts)
+    assert rc == [r + 1] * p
+    for q in range(p):
+        assert torch.all(recv[q * (r + 1):(q + 1) * (r + 1)] == q * 10 + r)

@@ -121,6 +121,25 @@ def sparse_engine(comm):
     assert len(out) == 12 + p and torch.all(out["feat3"] == p * (p + 1) / 2) and torch.all(out[f"only{r}"] == 1)
     out2 = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.MAX)   # keys known now: no string sync
     assert torch.all(out2["feat0"] == p)
+    # the rest of the map family through the public API (device values -> device paths)
+    root = p - 1
+    red = comm.reduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.SUM, root)
+    if r == root:
+        assert len(red) == 12 + p and torch.all(red["feat5"] == p * (p + 1) / 2)
+    g = comm.gatherMap({} if r == 0 else {f"g{r}": torch.ones(2)}, Operands.FLOAT_OPERAND(), root)
+    if r == root:
+        assert sorted(g) == sorted(f"g{q}" for q in range(1, p))
+    lst = comm.allgatherMap({f"a{r}": torch.full((2,), float(r))}, Operands.FLOAT_OPERAND())
+    assert [float(d[f"a{q}"][0]) for q, d in enumerate(lst)] == [float(q) for q in range(p)]
+    b = comm.broadcastMap({"z": torch.tensor([3.0, 4.0])} if r == 0 else {}, Operands.FLOAT_OPERAND(), 0)
+    assert torch.equal(b["z"], torch.tensor([3.0, 4.0]))
+    hb = comm.broadcastMap({"h": 1.5} if r == 0 else {}, Operands.DOUBLE_OPERAND(), 0)   # host values
+    assert hb == {"h": 1.5}
+    ks, vs = comm.reduceSparse(torch.tensor([1, 2], dtype=torch.int64), torch.ones(2, 3), Operators.Float.SUM, 0)
+    if r == 0:
+        assert ks.tolist() == [1, 2] and torch.all(vs == p)
+    recv, rc = comm.alltoallArray(torch.full((p, 2), float(r)), [1] * p)
+    assert rc == [1] * p and recv[:, 0].tolist() == [float(q) for q in range(p)]
     return "ok"
 
 

@@ -242,3 +242,18 @@ def test_partition_pack_matches_sort_path():
     sk, sv, counts, _ = K.partition_pack(keys, vals, 8)
     assert torch.equal(sk, keys[perm]) and torch.equal(sv, vals[perm])
     assert torch.equal(counts, hist.long())
+
+
+@pytest.mark.parametrize("dim,dtype", [(16, torch.float32), (5, torch.float32), (8, torch.int16), (3, torch.int8)])
+def test_reduce_by_key_first_is_k8_dedupe(dim, dtype):
+    """MP4X_FIRST: every key keeps the row of its first occurrence (K8 map merge)."""
+    K = _native()
+    n = 5000
+    keys = torch.randint(0, 700, (n,), device=DEV, dtype=torch.int64)
+    vals = torch.randint(-100, 100, (n, dim), device=DEV).to(dtype)
+    uk, uv, cnt = K.reduce_by_key(keys, vals, 11)
+    ref_k, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    first = torch.full((ref_k.numel(),), n, device=DEV, dtype=torch.int64)
+    first.scatter_reduce_(0, inv, torch.arange(n, device=DEV), "amin")
+    assert torch.equal(uk, ref_k) and torch.equal(uv, vals[first])
+    assert int(cnt.sum()) == n
