@@ -68,6 +68,17 @@ int mp4x_dequant_reduce_fp8(int dtype_out, void* out, const uint8_t* const* qs, 
                             int nin, int64_t n, int accumulate, uint8_t* q_out, float* s_out, void* stream);
 int mp4x_dequant_fp8(int dtype_out, void* out, const uint8_t* q, const float* scales, int64_t n, void* stream);
 
+// K6b lossless zero suppression.  table (device int64): elem_start[nchunk], elem_len[nchunk],
+// blk_start[nchunk + 1] in 256-element blocks.  Encode: masks[4 * nblk], counts[nblk],
+// offs[nblk + 1] (offs[nblk] = total non-zero words), vals (worst case n words).  Decode:
+// the same masks / counts / vals (chunks concatenated) expanded into out per table.
+size_t mp4x_zs_temp_bytes(int64_t nblk);
+int mp4x_zs_encode(int elem_bytes, const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,
+                   int32_t* counts, int64_t* offs, void* vals, void* temp, size_t temp_bytes, void* stream);
+int mp4x_zs_decode(int elem_bytes, const uint64_t* masks, const int32_t* counts, const void* vals,
+                   const int64_t* table, int nchunk, int64_t nblk, void* out, int64_t* offs, void* temp,
+                   size_t temp_bytes, void* stream);
+
 // ---------------------------------------------------------------- K4 / K5 / K7 sparse
 // Owner of each key: dest[i] = (uint64)key[i] % p.  hist[p] += counts (hist zeroed by caller).
 int mp4x_key_owner(const int64_t* keys, int64_t n, int p, int32_t* dest, int32_t* hist, void* stream);

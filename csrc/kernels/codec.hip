@@ -11,6 +11,8 @@
 //   dequant_reduce: one wave per block, NIN fp8 chunks dequantised and summed in f32
 //                   registers (the two-shot compressed allreduce's reduce step), optionally
 //                   re-quantised in the same pass for the all-gather leg.
+#include <hipcub/hipcub.hpp>
+
 #include "common.hpp"
 
 namespace mp4x {
@@ -191,6 +193,143 @@ static int dr_dt(void* out, const uint8_t* const* qs, const float* const* ss, in
   }
 }
 
+
+// ---------------------------------------------------------------- K6b lossless zero suppression
+// The reference's compress=true is lossless Deflate.  For device tensors the lossless codec is
+// zero suppression, the case where it pays on accelerator data (sparse / masked gradients,
+// histograms).  Per 256-element block:
+//   masks  4 x uint64 (ballot of "word != 0", one per 64-lane slice)
+//   counts int32 non-zero words  ->  exclusive scan (hipCUB) -> offsets
+//   vals   the non-zero words, compacted in order
+// "Zero" means all bits zero, so -0.0, NaN payloads and every integer pattern round-trip
+// exactly.  Blocks never straddle chunks: a chunk table (elem_start, elem_len, blk_start)
+// maps block b to its chunk (binary search), so p destination chunks encode in ONE pass and
+// their value runs come out contiguous per chunk for a ragged all-to-all.
+constexpr int kZsBlock = 256;
+
+struct ZsChunk {
+  int64_t base, len;   // element start / remaining elements of this block inside its chunk
+};
+
+__device__ __forceinline__ ZsChunk zs_locate(const int64_t* __restrict__ table, int nchunk, int64_t b) {
+  const int64_t* es = table;
+  const int64_t* el = table + nchunk;
+  const int64_t* bs = table + 2 * nchunk;       // nchunk + 1 entries
+  int lo = 0, hi = nchunk - 1;
+  while (lo < hi) {                              // last j with bs[j] <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (bs[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t lb = b - bs[lo];
+  return {es[lo] + lb * kZsBlock, el[lo] - lb * kZsBlock};
+}
+
+template <typename W>
+__global__ __launch_bounds__(kBlock) void k_zs_mask(const W* __restrict__ in, const int64_t* __restrict__ table,
+                                                    int nchunk, int64_t nblk, uint64_t* __restrict__ masks,
+                                                    int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t b = wave; b < nblk; b += nwaves) {
+    const ZsChunk c = zs_locate(table, nchunk, b);
+    W v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = q * 64 + lane;
+      v[q] = i < c.len ? in[c.base + i] : (W)0;
+    }
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t m = __ballot(v[q] != (W)0);
+      if (lane == 0) masks[b * 4 + q] = m;
+      cnt += __popcll(m);
+    }
+    if (lane == 0) counts[b] = cnt;
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(kBlock) void k_zs_compact(const W* __restrict__ in, const int64_t* __restrict__ table,
+                                                       int nchunk, int64_t nblk, const int64_t* __restrict__ offs,
+                                                       W* __restrict__ vals) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t b = wave; b < nblk; b += nwaves) {
+    const ZsChunk c = zs_locate(table, nchunk, b);
+    int64_t pos = offs[b];
+    W v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t i = q * 64 + lane;
+      v[q] = i < c.len ? in[c.base + i] : (W)0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t m = __ballot(v[q] != (W)0);
+      if (v[q] != (W)0) vals[pos + __popcll(m & lt)] = v[q];
+      pos += __popcll(m);
+    }
+  }
+}
+
+template <typename W>
+__global__ __launch_bounds__(kBlock) void k_zs_expand(const uint64_t* __restrict__ masks,
+                                                      const int64_t* __restrict__ offs, const W* __restrict__ vals,
+                                                      const int64_t* __restrict__ table, int nchunk, int64_t nblk,
+                                                      W* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1;
+  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t b = wave; b < nblk; b += nwaves) {
+    const ZsChunk c = zs_locate(table, nchunk, b);
+    int64_t pos = offs[b];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint64_t m = masks[b * 4 + q];
+      const int64_t i = q * 64 + lane;
+      if (i < c.len) out[c.base + i] = ((m >> lane) & 1) ? vals[pos + __popcll(m & lt)] : (W)0;
+      pos += __popcll(m);
+    }
+  }
+}
+
+__global__ void k_zs_total(const int64_t* __restrict__ offs, const int32_t* __restrict__ counts, int64_t nblk,
+                           int64_t* __restrict__ total) {
+  *total = nblk ? offs[nblk - 1] + counts[nblk - 1] : 0;
+}
+
+template <typename W>
+static int zs_encode_t(const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,
+                       int32_t* counts, int64_t* offs, void* vals, void* temp, size_t temp_bytes, hipStream_t st) {
+  const int g = grid_for(nblk * 64, 1);
+  hipLaunchKernelGGL(k_zs_mask<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, masks, counts);
+  int e = (int)hipGetLastError();
+  if (e) return e;
+  e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
+  if (e) return e;
+  hipLaunchKernelGGL(k_zs_total, dim3(1), dim3(1), 0, st, offs, counts, nblk, offs + nblk);
+  hipLaunchKernelGGL(k_zs_compact<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, offs,
+                     (W*)vals);
+  return (int)hipGetLastError();
+}
+
+template <typename W>
+static int zs_decode_t(const uint64_t* masks, const int32_t* counts, const void* vals, const int64_t* table,
+                       int nchunk, int64_t nblk, void* out, int64_t* offs, void* temp, size_t temp_bytes,
+                       hipStream_t st) {
+  int e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
+  if (e) return e;
+  const int g = grid_for(nblk * 64, 1);
+  hipLaunchKernelGGL(k_zs_expand<W>, dim3(g), dim3(kBlock), 0, st, masks, offs, (const W*)vals, table, nchunk,
+                     nblk, (W*)out);
+  return (int)hipGetLastError();
+}
+
 }  // namespace mp4x
 
 using namespace mp4x;
@@ -226,4 +365,44 @@ extern "C" int mp4x_dequant_fp8(int dtype_out, void* out, const uint8_t* q, cons
   const uint8_t* qs[1] = {q};
   const float* ss[1] = {scales};
   return mp4x_dequant_reduce_fp8(dtype_out, out, qs, ss, 1, n, 0, nullptr, nullptr, stream);
+}
+
+extern "C" size_t mp4x_zs_temp_bytes(int64_t nblk) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int64_t*)nullptr,
+                                         (int)(nblk < 1 ? 1 : nblk), (hipStream_t)0);
+  return bytes;
+}
+
+// table (device int64): elem_start[nchunk], elem_len[nchunk], blk_start[nchunk + 1] (blk_start[j]
+// = sum of ceil(elem_len[i] / 256) for i < j).  offs needs nblk + 1 entries; offs[nblk] = total
+// non-zero words.  vals must hold the worst case (every word non-zero).
+extern "C" int mp4x_zs_encode(int elem_bytes, const void* in, const int64_t* table, int nchunk, int64_t nblk,
+                              uint64_t* masks, int32_t* counts, int64_t* offs, void* vals, void* temp,
+                              size_t temp_bytes, void* stream) {
+  if (nblk <= 0) return 0;
+  if (nchunk <= 0) return MP4X_E_BADARG;
+  hipStream_t st = (hipStream_t)stream;
+  switch (elem_bytes) {
+    case 1: return zs_encode_t<uint8_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+    case 2: return zs_encode_t<uint16_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+    case 4: return zs_encode_t<uint32_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+    case 8: return zs_encode_t<uint64_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+extern "C" int mp4x_zs_decode(int elem_bytes, const uint64_t* masks, const int32_t* counts, const void* vals,
+                              const int64_t* table, int nchunk, int64_t nblk, void* out, int64_t* offs, void* temp,
+                              size_t temp_bytes, void* stream) {
+  if (nblk <= 0) return 0;
+  if (nchunk <= 0) return MP4X_E_BADARG;
+  hipStream_t st = (hipStream_t)stream;
+  switch (elem_bytes) {
+    case 1: return zs_decode_t<uint8_t>(masks, counts, vals, table, nchunk, nblk, out, offs, temp, temp_bytes, st);
+    case 2: return zs_decode_t<uint16_t>(masks, counts, vals, table, nchunk, nblk, out, offs, temp, temp_bytes, st);
+    case 4: return zs_decode_t<uint32_t>(masks, counts, vals, table, nchunk, nblk, out, offs, temp, temp_bytes, st);
+    case 8: return zs_decode_t<uint64_t>(masks, counts, vals, table, nchunk, nblk, out, offs, temp, temp_bytes, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
 }

@@ -15,7 +15,8 @@ serializer — and the engines pick the data path from it:
   ``Serializer<T>``).
 
 ``compress=True`` is the reference's Kryo ``DeflateSerializer`` wrapper
-(J/operand/DoubleOperand.java:267-277): lossless zlib on the host wire.  On the
+(J/operand/DoubleOperand.java:267-277): lossless zlib on the host wire, lossless
+zero suppression (kernel K6b, ``codec="zs"``) for device-tensor allreduce.  On the
 device path the lossy block-scaled fp8 / bf16 wire codecs (kernel K6) are
 selected with ``codec="fp8"`` / ``codec="bf16"``.
 """
@@ -95,7 +96,7 @@ class Operand:
         self.compress = bool(compress)
         self.serializer = serializer
         self.elem_type = elem_type
-        if codec not in (None, "none", "zlib", "fp8", "bf16"):
+        if codec not in (None, "none", "zlib", "fp8", "bf16", "zs"):
             raise ValueError(f"unknown codec {codec!r}")
         self.codec = None if codec == "none" else codec
 

@@ -179,6 +179,72 @@ def key_owner(keys: torch.Tensor, p: int, stream=None):
     return dest, hist
 
 
+ZS_BLOCK = 256
+
+
+def _zs_table(chunks, dev):
+    starts = [int(c[0]) for c in chunks]
+    lens = [int(c[1]) for c in chunks]
+    bs = [0]
+    for ln in lens:
+        bs.append(bs[-1] + (ln + ZS_BLOCK - 1) // ZS_BLOCK)
+    return torch.tensor(starts + lens + bs, dtype=torch.int64, device=dev), bs
+
+
+def zs_encode(x: torch.Tensor, chunks=None, stream=None):
+    """K6b lossless zero suppression of a flat tensor, per chunk ``(start, len)`` (default: whole).
+
+    Returns ``(masks int64[4*nblk], counts int32[nblk], vals x.dtype[nnz], nnz per chunk, blk_start)``;
+    chunk j owns blocks ``blk_start[j]:blk_start[j+1]`` and its non-zero words are the j-th
+    consecutive run of ``vals``.  One device->host read (the per-chunk totals)."""
+    _dev_check(x)
+    x = x.reshape(-1)
+    if chunks is None:
+        chunks = [(0, x.numel())]
+    dev = x.device
+    table, bs = _zs_table(chunks, dev)
+    nblk = bs[-1]
+    total = sum(int(c[1]) for c in chunks)
+    masks = torch.empty(4 * nblk, dtype=torch.int64, device=dev)
+    counts = torch.empty(nblk, dtype=torch.int32, device=dev)
+    offs = torch.zeros(nblk + 1, dtype=torch.int64, device=dev)
+    vals = torch.empty(max(total, 1), dtype=x.dtype, device=dev)
+    lib = native.hip()
+    tb = lib.mp4x_zs_temp_bytes(nblk)
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+    check(lib.mp4x_zs_encode(x.element_size(), x.data_ptr(), table.data_ptr(), len(chunks), nblk, masks.data_ptr(),
+                             counts.data_ptr(), offs.data_ptr(), vals.data_ptr(), temp.data_ptr(), tb,
+                             stream_ptr(stream)), "mp4x_zs_encode")
+    at = offs[torch.tensor(bs, dtype=torch.int64, device=dev)].tolist() if nblk else [0] * len(bs)
+    nnz = [at[j + 1] - at[j] for j in range(len(chunks))]
+    return masks, counts, vals[:at[-1]], nnz, bs
+
+
+def zs_decode(masks: torch.Tensor, counts: torch.Tensor, vals: torch.Tensor, chunks, out: torch.Tensor,
+              stream=None):
+    """Inverse of :func:`zs_encode`: chunk j (masks / counts / vals concatenated in chunk order)
+    expands into ``out.view(-1)[start_j : start_j + len_j]``."""
+    _dev_check(masks, counts, vals, out)
+    dev = out.device
+    table, bs = _zs_table(chunks, dev)
+    nblk = bs[-1]
+    if nblk == 0:
+        return out
+    if masks.numel() != 4 * nblk or counts.numel() != nblk:
+        raise ValueError("zs_decode: masks / counts do not match the chunk table")
+    if vals.element_size() != out.element_size():
+        raise ValueError("zs_decode: vals / out word size differ")
+    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    lib = native.hip()
+    tb = lib.mp4x_zs_temp_bytes(nblk)
+    temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=dev)
+    check(lib.mp4x_zs_decode(out.element_size(), masks.data_ptr(), counts.data_ptr(),
+                             vals.data_ptr() if vals.numel() else None, table.data_ptr(), len(chunks), nblk,
+                             out.data_ptr(), offs.data_ptr(), temp.data_ptr(), tb, stream_ptr(stream)),
+          "mp4x_zs_decode")
+    return out
+
+
 PACK_MAX_P = 2048
 
 

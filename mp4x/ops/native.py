@@ -43,6 +43,11 @@ _HIP_SIGS = {
     "mp4x_quant_fp8": (c_int, [c_int, c_void_p, c_int64, c_void_p, c_void_p, c_void_p]),
     "mp4x_dequant_reduce_fp8": (c_int, [c_int, c_void_p, PP, PP, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "mp4x_dequant_fp8": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
+    "mp4x_zs_temp_bytes": (c_size_t, [c_int64]),
+    "mp4x_zs_encode": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_size_t, c_void_p]),
+    "mp4x_zs_decode": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p,
+                               c_void_p, c_size_t, c_void_p]),
     "mp4x_key_owner": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "mp4x_sort_pairs_temp_bytes": (c_size_t, [c_int64, c_int]),
     "mp4x_sort_pairs_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_size_t, c_void_p]),

@@ -265,6 +265,9 @@ class DeviceEngine:
                 and op is not None and not getattr(op, "is_custom", False) and op.code == OpCode.SUM \
                 and self.device.type == "cuda":
             return codec
+        if kind == "allreduce" and op is not None and not getattr(op, "is_custom", False) and \
+                (codec == "zs" or (codec is None and getattr(operand, "compress", False))):
+            return "zs"       # lossless wire compression (the reference's compress=true contract)
         if forced in ("ipc1", "ipc2", "ipc2p") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             return forced
         if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
@@ -317,6 +320,8 @@ class DeviceEngine:
                            overlap=True if algo == "ipc2p" else None)
         elif algo == "rhd":
             self._allreduce_rhd(view, op)
+        elif algo == "zs":
+            self._allreduce_zs(view, op)
         elif algo == "fp8":
             self._allreduce_fp8(view)
         elif algo == "bf16":
@@ -502,6 +507,72 @@ class DeviceEngine:
         sends = [(mine, j) for j in range(p) if j != r and tos[r] > froms[r]]
         recvs = [(view[froms[j]:tos[j]], j) for j in range(p) if j != r and tos[j] > froms[j]]
         self.coll.p2p(sends, recvs)
+
+    def _allreduce_zs(self, view: torch.Tensor, op):
+        """Lossless compressed two-shot allreduce (``compress=True`` / ``codec="zs"``).
+
+        K6b zero suppression on both legs: encode the p destination chunks in one pass, ragged
+        all-to-all of (masks, counts, non-zero words), decode into p dense rows, K1 rank-ordered
+        reduce, encode the owned result, all-gather-v, decode every chunk in place.  Exact for
+        every dtype and op (only all-zero words are elided)."""
+        from . import zs
+        p, r = self.p, self.rank
+        n = view.numel()
+        es = view.element_size()
+        froms, tos, counts = self._chunking(n)
+        chunks = [(froms[j], counts[j]) for j in range(p)]
+        masks, cnts, vals, nnz, bs = zs.encode(view, chunks)
+        msz, csz, vsz = zs.split_sizes(bs, nnz)
+        dev = view.device
+        snnz = torch.tensor(nnz, dtype=torch.int64, device=dev)
+        rnnz = torch.empty_like(snnz)
+        self.coll.all_to_all_single(rnnz, snnz)
+        rn = [int(x) for x in rnnz.tolist()]
+        cr = counts[r]
+        nbr = zs.nblocks(cr)
+        rm = torch.empty(4 * nbr * p, dtype=torch.int64, device=dev)
+        rc = torch.empty(nbr * p, dtype=torch.int32, device=dev)
+        rv = torch.empty(sum(rn), dtype=view.dtype, device=dev)
+        self.coll.all_to_all_single(rm, masks, [4 * nbr] * p, msz)
+        self.coll.all_to_all_single(rc, cnts, [nbr] * p, csz)
+        self.coll.all_to_all_single(rv.view(torch.uint8), vals.contiguous().view(torch.uint8),
+                                    [x * es for x in rn], [x * es for x in vsz])
+        dense = torch.empty(max(1, p * cr), dtype=view.dtype, device=dev)
+        if cr:
+            zs.decode(rm, rc, rv, [(j * cr, cr) for j in range(p)], dense)
+        mine = view[froms[r]:tos[r]]
+        if cr:
+            self._reduce_into(mine, [dense[j * cr:(j + 1) * cr] for j in range(p)], op)
+        # all-gather leg: one packed byte segment per rank [masks | counts | words], 16-B padded
+        m2, c2, v2, nnz2, _ = zs.encode(mine, [(0, cr)])
+        t = torch.tensor([nnz2[0]], dtype=torch.int64, device=dev)
+        ts = [torch.empty_like(t) for _ in range(p)]
+        self.coll.all_gather(ts, t)
+        all_nnz = [int(x.item()) for x in ts]
+
+        def seg_bytes(j):
+            nb = zs.nblocks(counts[j])
+            return (nb * 36 + all_nnz[j] * es + 15) // 16 * 16
+
+        offs = [0]
+        for j in range(p):
+            offs.append(offs[-1] + seg_bytes(j))
+        wire = torch.zeros(offs[-1], dtype=torch.uint8, device=dev)
+        nb = zs.nblocks(cr)
+        seg = wire[offs[r]:offs[r + 1]]
+        seg[:nb * 32].copy_(m2.view(torch.uint8))
+        seg[nb * 32:nb * 36].copy_(c2.view(torch.uint8))
+        if nnz2[0]:
+            seg[nb * 36:nb * 36 + nnz2[0] * es].copy_(v2.contiguous().view(torch.uint8))
+        self._allgather_p2p(wire, offs[:-1], offs[1:])
+        for j in range(p):
+            if j == r or counts[j] == 0:
+                continue
+            nbj = zs.nblocks(counts[j])
+            sj = wire[offs[j]:offs[j + 1]]
+            zs.decode(sj[:nbj * 32].view(torch.int64), sj[nbj * 32:nbj * 36].view(torch.int32),
+                      sj[nbj * 36:nbj * 36 + all_nnz[j] * es].view(view.dtype), [(froms[j], counts[j])], view)
+        return view
 
     def _allreduce_fp8(self, view: torch.Tensor):
         """Compressed two-shot allreduce (K6 codec on the wire, f32 accumulation)."""

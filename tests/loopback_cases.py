@@ -181,3 +181,42 @@ def map_family_cases(eng, r, p):
     assert rc == [r + 1] * p
     for q in range(p):
         assert torch.all(recv[q * (r + 1):(q + 1) * (r + 1)] == q * 10 + r)
+
+
+def zs_cases(eng, r, p):
+    """Lossless zero-suppression allreduce (compress=True on device tensors): exact results for
+    sparse, dense and all-zero data, 1/2/8-byte words, ragged chunks."""
+    dev = eng.device
+    n = 3 * 256 * p + 77
+    g = torch.Generator().manual_seed(7 + r)
+    dense = torch.randn(n, generator=g).to(dev)
+    sparse = dense * (torch.rand(n, generator=g) < 0.05).to(dev)
+    for x, name in ((sparse, "sparse"), (dense, "dense")):
+        xs = []
+        for q in range(p):
+            gq = torch.Generator().manual_seed(7 + q)
+            d = torch.randn(n, generator=gq)
+            xs.append((d * (torch.rand(n, generator=gq) < 0.05)) if name == "sparse" else d)
+        y = x.clone()
+        eng.allreduce(y, 0, n, Operators.Float.MAX, Operands.FLOAT_OPERAND(compress=True))
+        ref = xs[0].clone()
+        for q in range(1, p):
+            ref = torch.maximum(ref, xs[q])
+        assert torch.equal(y.cpu(), ref), name
+    assert eng.stats.get("allreduce.zs", 0) >= 2
+    for dt, op in ((torch.int8, Operators.Byte.BITS_XOR), (torch.int16, Operators.Short.SUM),
+                   (torch.int64, Operators.Long.SUM)):
+        v = torch.zeros(n, dtype=dt, device=dev)
+        v[r::97] = r + 1
+        eng.allreduce(v, 0, n, op, Operands.LONG_OPERAND(compress=True))
+        exp = torch.zeros(n, dtype=torch.int64)
+        for q in range(p):
+            if op is Operators.Byte.BITS_XOR:
+                exp[q::97] ^= q + 1
+            else:
+                exp[q::97] += q + 1
+        assert torch.equal(v.cpu().long(), exp), dt
+    z = torch.zeros(n, device=dev)
+    eng.allreduce(z, 0, n, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="zs"))   # all-zero input
+    assert torch.all(z == 0)
+    return True

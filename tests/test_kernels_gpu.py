@@ -257,3 +257,26 @@ def test_reduce_by_key_first_is_k8_dedupe(dim, dtype):
     first.scatter_reduce_(0, inv, torch.arange(n, device=DEV), "amin")
     assert torch.equal(uk, ref_k) and torch.equal(uv, vals[first])
     assert int(cnt.sum()) == n
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16, torch.int8])
+def test_zs_codec_roundtrip_bits(dtype):
+    """K6b: masks / counts / compacted words decode to the identical bit pattern (-0.0, NaN kept)."""
+    K = _native()
+    from mp4x.parallel import zs
+    n = 10_000
+    x = (torch.randn(n, device=DEV) * 10).to(dtype)
+    x[torch.rand(n, device=DEV) < 0.8] = 0
+    if dtype.is_floating_point:
+        x[3] = -0.0
+        x[4] = float("nan")
+    chunks = [(0, 4000), (4000, 1), (4001, 0), (4001, n - 4001)]
+    masks, counts, vals, nnz, bs = K.zs_encode(x, chunks)
+    cm, cc, cv, cnnz, cbs = zs.encode(x.cpu(), chunks)            # CPU twin: identical format
+    assert nnz == cnnz and bs == cbs
+    assert torch.equal(masks.cpu(), cm) and torch.equal(counts.cpu(), cc)
+    iv = {1: torch.uint8, 2: torch.int16, 4: torch.int32, 8: torch.int64}[x.element_size()]
+    assert torch.equal(vals.cpu().view(iv), cv.view(iv))
+    out = torch.full_like(x, 7)
+    K.zs_decode(masks, counts, vals, chunks, out)
+    assert torch.equal(out.view(iv), x.view(iv))

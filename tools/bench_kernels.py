@@ -110,6 +110,18 @@ def main():
     res["k4_owner_sort_gather_200kx64_p8"] = {"ms": ms, "GBps": pv.numel() * 4 * 2 / ms / 1e6}
     ms = timeit(lambda: K.partition_pack(pk, pv, 8), a.iters)
     res["k4b_partition_pack_200kx64_p8"] = {"ms": ms, "GBps": pv.numel() * 4 * 2 / ms / 1e6}
+    # K6b lossless zero suppression, 256 MiB f32 at 5 % and 100 % density
+    zn = 64 << 20
+    for dens in (0.05, 1.0):
+        zx = torch.randn(zn, device=dev)
+        if dens < 1:
+            zx *= (torch.rand(zn, device=dev) < dens)
+        ms = timeit(lambda: K.zs_encode(zx), max(3, a.iters // 4))
+        res[f"k6b_zs_encode_256MiB_d{dens}"] = {"ms": ms, "GBps": zn * 4 / ms / 1e6}
+        m_, c_, v_, _, _ = K.zs_encode(zx)
+        zo = torch.empty_like(zx)
+        ms = timeit(lambda: K.zs_decode(m_, c_, v_, [(0, zn)], zo), max(3, a.iters // 4))
+        res[f"k6b_zs_decode_256MiB_d{dens}"] = {"ms": ms, "GBps": zn * 4 / ms / 1e6}
     print(json.dumps(res, indent=1))
 
 
