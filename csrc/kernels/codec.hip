@@ -224,77 +224,211 @@ __device__ __forceinline__ ZsChunk zs_locate(const int64_t* __restrict__ table, 
   return {es[lo] + lb * kZsBlock, el[lo] - lb * kZsBlock};
 }
 
+// Lane l owns the 4 consecutive words 4l..4l+3 of a block (one 16-B load for 4-byte words),
+// so mask word k holds bit l = "word 4l+k is non-zero".  The compaction stays in element
+// order: words before (l, k) = sum_k' popc(mask_k' & lanes<l) + non-zeros of lane l before k.
+template <typename W>
+__device__ __forceinline__ void zs_load4(const W* __restrict__ in, int64_t base, int64_t len, int lane, W (&v)[4]) {
+  const int64_t e = (int64_t)lane * 4;
+  const W* p = in + base + e;
+  if (e + 3 < len && (((uintptr_t)p) % (4 * sizeof(W))) == 0) {
+    if constexpr (sizeof(W) == 8) {
+      const u32x4 t0 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+      const u32x4 t1 = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + 1);
+      __builtin_memcpy(v, &t0, 16);
+      __builtin_memcpy(v + 2, &t1, 16);
+    } else if constexpr (sizeof(W) == 4) {
+      const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+      __builtin_memcpy(v, &t, 16);
+    } else if constexpr (sizeof(W) == 2) {
+      const uint2 t = *reinterpret_cast<const uint2*>(p);
+      __builtin_memcpy(v, &t, 8);
+    } else {
+      const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+      __builtin_memcpy(v, &t, 4);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = (e + k < len) ? p[k] : (W)0;
+  }
+}
+
+template <typename W>
+__device__ __forceinline__ void zs_store4(W* __restrict__ out, int64_t base, int64_t len, int lane, const W (&v)[4]) {
+  const int64_t e = (int64_t)lane * 4;
+  W* p = out + base + e;
+  if (e + 3 < len && (((uintptr_t)p) % (4 * sizeof(W))) == 0) {
+    if constexpr (sizeof(W) == 8) {
+      u32x4 t0, t1;
+      __builtin_memcpy(&t0, v, 16);
+      __builtin_memcpy(&t1, v + 2, 16);
+      __builtin_nontemporal_store(t0, reinterpret_cast<u32x4*>(p));
+      __builtin_nontemporal_store(t1, reinterpret_cast<u32x4*>(p) + 1);
+    } else if constexpr (sizeof(W) == 4) {
+      u32x4 t;
+      __builtin_memcpy(&t, v, 16);
+      __builtin_nontemporal_store(t, reinterpret_cast<u32x4*>(p));
+    } else if constexpr (sizeof(W) == 2) {
+      uint2 t;
+      __builtin_memcpy(&t, v, 8);
+      *reinterpret_cast<uint2*>(p) = t;
+    } else {
+      uint32_t t;
+      __builtin_memcpy(&t, v, 4);
+      *reinterpret_cast<uint32_t*>(p) = t;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (e + k < len) p[k] = v[k];
+  }
+}
+
+// The chunk table is staged in LDS (binary searches then cost LDS latency, not L2 round
+// trips), and each wave keeps ZU consecutive blocks in flight per iteration.
+constexpr int kZsMaxLdsChunks = 256;
+constexpr int ZU = 4;        // blocks in flight per wave: mask pass
+constexpr int ZU2 = 4;       // compaction / expansion (LDS-staged, ZU2 * 256 words per wave)
+
+// Always LDS (nchunk <= kZsMaxLdsChunks, checked on the host): a pointer that could be either
+// LDS or global compiles to flat loads, whose s_waitcnt also drains every outstanding global
+// load — that serialised the unrolled data loads (measured 2.2-3.6 TB/s before the fix).
+__device__ __forceinline__ const int64_t* zs_table_lds(const int64_t* __restrict__ table, int nchunk,
+                                                       int64_t* lds) {
+  for (int i = threadIdx.x; i < 3 * nchunk + 1; i += kBlock) lds[i] = table[i];
+  __syncthreads();
+  return lds;
+}
+
 template <typename W>
 __global__ __launch_bounds__(kBlock) void k_zs_mask(const W* __restrict__ in, const int64_t* __restrict__ table,
                                                     int nchunk, int64_t nblk, uint64_t* __restrict__ masks,
                                                     int32_t* __restrict__ counts) {
+  __shared__ int64_t lt_tab[3 * kZsMaxLdsChunks + 1];
+  const int64_t* tab = zs_table_lds(table, nchunk, lt_tab);
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t b = wave; b < nblk; b += nwaves) {
-    const ZsChunk c = zs_locate(table, nchunk, b);
-    W v[4];
+  for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
+    ZsChunk c[ZU];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t i = q * 64 + lane;
-      v[q] = i < c.len ? in[c.base + i] : (W)0;
-    }
-    int cnt = 0;
+    for (int u = 0; u < ZU; ++u) c[u] = (b0 + u < nblk) ? zs_locate(tab, nchunk, b0 + u) : ZsChunk{0, 0};
+    W v[ZU][4];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint64_t m = __ballot(v[q] != (W)0);
-      if (lane == 0) masks[b * 4 + q] = m;
-      cnt += __popcll(m);
+    for (int u = 0; u < ZU; ++u) zs_load4<W>(in, c[u].base, c[u].len, lane, v[u]);   // ZU loads in flight
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (b0 + u >= nblk) break;
+      int cnt = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint64_t m = __ballot(v[u][k] != (W)0);
+        if (lane == 0) masks[(b0 + u) * 4 + k] = m;
+        cnt += __popcll(m);
+      }
+      if (lane == 0) counts[b0 + u] = cnt;
     }
-    if (lane == 0) counts[b] = cnt;
   }
 }
 
-template <typename W>
+// Compaction and expansion stage each wave's ZU consecutive blocks through LDS.  Their
+// non-zero words form ONE contiguous range [offs[b0], offs[b0 + ZU]) of vals.  Global traffic
+// on that side is therefore coalesced full-line stores or loads. Per-lane scattered 4-byte
+// accesses would become one partial-line transaction each (measured 3.0 / 2.5 TB/s before).
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <typename W, int ZU>
 __global__ __launch_bounds__(kBlock) void k_zs_compact(const W* __restrict__ in, const int64_t* __restrict__ table,
                                                        int nchunk, int64_t nblk, const int64_t* __restrict__ offs,
                                                        W* __restrict__ vals) {
+  __shared__ int64_t lt_tab[3 * kZsMaxLdsChunks + 1];
+  __shared__ W stage[kBlock / 64][ZU * kZsBlock];
+  const int64_t* tab = zs_table_lds(table, nchunk, lt_tab);
   const int lane = threadIdx.x & 63;
+  W* st = stage[threadIdx.x >> 6];
   const uint64_t lt = (1ull << lane) - 1;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t b = wave; b < nblk; b += nwaves) {
-    const ZsChunk c = zs_locate(table, nchunk, b);
-    int64_t pos = offs[b];
-    W v[4];
+  for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
+    ZsChunk c[ZU];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t i = q * 64 + lane;
-      v[q] = i < c.len ? in[c.base + i] : (W)0;
-    }
+    for (int u = 0; u < ZU; ++u) c[u] = (b0 + u < nblk) ? zs_locate(tab, nchunk, b0 + u) : ZsChunk{0, 0};
+    W v[ZU][4];
+    int64_t pos[ZU];
+    const int64_t bend = (b0 + ZU < nblk) ? b0 + ZU : nblk;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint64_t m = __ballot(v[q] != (W)0);
-      if (v[q] != (W)0) vals[pos + __popcll(m & lt)] = v[q];
-      pos += __popcll(m);
+    for (int u = 0; u < ZU; ++u) {
+      zs_load4<W>(in, c[u].base, c[u].len, lane, v[u]);
+      pos[u] = (b0 + u < nblk) ? offs[b0 + u] : 0;
     }
+    const int64_t base = offs[b0];
+    int total = (int)(offs[bend] - base);
+    total = total < 0 ? 0 : (total > ZU * kZsBlock ? ZU * kZsBlock : total);   // never past the stage
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (b0 + u >= nblk) break;
+      int q = (int)(pos[u] - base);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q += __popcll(__ballot(v[u][k] != (W)0) & lt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (v[u][k] != (W)0) st[q++] = v[u][k];
+    }
+    wave_lds_sync();
+    for (int i = lane; i < total; i += 64) vals[base + i] = st[i];
+    wave_lds_sync();
   }
 }
 
-template <typename W>
+template <typename W, int ZU>
 __global__ __launch_bounds__(kBlock) void k_zs_expand(const uint64_t* __restrict__ masks,
                                                       const int64_t* __restrict__ offs, const W* __restrict__ vals,
                                                       const int64_t* __restrict__ table, int nchunk, int64_t nblk,
                                                       W* __restrict__ out) {
+  __shared__ int64_t lt_tab[3 * kZsMaxLdsChunks + 1];
+  __shared__ W stage[kBlock / 64][ZU * kZsBlock];
+  const int64_t* tab = zs_table_lds(table, nchunk, lt_tab);
   const int lane = threadIdx.x & 63;
+  W* st = stage[threadIdx.x >> 6];
   const uint64_t lt = (1ull << lane) - 1;
   const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t b = wave; b < nblk; b += nwaves) {
-    const ZsChunk c = zs_locate(table, nchunk, b);
-    int64_t pos = offs[b];
+  for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
+    ZsChunk c[ZU];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint64_t m = masks[b * 4 + q];
-      const int64_t i = q * 64 + lane;
-      if (i < c.len) out[c.base + i] = ((m >> lane) & 1) ? vals[pos + __popcll(m & lt)] : (W)0;
-      pos += __popcll(m);
+    for (int u = 0; u < ZU; ++u) c[u] = (b0 + u < nblk) ? zs_locate(tab, nchunk, b0 + u) : ZsChunk{0, 0};
+    const int64_t bend = (b0 + ZU < nblk) ? b0 + ZU : nblk;
+    const int64_t base = offs[b0];
+    int total = (int)(offs[bend] - base);
+    total = total < 0 ? 0 : (total > ZU * kZsBlock ? ZU * kZsBlock : total);   // never past the stage
+    uint64_t m[ZU][4];
+    int64_t pos[ZU];
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (b0 + u < nblk) {
+        pos[u] = offs[b0 + u];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[u][k] = masks[(b0 + u) * 4 + k];
+      }
     }
+    for (int i = lane; i < total; i += 64) st[i] = vals[base + i];     // coalesced
+    wave_lds_sync();
+    W v[ZU][4] = {};
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (b0 + u >= nblk) break;
+      int q = (int)(pos[u] - base);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q += __popcll(m[u][k] & lt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[u][k] = ((m[u][k] >> lane) & 1) ? st[q++] : (W)0;
+    }
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) zs_store4<W>(out, c[u].base, c[u].len, lane, v[u]);
+    wave_lds_sync();
   }
 }
 
@@ -306,14 +440,15 @@ __global__ void k_zs_total(const int64_t* __restrict__ offs, const int32_t* __re
 template <typename W>
 static int zs_encode_t(const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,
                        int32_t* counts, int64_t* offs, void* vals, void* temp, size_t temp_bytes, hipStream_t st) {
-  const int g = grid_for(nblk * 64, 1);
+  const int g = grid_for((nblk + ZU - 1) / ZU * 64, 1);
   hipLaunchKernelGGL(k_zs_mask<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, masks, counts);
   int e = (int)hipGetLastError();
   if (e) return e;
   e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
   if (e) return e;
   hipLaunchKernelGGL(k_zs_total, dim3(1), dim3(1), 0, st, offs, counts, nblk, offs + nblk);
-  hipLaunchKernelGGL(k_zs_compact<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, offs,
+  const int g2 = grid_for((nblk + ZU2 - 1) / ZU2 * 64, 1);
+  hipLaunchKernelGGL((k_zs_compact<W, ZU2>), dim3(g2), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, offs,
                      (W*)vals);
   return (int)hipGetLastError();
 }
@@ -324,8 +459,10 @@ static int zs_decode_t(const uint64_t* masks, const int32_t* counts, const void*
                        hipStream_t st) {
   int e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
   if (e) return e;
-  const int g = grid_for(nblk * 64, 1);
-  hipLaunchKernelGGL(k_zs_expand<W>, dim3(g), dim3(kBlock), 0, st, masks, offs, (const W*)vals, table, nchunk,
+  // offs[nblk] (= total words) bounds the last wave's staged range: it must be written here too
+  hipLaunchKernelGGL(k_zs_total, dim3(1), dim3(1), 0, st, offs, counts, nblk, offs + nblk);
+  const int g = grid_for((nblk + ZU2 - 1) / ZU2 * 64, 1);
+  hipLaunchKernelGGL((k_zs_expand<W, ZU2>), dim3(g), dim3(kBlock), 0, st, masks, offs, (const W*)vals, table, nchunk,
                      nblk, (W*)out);
   return (int)hipGetLastError();
 }
@@ -381,7 +518,7 @@ extern "C" int mp4x_zs_encode(int elem_bytes, const void* in, const int64_t* tab
                               uint64_t* masks, int32_t* counts, int64_t* offs, void* vals, void* temp,
                               size_t temp_bytes, void* stream) {
   if (nblk <= 0) return 0;
-  if (nchunk <= 0) return MP4X_E_BADARG;
+  if (nchunk <= 0 || nchunk > kZsMaxLdsChunks) return MP4X_E_BADARG;
   hipStream_t st = (hipStream_t)stream;
   switch (elem_bytes) {
     case 1: return zs_encode_t<uint8_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
@@ -396,7 +533,7 @@ extern "C" int mp4x_zs_decode(int elem_bytes, const uint64_t* masks, const int32
                               const int64_t* table, int nchunk, int64_t nblk, void* out, int64_t* offs, void* temp,
                               size_t temp_bytes, void* stream) {
   if (nblk <= 0) return 0;
-  if (nchunk <= 0) return MP4X_E_BADARG;
+  if (nchunk <= 0 || nchunk > kZsMaxLdsChunks) return MP4X_E_BADARG;
   hipStream_t st = (hipStream_t)stream;
   switch (elem_bytes) {
     case 1: return zs_decode_t<uint8_t>(masks, counts, vals, table, nchunk, nblk, out, offs, temp, temp_bytes, st);

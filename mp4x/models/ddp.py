@@ -40,7 +40,7 @@ class _Bucket:
 
 class GradientSynchronizer:
     def __init__(self, comm, params: Iterable[torch.nn.Parameter], bucket_mb: Optional[float] = None,
-                 average: bool = True, codec: Optional[str] = None):
+                 average: bool = True, codec: Optional[str] = None, autotune: bool = False):
         self.comm = comm
         self.p = comm.getSlaveNum()
         self.average = average
@@ -69,6 +69,25 @@ class GradientSynchronizer:
         self.cuda = self.buckets[0].buffer.is_cuda
         self.stream = torch.cuda.Stream() if self.cuda else None
         self._launched: List[_Bucket] = []
+        self.tuned = {}
+        if autotune:
+            self.autotune()
+
+    def autotune(self):
+        """Collective: measure the allreduce schedules once per distinct bucket (dtype, size
+        class) and pin the fastest in the device engine (see ``DeviceEngine.autotune_allreduce``).
+        Returns {bucket index: {algo: seconds}}."""
+        if self.p == 1 or self.operand.codec:
+            return self.tuned
+        seen = set()
+        for i, b in enumerate(self.buckets):
+            key = (b.buffer.dtype, max(0, b.buffer.numel() * b.buffer.element_size() - 1).bit_length())
+            if key in seen:
+                continue
+            seen.add(key)
+            op = for_dtype(Operators.Float.SUM, dtype_of_torch(b.buffer.dtype))
+            self.tuned[i] = self.comm.device.autotune_allreduce(b.buffer, op)
+        return self.tuned
 
     def _hook(self, p):
         b = self._owner[p]

@@ -33,14 +33,14 @@ def synthetic_batch(step: int, global_batch: int, din: int, dout: int, device, s
 
 
 def train_dp(comm, steps: int = 5, global_batch: int = 64, din: int = 64, hidden: int = 128, dout: int = 16,
-             lr: float = 0.05, device="cpu", bucket_mb: float = 0.01) -> List[float]:
+             lr: float = 0.05, device="cpu", bucket_mb: float = 0.01, autotune: bool = False) -> List[float]:
     """Returns the GLOBAL loss per step (mean over all ranks' shards)."""
     from ..operands import Operands
     from ..operators import Operators
     p, r = comm.getSlaveNum(), comm.getRank()
     torch.manual_seed(0)
     model = MLP(din, hidden, dout).to(device)
-    sync = GradientSynchronizer(comm, model.parameters(), bucket_mb=bucket_mb)
+    sync = GradientSynchronizer(comm, model.parameters(), bucket_mb=bucket_mb, autotune=autotune)
     opt = torch.optim.SGD(model.parameters(), lr=lr)
     losses = []
     shard = global_batch // p

@@ -180,6 +180,7 @@ def key_owner(keys: torch.Tensor, p: int, stream=None):
 
 
 ZS_BLOCK = 256
+ZS_MAX_CHUNKS = 256      # the chunk table is staged in LDS
 
 
 def _zs_table(chunks, dev):
@@ -201,6 +202,8 @@ def zs_encode(x: torch.Tensor, chunks=None, stream=None):
     x = x.reshape(-1)
     if chunks is None:
         chunks = [(0, x.numel())]
+    if len(chunks) > ZS_MAX_CHUNKS:
+        raise ValueError(f"zs_encode: at most {ZS_MAX_CHUNKS} chunks per call")
     dev = x.device
     table, bs = _zs_table(chunks, dev)
     nblk = bs[-1]
@@ -225,6 +228,8 @@ def zs_decode(masks: torch.Tensor, counts: torch.Tensor, vals: torch.Tensor, chu
     """Inverse of :func:`zs_encode`: chunk j (masks / counts / vals concatenated in chunk order)
     expands into ``out.view(-1)[start_j : start_j + len_j]``."""
     _dev_check(masks, counts, vals, out)
+    if len(chunks) > ZS_MAX_CHUNKS:
+        raise ValueError(f"zs_decode: at most {ZS_MAX_CHUNKS} chunks per call")
     dev = out.device
     table, bs = _zs_table(chunks, dev)
     nblk = bs[-1]

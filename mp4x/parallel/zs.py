@@ -2,8 +2,9 @@
 
 Reference: ``compress=true`` wraps every Kryo stream in lossless Deflate
 (J/operand/DoubleOperand.java:267-277).  On device tensors the lossless codec is zero
-suppression: per 256-element block a 256-bit non-zero mask (4 × int64), a non-zero count and
-the compacted non-zero words.  Dense data costs 1/8 bit per element of masks plus the
+suppression: per 256-element block a 256-bit non-zero mask (4 × int64; bit l of mask word k <-> word
+4l + k, the layout of one wave whose lane l loads words 4l..4l+3), a non-zero count and the
+compacted non-zero words in element order.  Dense data costs 1/8 bit per element of masks plus the
 counts, so ``DeviceEngine`` only sends encoded chunks when they are smaller than raw.
 
 The CPU twin produces the identical format with torch ops so the gloo / loopback tests run
@@ -53,7 +54,7 @@ def encode(x: torch.Tensor, chunks: Sequence[Tuple[int, int]]):
         nb = nblocks(ln)
         pad = torch.zeros(nb * BLOCK, dtype=bits.dtype)
         pad[:ln] = bits[s:s + ln]
-        nz = (pad != 0).view(nb, 4, 64)
+        nz = (pad != 0).view(nb, 64, 4).transpose(1, 2)      # mask k, bit l <-> word 4l + k
         ms.append((nz.long() * w).sum(-1).reshape(-1))
         cs.append(nz.sum((1, 2)).to(torch.int32))
         v = x[s:s + ln][bits[s:s + ln] != 0]
@@ -77,7 +78,7 @@ def decode(masks: torch.Tensor, counts: torch.Tensor, vals: torch.Tensor, chunks
     for s, ln in chunks:
         nb = nblocks(ln)
         m = masks[4 * mb:4 * (mb + nb)]
-        nz = ((m[:, None] >> lanes) & 1).bool().reshape(-1)[:ln]
+        nz = ((m[:, None] >> lanes) & 1).bool().view(nb, 4, 64).transpose(1, 2).reshape(-1)[:ln]
         k = int(nz.sum())
         seg = torch.zeros(ln, dtype=o.dtype)
         seg[nz] = vals[vo:vo + k]

@@ -9,16 +9,16 @@ torch = pytest.importorskip("torch")
 from harness import run_ranks  # noqa: E402
 
 
-def _mlp(comm):
+def _mlp(comm, autotune=False):
     from mp4x.models.mlp import train_dp
-    return train_dp(comm, steps=6, global_batch=48)
+    return train_dp(comm, steps=6, global_batch=48, autotune=autotune)
 
 
-@pytest.mark.parametrize("p", [2, 3])
-def test_dp_mlp_matches_single_process(p):
+@pytest.mark.parametrize("p,autotune", [(2, False), (3, False), (2, True)])
+def test_dp_mlp_matches_single_process(p, autotune):
     from mp4x.models.mlp import train_single
     ref = train_single(steps=6, global_batch=48)
-    res, code, _ = run_ranks(p, _mlp, timeout=120)
+    res, code, _ = run_ranks(p, _mlp, (autotune,), timeout=120)
     for r, losses in res.items():
         np.testing.assert_allclose(losses, ref, rtol=2e-5, atol=1e-6)
 
