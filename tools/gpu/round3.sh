@@ -11,6 +11,6 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_n1.lo
 timeout -k 10 300 python bench/loopback_paths.py > gpurun_out/loopback_paths.jsonl 2>&1; rc=$?; echo lb rc=$rc; grep -v amdgpu.ids gpurun_out/loopback_paths.jsonl
 [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-LB_ITERS=2 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/lbprof" -o lb -- python3 "$GRAFT_REPO_ROOT/bench/loopback_paths.py" > "$GRAFT_REPO_ROOT/gpurun_out/lbprof.log" 2>&1; rc=$?
+LB_ITERS=2 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/lbprof" -o lb --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench/loopback_paths.py" > "$GRAFT_REPO_ROOT/gpurun_out/lbprof.log" 2>&1; rc=$?
 echo rocprof rc=$rc; find "$GRAFT_REPO_ROOT/gpurun_out/lbprof" -name "*kernel_stats.csv" | head -3
 exit $rc
