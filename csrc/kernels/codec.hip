@@ -366,6 +366,7 @@ __global__ __launch_bounds__(kBlock) void k_zs_compact(const W* __restrict__ in,
     }
     const int64_t base = offs[b0];
     int total = (int)(offs[bend] - base);
+    MP4X_DASSERT(total >= 0 && total <= ZU * kZsBlock);
     total = total < 0 ? 0 : (total > ZU * kZsBlock ? ZU * kZsBlock : total);   // never past the stage
 #pragma unroll
     for (int u = 0; u < ZU; ++u) {
@@ -403,6 +404,7 @@ __global__ __launch_bounds__(kBlock) void k_zs_expand(const uint64_t* __restrict
     const int64_t bend = (b0 + ZU < nblk) ? b0 + ZU : nblk;
     const int64_t base = offs[b0];
     int total = (int)(offs[bend] - base);
+    MP4X_DASSERT(total >= 0 && total <= ZU * kZsBlock);
     total = total < 0 ? 0 : (total > ZU * kZsBlock ? ZU * kZsBlock : total);   // never past the stage
     uint64_t m[ZU][4];
     int64_t pos[ZU];

@@ -9,6 +9,21 @@ namespace mp4x {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Device-side bounds checks of the debug build (tools/build_native.py --debug): report and trap
+// the wave, so a bad index fails at its source instead of as a later memory fault.
+#ifdef MP4X_DEBUG
+#define MP4X_DASSERT(cond)                                                                     \
+  do {                                                                                         \
+    if (!(cond)) {                                                                             \
+      printf("mp4x device assert failed: %s (%s:%d) block %d thread %d\n", #cond, __FILE__,    \
+             __LINE__, (int)blockIdx.x, (int)threadIdx.x);                                     \
+      __builtin_trap();                                                                        \
+    }                                                                                          \
+  } while (0)
+#else
+#define MP4X_DASSERT(cond) ((void)0)
+#endif
+
 constexpr int kBlock = 256;          // 4 wave64 per workgroup
 constexpr int kMaxGrid = 256 * 8;    // 256 CUs x 8 resident blocks: grid-stride beyond this
 

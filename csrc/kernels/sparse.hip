@@ -102,6 +102,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce_vec(const int64_t* __
     if (u >= nruns) continue;
     const int64_t s = starts[u];
     const int64_t e = (u + 1 < nruns) ? starts[u + 1] : n;
+    MP4X_DASSERT(s >= 0 && s < e && e <= n);
     if (sub == 0) {
       out_keys[u] = sk[s];
       if (out_count) out_count[u] = (int32_t)(e - s);
@@ -240,6 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restri
     int inb = rank;
     for (int q = 0; q < w; ++q) inb += wcnt[q * p + d];
     const int64_t ps = off[(int64_t)d * nblk + b] + inb;
+    MP4X_DASSERT(ps >= 0 && ps < n);
     out_keys[ps] = k;
     if (out_perm) out_perm[ps] = i;
     pos[tid] = ps;

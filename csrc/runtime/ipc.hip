@@ -141,6 +141,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
                                                               u32x4* __restrict__ out, uint32_t epoch,
                                                               const uint32_t* epoch_dev) {
   constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
   epoch = resolve_epoch(epoch, epoch_dev);
   if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t chunk = (nvec + p - 1) / p;

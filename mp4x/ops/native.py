@@ -19,7 +19,9 @@ from ..exceptions import NativeError, Mp4jException
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 NATIVE_DIR = os.path.join(os.path.dirname(_HERE), "_native")
-HIP_LIB = os.path.join(NATIVE_DIR, "libmp4x_hip.so")
+# MP4X_NATIVE_DEBUG=1: the -DMP4X_DEBUG build with device-side bounds asserts
+HIP_LIB = os.path.join(NATIVE_DIR, "libmp4x_hip_debug.so" if os.environ.get("MP4X_NATIVE_DEBUG") == "1"
+                       else "libmp4x_hip.so")
 HOST_LIB = os.path.join(NATIVE_DIR, "libmp4x_host.so")
 
 c_void_p, c_int, c_int64, c_double, c_size_t = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double, ctypes.c_size_t

@@ -9,7 +9,10 @@
   the TCP data-plane engine; plain g++, no GPU dependency.
 
 Incremental: objects are rebuilt only when a source or header is newer.
-Usage: python tools/build_native.py [--clean] [-j N]
+``--debug`` builds ``libmp4x_hip_debug.so`` instead: ``-O1 -g -DMP4X_DEBUG``, which turns on the
+device-side bounds asserts (``MP4X_DASSERT``: printf + trap) in the kernels; load it with
+``MP4X_NATIVE_DEBUG=1`` (SURVEY §5.2 "HIP kernel bounds checks in debug builds").
+Usage: python tools/build_native.py [--clean] [--debug] [-j N]
 """
 import argparse
 import concurrent.futures as cf
@@ -59,28 +62,30 @@ def run(cmd):
     return r.stdout
 
 
-def build_hip(jobs):
+def build_hip(jobs, debug=False):
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")) + glob.glob(os.path.join(CSRC, "runtime", "*.hip")))
     deps = headers()
-    os.makedirs(OBJ, exist_ok=True)
+    objdir = OBJ + ("_debug" if debug else "")
+    os.makedirs(objdir, exist_ok=True)
     objs = []
     todo = []
     for s in srcs:
-        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        o = os.path.join(objdir, os.path.basename(s) + ".o")
         objs.append(o)
         if newer(s, o, deps):
             todo.append((s, o))
 
     def comp(so):
         s, o = so
-        run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
+        opt = ["-O1", "-g", "-DMP4X_DEBUG"] if debug else ["-O3"]
+        run([HIPCC, f"--offload-arch={ARCH}"] + opt + ["-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
              "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
         return s
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for s in ex.map(comp, todo):
             print("  hipcc", os.path.relpath(s, ROOT))
-    out = os.path.join(OUT, "libmp4x_hip.so")
+    out = os.path.join(OUT, "libmp4x_hip_debug.so" if debug else "libmp4x_hip.so")
     if todo or not os.path.exists(out):
         tl = torch_lib_dir()
         libdir = tl or "/opt/rocm/lib"
@@ -131,13 +136,17 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--debug", action="store_true", help="device-assert build -> libmp4x_hip_debug.so")
     a = ap.parse_args(argv)
     if a.clean:
         shutil.rmtree(os.path.join(ROOT, "build"), ignore_errors=True)
         for f in glob.glob(os.path.join(OUT, "*.so")):
             os.remove(f)
     os.makedirs(OUT, exist_ok=True)
-    print(f"mp4x native build (arch {ARCH})")
+    print(f"mp4x native build (arch {ARCH}{', debug' if a.debug else ''})")
+    if a.debug:
+        build_hip(a.j, debug=True)
+        return 0
     build_hip(a.j)
     build_host(a.j)
     return 0
