@@ -244,6 +244,16 @@ extern "C" int mp4x_ipc_alloc(size_t bytes, void** ptr) {
 
 extern "C" int mp4x_ipc_free(void* ptr) { return (int)hipFree(ptr); }
 
+// PCI bus id of the current device: ranks compare them to detect a GPU shared by several
+// ranks (single-GPU rehearsal), where the per-block barriers need every rank's blocks
+// co-resident and the block count must shrink accordingly.
+extern "C" int mp4x_device_pci_id(char* buf, int len) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceGetPCIBusId(buf, len, dev);
+}
+
 extern "C" int mp4x_ipc_handle_size(void) { return (int)sizeof(hipIpcMemHandle_t); }
 
 extern "C" int mp4x_ipc_get_handle(void* ptr, void* handle_out) {

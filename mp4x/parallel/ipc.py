@@ -37,7 +37,12 @@ native.register_signatures({
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
                                    c_int, c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
+    "mp4x_device_pci_id": (c_int, [ctypes.c_char_p, c_int]),
 })
+
+# Resident 512-thread blocks per MI355X: 256 CUs x 4 (2048 threads / CU).  Per-block barriers
+# need block b of EVERY rank resident at once, so ranks sharing one GPU split this budget.
+_RESIDENT_BLOCKS = 1024
 
 ONESHOT, TWOSHOT = 0, 1
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64}
@@ -63,7 +68,14 @@ class IpcAllreduce:
         hsg = ctypes.create_string_buffer(hs)
         check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
         check(self.lib.mp4x_ipc_get_handle(self._sig, hsg), "ipc_get_handle(sig)")
-        allh = comm.server.call("allgather_obj", self.rank, hd.raw + hsg.raw)
+        pci = ctypes.create_string_buffer(64)
+        check(self.lib.mp4x_device_pci_id(pci, 64), "device_pci_id")
+        allh = comm.server.call("allgather_obj", self.rank, hd.raw + hsg.raw + pci.value)
+        ids = [bytes(b[2 * hs:]) for b in allh]
+        share = max(ids.count(i) for i in ids)
+        # ranks on one device (rehearsal): cap the grid so all ranks' blocks fit at once
+        self.max_blocks = 0 if share == 1 else max(8, _RESIDENT_BLOCKS // (2 * share))
+        self.shared_gpu = share > 1
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
         self._opened: List[c_void_p] = []
@@ -75,7 +87,7 @@ class IpcAllreduce:
                     self.sig_ptrs.append(self._sig.value)
                     continue
                 for i, lst in ((0, self.data_ptrs), (1, self.sig_ptrs)):
-                    h = ctypes.create_string_buffer(bytes(blob[i * hs:(i + 1) * hs]), hs)
+                    h = ctypes.create_string_buffer(bytes(blob[i * hs:(i + 1) * hs]), hs)   # pci id follows
                     ptr = c_void_p()
                     check(self.lib.mp4x_ipc_open_handle(h, ctypes.byref(ptr)), f"ipc_open_handle(rank {r})")
                     self._opened.append(ptr)
@@ -120,6 +132,9 @@ class IpcAllreduce:
         if total % 16 or out.data_ptr() % 16:
             raise Mp4jException("IPC allreduce needs 16-byte multiples")
         dt = int(dtype_of_torch(view.dtype))
+        if not blocks and self.max_blocks:
+            vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
+            blocks = max(1, min(self.max_blocks, -(-min(total, self.nbytes) // 16 // vec_per_block)))
         src = view.view(torch.uint8)
         dst = out.view(torch.uint8)
         if overlap is None:

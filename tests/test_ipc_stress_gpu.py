@@ -1,0 +1,92 @@
+"""Randomised soak of the IPC allreduce protocol (race detection).
+
+p processes share GPU 0 and run the SAME seeded random sequence of calls: sizes from 16 B to
+3 MiB through a 1 MiB buffer (so some calls are piecewise, pipelined or serial), one-shot /
+two-shot, SUM / MAX, f32 / bf16 / f64 / i32, in place and out of place, back to back with no
+host synchronisation in between.  Every result is checked exactly (integers, small-integer
+floats) against a local recomputation; the barrier error word must stay 0.
+"""
+import multiprocessing as mp
+import tempfile
+import traceback
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+ITERS = 120
+
+
+def _worker(port, q, seed):
+    try:
+        import random
+
+        import torch
+        from mp4x import Operators, ProcessCommSlave
+        from mp4x.parallel.ipc import ONESHOT, TWOSHOT, IpcAllreduce
+        torch.cuda.set_device(0)
+        comm = ProcessCommSlave("s", "127.0.0.1", port, heartbeat=False)
+        r, p = comm.getRank(), comm.getSlaveNum()
+        ipc = IpcAllreduce(comm, nbytes=1 << 20)
+        rng = random.Random(seed)
+        pending = []
+        bad = []
+        for it in range(ITERS):
+            dt = rng.choice([torch.float32, torch.bfloat16, torch.float64, torch.int32])
+            es = torch.empty(0, dtype=dt).element_size()
+            nbytes = rng.choice([16, 256, 4096, 65536, 300_000 // 16 * 16, (1 << 20) + 4096, 3 << 20])
+            n = nbytes // es
+            algo = rng.choice([ONESHOT, TWOSHOT])
+            opname = "SUM" if dt in (torch.int32, torch.float64) else rng.choice(["SUM", "MAX"])
+            overlap = rng.choice([True, False])
+            inplace = rng.choice([True, False])
+            # rank-dependent small integers: exact in every dtype, sums stay exact
+            base = torch.arange(n, device="cuda", dtype=torch.int64) % 13
+            x = ((base + r * 3 + it) % 17).to(dt)
+            out = x if inplace else torch.empty_like(x)
+            ops = {torch.float32: Operators.Float, torch.bfloat16: Operators.BFloat16,
+                   torch.float64: Operators.Double, torch.int32: Operators.Int}[dt]
+            ipc.allreduce(x, getattr(ops, opname), algo=algo, out=out, overlap=overlap)
+            pending.append((it, dt, n, opname, out))
+            if len(pending) >= 8 or it == ITERS - 1:   # check lazily: several calls in flight
+                torch.cuda.synchronize()
+                for it2, dt2, n2, op2, o in pending:
+                    b = torch.arange(n2, device="cuda", dtype=torch.int64) % 13
+                    xs = [((b + j * 3 + it2) % 17) for j in range(p)]
+                    ref = sum(xs) if op2 == "SUM" else torch.stack(xs).max(0).values
+                    if not torch.equal(o.to(torch.int64), ref):
+                        bad.append((it2, str(dt2), n2, op2))
+                pending = []
+        comm.barrier()
+        ew = ipc.error_word()
+        ipc.close()
+        comm.close(0)
+        q.put((r, "ok", (bad, ew)))
+    except BaseException:
+        q.put((-1, "err", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("p,seed", [(4, 1), (8, 2)])
+def test_ipc_protocol_random_soak(p, seed):
+    from mp4x import CommMaster
+    m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(m.port, q, seed)) for _ in range(p)]
+    for pr in procs:
+        pr.start()
+    try:
+        for _ in range(p):
+            r, st, val = q.get(timeout=420)
+            assert st == "ok", val
+            bad, ew = val
+            assert ew == 0, f"rank {r}: barrier timeout flag {ew}"
+            assert not bad, (r, bad[:5])
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+        m.stop(timeout=5)
