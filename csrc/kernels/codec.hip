@@ -33,7 +33,7 @@ __device__ __forceinline__ void load4(const void* p, int64_t e, int64_t n, float
   const S* s = reinterpret_cast<const S*>(p);
   if (e + 3 < n) {
     if constexpr (sizeof(S) == 4) {
-      u32x4 v = *reinterpret_cast<const u32x4*>(s + e);
+      u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + e));   // streamed once
       S t[4];
       __builtin_memcpy(t, &v, 16);
 #pragma unroll
@@ -66,7 +66,7 @@ __device__ __forceinline__ void store4(void* p, int64_t e, int64_t n, const floa
     if constexpr (sizeof(S) == 4) {
       u32x4 v;
       __builtin_memcpy(&v, t, 16);
-      *reinterpret_cast<u32x4*>(s + e) = v;
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(s + e));
     } else if constexpr (sizeof(S) == 2) {
       uint2 v;
       __builtin_memcpy(&v, t, 8);
@@ -95,7 +95,7 @@ __device__ __forceinline__ void quant_block(const float (&x)[4], uint32_t* q, fl
   float m = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
   m = wave_max(m);
   const float scale = m > 0.0f ? m / kFp8Max : 1.0f;
-  q[blk * 64 + lane] = pack_fp8(x, 1.0f / scale);
+  __builtin_nontemporal_store(pack_fp8(x, 1.0f / scale), q + blk * 64 + lane);
   if (lane == 0) scales[blk] = scale;
 }
 
@@ -139,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_reduce(void* __restrict__ ou
     float s[NIN];
 #pragma unroll
     for (int k = 0; k < NIN; ++k) {   // issue every load first: NIN independent requests in flight
-      w[k] = in.q[k][b * 64 + lane];
+      w[k] = __builtin_nontemporal_load(in.q[k] + b * 64 + lane);
       s[k] = in.s[k][b];
     }
 #pragma unroll
