@@ -70,8 +70,6 @@ def process_checks(comm: ProcessCommSlave, arr_size: int, obj_size: int, run_tim
     root = p - 1 if p > 1 else 0
     for name, dt, mk, ops in PRIM:
         operand = mk(compress)
-        if device != "cpu" and name in ("short",) and False:
-            continue
         for it in range(run_time):
             t0 = time.perf_counter()
             a = A.full(arr_size, -1, dt)

@@ -6,11 +6,11 @@ the current torch stream.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 
-from ..operators import DType, OpCode, dtype_of_torch
+from ..operators import DType, dtype_of_torch
 from . import native
 from .native import check, ptr_array, stream_ptr
 

@@ -13,7 +13,7 @@ from __future__ import annotations
 import ctypes
 import os
 import threading
-from typing import Optional, Sequence
+from typing import Sequence
 
 from ..exceptions import NativeError, Mp4jException
 

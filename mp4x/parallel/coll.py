@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import threading
 from collections import defaultdict
-from typing import List, Optional, Sequence, Tuple
+from typing import List, Sequence, Tuple
 
 import torch
 import torch.distributed as dist

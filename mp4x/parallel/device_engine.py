@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from ..exceptions import Mp4jException
-from ..operators import (DType, OpCode, Operator, dtype_of_torch, for_dtype, torch_dtype_of)
+from ..operators import DType, OpCode, Operator, dtype_of_torch, for_dtype
 from ..utils.commutils import CommUtils
 
 LOG = logging.getLogger("mp4x.device")
@@ -465,9 +465,7 @@ class DeviceEngine:
 
     def _allreduce_a2a(self, view: torch.Tensor, op):
         """Two-shot: all-to-all → rank-ordered K1 reduce → all-gather (allreduce split rule)."""
-        n = view.numel()
-        froms, tos, counts = self._chunking(n)
-        mine = view[froms[self.rank]:tos[self.rank]]
+        froms, tos, _ = self._chunking(view.numel())
         self._reduce_scatter_a2a(view, froms, tos, op)
         self._allgather_any(view, froms, tos)
         return view

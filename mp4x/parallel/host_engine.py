@@ -25,7 +25,7 @@ with ``barrier()``, :731, :1367).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List
 
 import numpy as np
 
@@ -233,8 +233,7 @@ class HostEngine:
                 held.append((rk, f, t))
         if r != root:
             parent = next(t[0] for t in tasks if t[1] == r)
-            if parent == root or True:
-                self.t.send(parent, tag, wire.pack_segments(arr, held, operand))
+            self.t.send(parent, tag, wire.pack_segments(arr, held, operand))
         return arr
 
     # ================================================================== MAP

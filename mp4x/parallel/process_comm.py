@@ -24,7 +24,6 @@ from __future__ import annotations
 
 import logging
 import os
-import sys
 import threading
 import time
 import traceback
@@ -35,13 +34,12 @@ import numpy as np
 from ..control.client import MasterClient
 from ..control.protocol import local_ip
 from ..exceptions import Mp4jException, RangeError
-from ..operands import Operand, Operands, Serializer, DEFAULT_SERIALIZER
-from ..operators import CustomOperator, DType, Operator, dtype_of_numpy
+from ..operands import Operand, Operands, DEFAULT_SERIALIZER
+from ..operators import CustomOperator
 from ..utils.commutils import CommUtils
 from ..utils.hashing import owner_of
 from .host_engine import HostEngine, choose_allreduce
 from .transport import HostTransport
-from . import wire
 
 LOG = logging.getLogger("mp4x.comm")
 
@@ -471,7 +469,7 @@ class ProcessCommSlave:
             # non-root results are unspecified by contract; the shm allreduce serves the root
             shm.allreduce(buf, frm, to, int(operand.dtype), int(operator.code))
             return arrData
-        froms, tos, counts = CommUtils.even_split(frm, to, self.slaveNum)
+        froms, tos, _ = CommUtils.even_split(frm, to, self.slaveNum)
         self.engine.ring_reduce_scatter(buf, froms, tos, operand, operator)
         self.engine.tree_gather(buf, froms, tos, operand, rootRank)
         return arrData

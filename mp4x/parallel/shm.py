@@ -20,7 +20,6 @@ from multiprocessing import shared_memory
 
 import numpy as np
 
-from ..exceptions import Mp4jException
 from ..ops import native
 from ..ops.native import check
 

@@ -28,9 +28,8 @@ from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
-from ..operators import OpCode, dtype_of_torch, for_dtype
+from ..operators import dtype_of_torch, for_dtype
 from ..utils.hashing import key_id
 
 

@@ -29,7 +29,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 from ..exceptions import Mp4jException
-from ..operands import Operand, Operands, DEFAULT_SERIALIZER
+from ..operands import Operand, Operands
 from ..utils.commutils import CommUtils
 from .process_comm import ProcessCommSlave, _is_device_tensor, _is_torch, _host_view
 from . import wire

@@ -19,7 +19,7 @@ import threading
 import time
 from collections import defaultdict
 from contextlib import contextmanager
-from typing import Dict, Optional
+from typing import Dict
 
 LOG = logging.getLogger("mp4x.trace")
 
