@@ -142,6 +142,7 @@ class DeviceEngine:
         self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
         self._ipc_obj = None
         self._ipc_large = None
+        self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
 
@@ -175,6 +176,9 @@ class DeviceEngine:
         if self._owns_pg and dist.is_initialized():
             try:
                 from torch.distributed.distributed_c10d import _abort_process_group
+                for c in self._rccl_variants.values():
+                    _abort_process_group(c.pg)
+                self._rccl_variants = {}
                 _abort_process_group(self.pg)
             except Exception:
                 try:
@@ -232,6 +236,23 @@ class DeviceEngine:
                 self.ipc_enabled = False
         return self._ipc_obj
 
+    RCCL_CTA_VARIANTS = (64, 112)
+
+    def rccl_variant(self, ctas: int):
+        """TorchColl over a second RCCL communicator created with ncclConfig minCTAs = maxCTAs =
+        ``ctas`` (channels).  RCCL's default channel count is a heuristic; on a full xGMI mesh more
+        channels can put more links and CUs on a large message, so autotune measures these
+        communicators side by side with the default one.  Collective, lazily created."""
+        c = self._rccl_variants.get(ctas)
+        if c is None:
+            from .coll import TorchColl
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.config.min_ctas = ctas
+            opts.config.max_ctas = ctas
+            pg = dist.new_group(ranks=list(range(self.p)), backend="nccl", pg_options=opts)
+            c = self._rccl_variants[ctas] = TorchColl(pg, self.backend)
+        return c
+
     def ipc_large(self):
         """Second IPC instance with a large buffer (``MP4X_IPC_LARGE_BYTES``, default 256 MiB)
         for messages above the two-shot tier, when autotuning (or ``MP4X_DEVICE_ALGO=ipc2``)
@@ -280,6 +301,9 @@ class DeviceEngine:
             return "a2a"
         if forced in ("rccl", "a2a"):
             return forced
+        if forced.startswith("rccl_c") and kind == "allreduce" and op is not None \
+                and self._algo_valid(forced, op, dtype, nbytes):
+            return forced
         if kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             if nbytes <= self.ipc_oneshot_max:
                 return "ipc1"
@@ -312,6 +336,8 @@ class DeviceEngine:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
             self.coll.all_reduce(view, op.code)
+        elif algo.startswith("rccl_c"):
+            self.rccl_variant(int(algo[6:])).all_reduce(view, op.code)
         elif algo in ("ipc1", "ipc2", "ipc2p"):
             from .ipc import ONESHOT, TWOSHOT
             nbytes = view.numel() * view.element_size()
@@ -337,6 +363,8 @@ class DeviceEngine:
     def _algo_valid(self, algo: str, op, dtype, nbytes: int) -> bool:
         if algo == "rccl":
             return self.rccl_ok(op, dtype)
+        if algo.startswith("rccl_c"):
+            return self.backend == "nccl" and self.rccl_ok(op, dtype)
         if algo in ("ipc1", "ipc2", "ipc2p"):
             return self._ipc_ok(op, dtype, nbytes)
         if algo == "rhd":
@@ -347,6 +375,8 @@ class DeviceEngine:
         c = []
         if self.rccl_ok(op, dtype):
             c.append("rccl")
+            if self.backend == "nccl" and nbytes >= (64 << 20):
+                c += [f"rccl_c{n}" for n in self.RCCL_CTA_VARIANTS]
         if self._ipc_ok(op, dtype, nbytes) and self.device.type == "cuda":
             if nbytes <= (4 << 20):
                 c.append("ipc1")
