@@ -158,7 +158,7 @@ def main():
             "vs_baseline": round(busbw / (ref / 1e3), 2) if ref else None,
             "dtype": "fp32",
             "data": "synthetic (torch.randn per rank)",
-            "config": {"model": "allreduceArray float[250000000] (1e9 bytes), Operators.Float.SUM",
+            "config": {"model": f"allreduceArray float[{n}] ({nbytes:.0e} bytes), Operators.Float.SUM",
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
                        "payload_bytes": nbytes, "algo": algo,
                        "in_place": p > 1, "autotune_ms": tuned},
