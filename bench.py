@@ -167,7 +167,9 @@ def main():
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
             "busbw_factor": factor,
-            "note": ("p=1: nothing crosses a link; busbw := algbw of the out-of-place single-rank allreduce"
+            "note": ("p=1: nothing crosses a link (nccl-tests busbw factor 2(p-1)/p = 0), so this is "
+                     "busbw := algbw of the out-of-place single-rank allreduce, a 1 GB HBM copy through K1; "
+                     "N>=2 values are xGMI-link-bound and not comparable to N=1 as a scaling base"
                      if p == 1 else "busbw = algbw * 2(p-1)/p; value = p * busbw"),
         }
         print(json.dumps(rec), flush=True)
