@@ -22,7 +22,13 @@
 #include <type_traits>
 #include <vector>
 
+#include <climits>
+
+#include <linux/futex.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "mp4x/ops.h"
 
@@ -191,11 +197,76 @@ void par_copy(void* dst, const void* src, int64_t bytes, int nt) {
   });
 }
 
+// ---------------------------------------------------------------- sense-counting barrier
+// Arrive: fetch_add on `count`; the last arriver resets it and bumps `gen`.  Waiters spin a
+// few `pause`s (short meetings: ~2 us for 2 threads), yield a little, then sleep on a futex on
+// `gen` (long meetings: no core burnt while a peer does real work, e.g. the root thread's
+// process-level collective).  `sleepers` lets the releaser skip the wake syscall when nobody
+// sleeps; both sides use seq_cst so a wake-up is never lost.  Process-shared for the /dev/shm
+// engine (shared futex), process-private for thread teams.
+struct BarrierWords {
+  std::atomic<uint32_t>* count;
+  std::atomic<uint32_t>* gen;
+  std::atomic<uint32_t>* abort;
+  std::atomic<uint32_t>* sleepers;
+  uint32_t n;
+  double timeout_s;
+  bool shared;
+};
+
+static inline long futex_op(std::atomic<uint32_t>* addr, int op, uint32_t val, const timespec* ts, bool shared) {
+  return syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), shared ? op : (op | FUTEX_PRIVATE_FLAG), val, ts,
+                 nullptr, 0);
+}
+
+static void barrier_wake_all(const BarrierWords& w) {
+  if (w.sleepers->load(std::memory_order_seq_cst)) futex_op(w.gen, FUTEX_WAKE, INT_MAX, nullptr, w.shared);
+}
+
+// 0 released, -1 timed out (aborts the barrier for everyone), -2 aborted.
+static int barrier_wait(const BarrierWords& w) {
+  if (w.abort->load(std::memory_order_acquire)) return -2;
+  const uint32_t g = w.gen->load(std::memory_order_acquire);
+  if (w.count->fetch_add(1, std::memory_order_acq_rel) == w.n - 1) {
+    w.count->store(0, std::memory_order_relaxed);
+    w.gen->fetch_add(1, std::memory_order_seq_cst);
+    barrier_wake_all(w);
+    return 0;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  uint64_t spins = 0;
+  const timespec nap = {0, 10 * 1000 * 1000};        // re-check abort / timeout every 10 ms
+  while (w.gen->load(std::memory_order_acquire) == g) {
+    if (w.abort->load(std::memory_order_relaxed)) return -2;
+    ++spins;
+    if (spins < 64) {                                // keep this spin SHORT (see TBarrier note)
+      __builtin_ia32_pause();
+      continue;
+    }
+    if (spins < 96) {
+      sched_yield();
+      continue;
+    }
+    w.sleepers->fetch_add(1, std::memory_order_seq_cst);
+    if (w.gen->load(std::memory_order_seq_cst) == g) futex_op(w.gen, FUTEX_WAIT, g, &nap, w.shared);
+    w.sleepers->fetch_sub(1, std::memory_order_seq_cst);
+    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > w.timeout_s) {
+      w.abort->store(1, std::memory_order_release);
+      w.gen->fetch_add(0, std::memory_order_seq_cst);
+      futex_op(w.gen, FUTEX_WAKE, INT_MAX, nullptr, w.shared);
+      return -1;
+    }
+  }
+  return 0;
+}
+
 // ---------------------------------------------------------------- shared-memory engine
 struct alignas(64) ShmHeader {
   std::atomic<uint32_t> count;
   std::atomic<uint32_t> gen;
   std::atomic<uint32_t> abort;
+  std::atomic<uint32_t> sleepers;
   uint32_t p;
   int64_t slot_bytes;
 };
@@ -214,30 +285,8 @@ struct Shm {
 
 int shm_barrier(Shm* s) {
   ShmHeader* h = s->hdr;
-  const uint32_t g = h->gen.load(std::memory_order_acquire);
-  if (h->count.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)s->p - 1) {
-    h->count.store(0, std::memory_order_relaxed);
-    h->gen.fetch_add(1, std::memory_order_release);
-    return 0;
-  }
-  auto t0 = std::chrono::steady_clock::now();
-  uint64_t spins = 0;
-  while (h->gen.load(std::memory_order_acquire) == g) {
-    if (h->abort.load(std::memory_order_relaxed)) return -2;
-    if (++spins < 256) {
-      __builtin_ia32_pause();           // short waits: stay on core
-    } else {
-      sched_yield();                    // long waits: give the core back
-      if ((spins & 1023) == 0) {
-        double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (el > s->timeout_s) {
-          h->abort.store(1, std::memory_order_relaxed);
-          return -1;
-        }
-      }
-    }
-  }
-  return 0;
+  BarrierWords w{&h->count, &h->gen, &h->abort, &h->sleepers, (uint32_t)s->p, s->timeout_s, true};
+  return barrier_wait(w);
 }
 
 }  // namespace
@@ -375,3 +424,125 @@ int mp4x_shm_broadcast(void* h, int es, void* buf, int64_t frm, int64_t to, int 
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- in-process thread barrier
+// ThreadCommSlave's threads meet 3-4 times per collective.  Python's threading.Barrier hands a
+// Condition lock around (~11 us per meeting); this sense-counting barrier spins briefly with
+// `pause` and then yields (2.2 us per meeting for 2 threads), and ctypes releases the GIL for
+// the whole wait.  The spin must stay SHORT: with 4096 pauses (~140 cycles each on recent Xeons)
+// the meeting cost rose to 67 us, because the spinners kept the cores the GIL holder needed.
+struct alignas(64) TBarrier {
+  std::atomic<uint32_t> count{0};
+  std::atomic<uint32_t> gen{0};
+  std::atomic<uint32_t> abort{0};
+  std::atomic<uint32_t> sleepers{0};
+  uint32_t n;
+  double timeout_s;
+  BarrierWords words() { return BarrierWords{&count, &gen, &abort, &sleepers, n, timeout_s, false}; }
+};
+
+extern "C" void* mp4x_tbarrier_create(int n, double timeout_s) {
+  if (n < 1) return nullptr;
+  TBarrier* b = new TBarrier();
+  b->n = (uint32_t)n;
+  b->timeout_s = timeout_s > 0 ? timeout_s : 1e30;
+  return b;
+}
+
+extern "C" void mp4x_tbarrier_destroy(void* h) { delete (TBarrier*)h; }
+
+extern "C" void mp4x_tbarrier_abort(void* h) {
+  TBarrier* b = (TBarrier*)h;
+  b->abort.store(1, std::memory_order_seq_cst);
+  futex_op(&b->gen, FUTEX_WAKE, INT_MAX, nullptr, false);   // sleepers re-check `abort`
+}
+
+extern "C" int mp4x_tbarrier_aborted(void* h) { return (int)((TBarrier*)h)->abort.load(std::memory_order_acquire); }
+
+// 0: released; -1: timed out (the barrier is then aborted for everyone); -2: aborted.
+extern "C" int mp4x_tbarrier_wait(void* h) {
+  TBarrier* b = (TBarrier*)h;
+  return barrier_wait(b->words());
+}
+
+// ---------------------------------------------------------------- native thread-team collectives
+// The thread level of ThreadCommSlave for host arrays, entirely below the GIL: every thread
+// makes ONE call per phase; the rendezvous, the data-parallel chunked reduction (thread t
+// reduces chunk t of [f, t) over all T buffers, the root thread's value first, then the others
+// in thread order — the reference's thread reduce, ThreadCommSlave.java:259-303) and the
+// copy-back all run in C++.  Python pays one GIL release/re-acquire per phase instead of one
+// per barrier.
+struct Team {
+  TBarrier bar;
+  std::vector<void*> slots;
+};
+
+extern "C" void* mp4x_team_create(int n, double timeout_s) {
+  if (n < 1) return nullptr;
+  Team* t = new Team();
+  t->bar.n = (uint32_t)n;
+  t->bar.timeout_s = timeout_s > 0 ? timeout_s : 1e30;
+  t->slots.assign(n, nullptr);
+  return t;
+}
+
+extern "C" void mp4x_team_destroy(void* h) { delete (Team*)h; }
+extern "C" int mp4x_team_barrier(void* h) { return mp4x_tbarrier_wait(&((Team*)h)->bar); }
+extern "C" int mp4x_team_aborted(void* h) { return mp4x_tbarrier_aborted(&((Team*)h)->bar); }
+extern "C" void mp4x_team_abort(void* h) { mp4x_tbarrier_abort(&((Team*)h)->bar); }
+
+static inline void team_chunk(int64_t f, int64_t t, int T, int tid, int64_t* lo, int64_t* hi) {
+  const int64_t n = t - f;
+  *lo = f + n * tid / T;
+  *hi = f + n * (tid + 1) / T;
+}
+
+static int team_reduce_phase(Team* tm, int tid, void* buf, int64_t f, int64_t t, int dtype, int op, int root) {
+  const int T = (int)tm->bar.n;
+  tm->slots[tid] = buf;
+  if (int rc = mp4x_tbarrier_wait(&tm->bar)) return rc;
+  const int es = esize(dtype);
+  int64_t lo, hi;
+  team_chunk(f, t, T, tid, &lo, &hi);
+  if (hi > lo) {
+    std::vector<const void*> ins;
+    ins.reserve(T);
+    ins.push_back((const char*)tm->slots[root] + lo * es);
+    for (int j = 0; j < T; ++j)
+      if (j != root) ins.push_back((const char*)tm->slots[j] + lo * es);
+    if (int rc = host_reduce(dtype, op, (char*)tm->slots[root] + lo * es, ins.data(), T, hi - lo, 1)) {
+      mp4x_tbarrier_abort(&tm->bar);
+      return rc;
+    }
+  }
+  return mp4x_tbarrier_wait(&tm->bar);
+}
+
+static int team_bcast_phase(Team* tm, int tid, void* buf, int64_t f, int64_t t, int es, int root) {
+  if (tid != root && t > f) std::memcpy((char*)buf + f * es, (const char*)tm->slots[root] + f * es, (t - f) * es);
+  return mp4x_tbarrier_wait(&tm->bar);
+}
+
+// [f, t) of every thread's buffer reduced into the root thread's buffer (then a barrier).
+extern "C" int mp4x_team_reduce(void* h, int tid, void* buf, int64_t f, int64_t t, int dtype, int op, int root) {
+  if (!esize(dtype)) return MP4X_E_UNSUPPORTED;
+  return team_reduce_phase((Team*)h, tid, buf, f, t, dtype, op, root);
+}
+
+// Root's [f, t) copied into every other thread's buffer: publish, barrier, copy, barrier.
+extern "C" int mp4x_team_bcast(void* h, int tid, void* buf, int64_t f, int64_t t, int elem_bytes, int root) {
+  Team* tm = (Team*)h;
+  tm->slots[tid] = buf;
+  if (int rc = mp4x_tbarrier_wait(&tm->bar)) return rc;
+  return team_bcast_phase(tm, tid, buf, f, t, elem_bytes, root);
+}
+
+// Fused thread-level allreduce (slaveNum == 1): publish, barrier, chunked reduce into thread
+// 0's buffer, barrier, copy-back, barrier.
+extern "C" int mp4x_team_allreduce(void* h, int tid, void* buf, int64_t f, int64_t t, int dtype, int op) {
+  Team* tm = (Team*)h;
+  const int es = esize(dtype);
+  if (!es) return MP4X_E_UNSUPPORTED;
+  if (int rc = team_reduce_phase(tm, tid, buf, f, t, dtype, op, 0)) return rc;
+  return team_bcast_phase(tm, tid, buf, f, t, es, 0);
+}

@@ -42,6 +42,73 @@ def _chunk(f: int, t: int, parts: int, i: int):
     return cf, ct
 
 
+class _TeamBarrier:
+    """The thread barrier of a ThreadCommSlave: the native thread team (csrc/host/host_ops.cpp
+    ``mp4x_team_*``) whose spin barrier both the Python-level choreography and the native
+    host-array thread reductions use (GIL released while waiting); ``threading.Barrier`` when
+    the host library is unavailable.  ``abort()`` breaks it, so a failing thread never leaves
+    its peers waiting."""
+
+    def __init__(self, n: int):
+        self._py = threading.Barrier(n)
+        self.team = None
+        self._lib = None
+        if n > 1:
+            try:
+                from ..ops import native
+                self._lib = native.host()
+                self.team = self._lib.mp4x_team_create(n, 0.0)
+            except Exception:
+                self.team = None
+
+    def wait(self):
+        if self.team:            # the same native barrier the team phases use (GIL released)
+            if self._lib.mp4x_team_barrier(self.team):
+                raise threading.BrokenBarrierError("thread barrier aborted")
+            return 0
+        return self._py.wait()
+
+    def abort(self):
+        self._py.abort()
+        if self.team:
+            self._lib.mp4x_team_abort(self.team)
+
+    @property
+    def broken(self) -> bool:
+        if self.team:
+            return bool(self._lib.mp4x_team_aborted(self.team))
+        return self._py.broken
+
+    def __del__(self):
+        try:
+            if self.team:
+                self._lib.mp4x_team_destroy(self.team)
+        except Exception:
+            pass
+
+
+_TEAM_DTYPES = None
+_TEAM_ON = __import__("os").environ.get("MP4X_THREAD_TEAM", "1") == "1"
+
+
+def _team_dtype(buf, operator):
+    """Native dtype code when ``buf`` / ``operator`` can take the native thread-team path."""
+    global _TEAM_DTYPES
+    if not isinstance(buf, np.ndarray) or buf.ndim != 1 or not buf.flags.c_contiguous:
+        return None
+    if getattr(operator, "is_custom", False) or not hasattr(operator, "code"):
+        return None
+    if _TEAM_DTYPES is None:
+        from ..operators import DType
+        _TEAM_DTYPES = {np.dtype(np.float64): int(DType.F64), np.dtype(np.float32): int(DType.F32),
+                        np.dtype(np.int64): int(DType.I64), np.dtype(np.int32): int(DType.I32),
+                        np.dtype(np.int16): int(DType.I16), np.dtype(np.int8): int(DType.I8)}
+    dt = _TEAM_DTYPES.get(buf.dtype)
+    if dt is None or int(getattr(operator, "dtype", dt)) != dt:
+        return None
+    return dt
+
+
 class ThreadCommSlave:
     """Process × thread communicator (reference ``ThreadCommSlave``)."""
 
@@ -50,7 +117,7 @@ class ThreadCommSlave:
         if threadNum < 1:
             raise Mp4jException("threadNum must be >= 1")
         self.threadNum = threadNum
-        self._barrier = threading.Barrier(threadNum)
+        self._barrier = _TeamBarrier(threadNum)
         self.processCommSlave = process_comm or ProcessCommSlave(loginName, masterHost, masterPort, **kw)
         self.rank = self.processCommSlave.getRank()
         self.slaveNum = self.processCommSlave.getSlaveNum()
@@ -80,6 +147,16 @@ class ThreadCommSlave:
             self._barrier.wait()
         except threading.BrokenBarrierError as e:
             raise Mp4jException("thread barrier broken") from e
+
+    def abort(self) -> None:
+        """Break the thread barriers (a failing thread releases its peers with an error)."""
+        self._barrier.abort()
+
+    def _team_call(self, fn, *args) -> None:
+        rc = fn(self._barrier.team, self.getThreadId(), *args)
+        if rc:
+            self._barrier.abort()
+            raise Mp4jException(f"thread team collective failed ({rc})")
 
     def barrier(self) -> None:
         self.threadBarrier()
@@ -437,6 +514,19 @@ class ThreadCommSlave:
         if self.threadNum == 1:
             return self.processCommSlave.allreduceArray(arrData, operand, operator, frm, to)
         CommUtils.isFromToLegal(frm, to)
+        if self._barrier.team and _TEAM_ON and not _is_device_tensor(arrData):
+            buf = _host_view(arrData, operand)
+            dt = _team_dtype(buf, operator)
+            if dt is not None:       # native thread team: one GIL round trip per phase
+                lib = self._barrier._lib
+                if self.slaveNum == 1:
+                    self._team_call(lib.mp4x_team_allreduce, buf.ctypes.data, frm, to, dt, int(operator.code))
+                    return arrData
+                self._team_call(lib.mp4x_team_reduce, buf.ctypes.data, frm, to, dt, int(operator.code), 0)
+                if self.getThreadId() == 0:
+                    self.processCommSlave.allreduceArray(arrData, operand, operator, frm, to)
+                self._team_call(lib.mp4x_team_bcast, buf.ctypes.data, frm, to, buf.itemsize, 0)
+                return arrData
         root = self._thread_reduce_array(arrData, operand, operator, frm, to, 0)
         tid = self.getThreadId()
         if tid == 0:
