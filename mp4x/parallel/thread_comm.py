@@ -208,6 +208,14 @@ class ThreadCommSlave:
     def _thread_reduce_array(self, arr, operand: Operand, operator, f: int, t: int, rt: int):
         """All T arrays' [f, t) reduced into thread rt's array (rt's value first, then threads in order)."""
         tid = self.getThreadId()
+        if self._barrier.team and _TEAM_ON and not _is_device_tensor(arr):
+            buf = _host_view(arr, operand)
+            dt = _team_dtype(buf, operator)
+            if dt is not None:     # native: publish + chunked reduce into rt's buffer + barrier
+                self._slots[tid] = arr
+                self._team_call(self._barrier._lib.mp4x_team_reduce, buf.ctypes.data, f, t, dt,
+                                int(operator.code), rt)
+                return self._slots[rt]
         self._publish(arr)
         T = self.threadNum
         order = [j for j in range(T) if j != rt]
