@@ -200,3 +200,81 @@ def stress(tc, iters):
 def test_thread_stress_interleaved_collectives():
     res, code, _ = run_ranks(2, stress, (150,), kind="thread", threads=4, timeout=240)
     assert code == 0 and all(all(v) for v in res.values())
+
+
+def _process_passthroughs(tc):
+    """Thread 0 of every process drives every ``XProcess`` pass-through (checkbyte/Thread*Check
+    :156-241 pattern); the other threads only join the final thread barrier."""
+    p, r, T = tc.getSlaveNum(), tc.getRank(), tc.getThreadNum()
+
+    def body(t):
+        if t == 0:
+            D, ops = Operands.DOUBLE_OPERAND(), Operators.Double
+            n = 40
+            fr = CommUtils.createProcessArrayFroms(n, p)
+            to = CommUtils.createProcessArrayTos(n, p)
+            a = np.full(n, -1.0)
+            a[fr[r]:to[r]] = r
+            tc.gatherArrayProcess(a, D, fr, to, 0)
+            if r == 0:
+                assert all((a[fr[i]:to[i]] == i).all() for i in range(p))
+            a = np.full(n, -1.0)
+            a[fr[r]:to[r]] = r
+            tc.allgatherArrayProcess(a, D, fr, to)
+            assert all((a[fr[i]:to[i]] == i).all() for i in range(p))
+            a = np.arange(n, dtype=np.float64) if r == 0 else np.zeros(n)
+            tc.scatterArrayProcess(a, D, fr, to, 0)
+            assert (a[fr[r]:to[r]] == np.arange(fr[r], to[r])).all()
+            a = np.full(n, 1.0 if r == 0 else 0.0)
+            tc.broadcastArrayProcess(a, D, 0, n, 0)
+            assert (a == 1).all()
+            assert tc.broadcastProcess(7.0 if r == 0 else 0.0, D, 0) == 7.0
+            a = np.ones(n)
+            tc.reduceScatterArrayProcess(a, D, ops.SUM, 0, [t_ - f_ for f_, t_ in zip(fr, to)])
+            assert (a[fr[r]:to[r]] == p).all()
+            a = np.ones(n)
+            tc.reduceArrayProcess(a, D, ops.SUM, 0, n, 0)
+            if r == 0:
+                assert (a == p).all()
+            assert tc.reduceProcess(1.0, D, ops.SUM, 0) == p or r != 0
+            a = np.ones(n)
+            tc.allreduceArrayProcess(a, D, ops.MAX, 0, n)
+            assert (a == 1).all()
+            a = np.ones(8)
+            tc.allreduceArrayRpcProcess(a, D, ops.SUM)
+            assert (a == p).all()
+            assert tc.allreduceRpcProcess(2.0, D, ops.SUM) == 2.0 * p
+            m = {"k": 1.0, f"u{r}": 1.0}
+            assert tc.allreduceMapProcess(m, D, ops.SUM)["k"] == p
+            got = tc.reduceMapProcess(m, D, ops.SUM, 0)
+            if r == 0:
+                assert got["k"] == p and len(got) == 1 + p
+            g = tc.gatherMapProcess({f"g{r}": 1.0}, D, 0)
+            if r == 0:
+                assert len(g) == p
+            lst = tc.allgatherMapProcess({f"a{r}": float(r)}, D)
+            assert [d[f"a{i}"] for i, d in enumerate(lst)] == [float(i) for i in range(p)]
+            b = tc.broadcastMapProcess({"b": 3.0} if r == 0 else {}, D, 0)
+            assert b == {"b": 3.0}
+            sm = tc.scatterMapProcess([{f"s{i}": float(i)} for i in range(p)] if r == 0 else None, D, 0)
+            assert sm == {f"s{r}": float(r)}
+            rs = tc.reduceScatterMapProcess([{f"x{i}": 1.0} for i in range(p)], D, ops.SUM)
+            assert rs == {f"x{r}": float(p)}
+            assert tc.allreduceSetUnionProcess({r}) == set(range(p))
+            assert tc.allreduceSetIntersectionProcess({r, 99}) == ({99} if p > 1 else {r, 99})
+            assert sorted(tc.allreduceListConcatProcess([r])) == list(range(p))
+            u = tc.reduceSetUnionProcess({r}, 0)
+            if r == 0:
+                assert u == set(range(p))
+            mu = tc.allreduceMapSetUnionProcess({"k": {r}})
+            assert mu["k"] == set(range(p))
+        tc.threadBarrier()
+        return True
+
+    return _run_threads(tc, body)
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_every_process_passthrough_from_thread0(p):
+    res, code, _ = run_ranks(p, _process_passthroughs, kind="thread", threads=2, timeout=120)
+    assert code == 0 and len(res) == p
