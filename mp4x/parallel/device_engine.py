@@ -313,6 +313,37 @@ class DeviceEngine:
             return "a2a"
         return "rccl"
 
+    # ------------------------------------------------------------------ hipGraph capture
+    _CAPTURABLE = ("rccl", "ipc1", "ipc2", "a2a", "rhd", "fp8", "bf16")
+
+    def capture(self, fn, warmup: int = 2):
+        """Capture ``fn()`` — a fixed sequence of device collectives on fixed tensors, e.g. a DDP
+        step's bucket allreduces — into one hipGraph and return the ``torch.cuda.CUDAGraph``;
+        ``graph.replay()`` then re-issues every kernel and RCCL call with no host launch cost.
+
+        Collective: every rank captures the same sequence.  The IPC instances switch to device
+        epochs first (``IpcAllreduce.prepare_graph``) so replays never reuse a flag value, and
+        while capturing ``select`` keeps to schedules without host synchronisation (no zs /
+        pipelined pieces / sparse)."""
+        if self.device.type != "cuda":
+            raise Mp4jException("capture needs a GPU device engine")
+        for inst in (self.ipc(), self._ipc_large):
+            if inst is not None:
+                inst.prepare_graph()
+        side = torch.cuda.Stream(device=self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                fn()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        self._sync()
+        self.barrier()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            fn()
+        self._sync()
+        return g
+
     def local_reduce(self, out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: int, operator):
         return local_reduce(out, inputs, f, t, operator)
 
@@ -327,6 +358,9 @@ class DeviceEngine:
             return arr
         op = self._op(operator, view)
         algo = self.select("allreduce", view.numel() * view.element_size(), op, view.dtype, operand)
+        if algo not in self._CAPTURABLE and view.is_cuda and torch.cuda.is_current_stream_capturing():
+            # host-synchronising schedule inside a hipGraph capture: use a capturable twin
+            algo = "ipc2" if algo == "ipc2p" else ("rccl" if self.rccl_ok(op, view.dtype) else "a2a")
         self._count("allreduce." + algo)
         self._run_allreduce(algo, view, op)
         return arr
