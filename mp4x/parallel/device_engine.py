@@ -790,6 +790,16 @@ class DeviceEngine:
         self._count("allgather_map")
         return allgather_map_device(self, mapData)
 
+    def reduce_scatter_map(self, mapDataList: List[Dict], operator):
+        from .sparse import reduce_scatter_map_device
+        self._count("reduce_scatter_map")
+        return reduce_scatter_map_device(self, mapDataList, operator)
+
+    def scatter_map(self, mapDataList, root: int):
+        from .sparse import scatter_map_device
+        self._count("scatter_map")
+        return scatter_map_device(self, mapDataList, root)
+
     def broadcast_map(self, mapData: Dict, root: int):
         from .sparse import broadcast_map_device
         self._count("broadcast_map")

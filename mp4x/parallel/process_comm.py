@@ -406,6 +406,9 @@ class ProcessCommSlave:
         if self.slaveNum == 1:
             return mapDataList[0]
         self._check_root(rootRank)
+        probe = next((d for d in mapDataList if d), {}) if self.rank == rootRank and mapDataList else {}
+        if self._map_on_device(probe):
+            return self.device.scatter_map(mapDataList if self.rank == rootRank else None, rootRank)
         blocks = [[d] for d in mapDataList] if self.rank == rootRank else None
         got = self.engine.tree_scatter_maps(blocks, operand, rootRank)
         if not got:
@@ -444,6 +447,8 @@ class ProcessCommSlave:
             return mapDataList[0]
         if len(mapDataList) != self.slaveNum:
             raise Mp4jException(f"mapDataList size={len(mapDataList)}, must be equal to slaveNum={self.slaveNum}")
+        if self._map_on_device(next((d for d in mapDataList if d), {})):
+            return self.device.reduce_scatter_map(mapDataList, operator)
         return self.engine.ring_reduce_scatter_maps([[d] for d in mapDataList], operand, operator)[0]
 
     def reduceScatterMapSpecial(self, mapDataListList: List[List[Dict]], operand: Operand, operator) -> List[Dict]:

@@ -361,6 +361,89 @@ def allgather_map_device(engine, mapData: Dict) -> List[Dict]:
     return out
 
 
+def _maps_by_dest(engine, maps: List[Dict]):
+    """A list of p maps (map j -> rank j) as per-dest (ids, rows) + counts + value shape; ONE
+    dictionary sync for all of them."""
+    d = _dictionary(engine)
+    new_all: Dict[str, int] = {}
+    id_lists = []
+    for m in maps:
+        ids, new = d.ids_for(list(m.keys()))
+        id_lists.append(ids)
+        new_all.update(new)
+    _sync_new_keys(engine, new_all)
+    ks, vs, counts, shape = [], [], [], None
+    for m, ids in zip(maps, id_lists):
+        vals = list(m.values())
+        dev = vals[0].device if vals else engine.device
+        if vals:
+            shape = tuple(vals[0].shape)
+            v = torch.stack([x.reshape(-1) for x in vals])
+        else:
+            v = torch.empty((0, 1), device=dev)
+        ks.append(torch.tensor(ids, dtype=torch.int64, device=dev))
+        vs.append(v)
+        counts.append(len(ids))
+    return ks, vs, counts, shape
+
+
+def reduce_scatter_map_device(engine, mapDataList: List[Dict], operator) -> Dict:
+    """``reduceScatterMap``: rank i gets the op-reduction of every rank's ``mapDataList[i]``.
+    One ragged all-to-all by explicit destination, then K5 reduce-by-key in rank order."""
+    ks, vs, counts, shape = _maps_by_dest(engine, mapDataList)
+    shape = engine.all_gather_object(shape)
+    shape = next((x for x in shape if x is not None), (1,))
+    dev = engine.device
+    width = 1
+    for d in shape:
+        width *= d
+    vs = [v if v.numel() else torch.empty((0, width), dtype=next((x.dtype for x in vs if x.numel()), torch.float32),
+                                          device=dev) for v in vs]
+    dt = next((v.dtype for v in vs if v.numel()), vs[0].dtype)
+    keys = torch.cat(ks) if ks else torch.empty(0, dtype=torch.int64, device=dev)
+    vals = torch.cat([v.to(dt) for v in vs])
+    send = torch.tensor(counts, dtype=torch.int64, device=keys.device)
+    recv = torch.empty_like(send)
+    engine.coll.all_to_all_single(recv, send)
+    rc = [int(x) for x in recv.tolist()]
+    rk = torch.empty(sum(rc), dtype=torch.int64, device=keys.device)
+    engine.coll.all_to_all_single(rk, keys, rc, counts)
+    rv = torch.empty((sum(rc), vals.shape[1]), dtype=vals.dtype, device=vals.device)
+    engine.coll.all_to_all_single(rv, vals, rc, counts)
+    op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(rv.dtype))
+    uk, uv, _ = _reduce_by_key(rk, rv, op)
+    return _tensors_map(engine, uk, uv, shape)
+
+
+def scatter_map_device(engine, mapDataList: Optional[List[Dict]], root: int) -> Dict:
+    """``scatterMap``: root's ``mapDataList[i]`` lands at rank i (grouped p2p from the root)."""
+    r, p = engine.rank, engine.p
+    if r == root:
+        ks, vs, counts, shape = _maps_by_dest(engine, mapDataList)
+        dt = next((v.dtype for v in vs if v.numel()), torch.float32)
+        meta = (counts, shape or (1,), str(dt).replace("torch.", ""))
+    else:
+        _sync_new_keys(engine, {})        # matches the root's one dictionary sync
+        meta = None
+    counts, shape, dt = engine.all_gather_object(meta)[root]
+    width = 1
+    for d in shape:
+        width *= d
+    dev = engine.device
+    if r == root:
+        sends = []
+        for j in range(p):
+            if j != root and counts[j]:
+                sends += [(ks[j], j), (vs[j].reshape(counts[j], width).to(getattr(torch, dt)).contiguous(), j)]
+        engine.coll.p2p(sends, [])
+        return _tensors_map(engine, ks[root], vs[root].reshape(counts[root], width), shape)
+    k = torch.empty(counts[r], dtype=torch.int64, device=dev)
+    v = torch.empty((counts[r], width), dtype=getattr(torch, dt), device=dev)
+    if counts[r]:
+        engine.coll.p2p([], [(k, root), (v, root)])
+    return _tensors_map(engine, k, v, shape)
+
+
 def broadcast_map_device(engine, mapData: Dict, root: int) -> Dict:
     """``broadcastMap``: root's map on every rank."""
     if engine.rank == root:

@@ -220,3 +220,23 @@ def zs_cases(eng, r, p):
     eng.allreduce(z, 0, n, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="zs"))   # all-zero input
     assert torch.all(z == 0)
     return True
+
+
+def scatter_family_cases(eng, r, p):
+    """scatterMap / reduceScatterMap with tensor values (explicit destinations)."""
+    from mp4x.parallel import sparse as S
+    dev = eng.device
+    lst = [{f"k{j}": torch.full((2,), float(r * 10 + j), device=dev), "common": torch.ones(2, device=dev)}
+           for j in range(p)]
+    got = S.reduce_scatter_map_device(eng, lst, Operators.Float.SUM)
+    assert set(got) == {f"k{r}", "common"}
+    assert torch.all(got["common"] == p) and torch.all(got[f"k{r}"] == sum(q * 10 + r for q in range(p)))
+    root = p - 1
+    sl = [({f"s{j}": torch.full((3,), float(j), device=dev)} if j != 1 else {}) for j in range(p)] \
+        if r == root else None
+    mine = S.scatter_map_device(eng, sl, root)
+    if r == 1:
+        assert mine == {}
+    else:
+        assert list(mine) == [f"s{r}"] and torch.all(mine[f"s{r}"] == r)
+    return True

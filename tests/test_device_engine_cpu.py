@@ -138,6 +138,12 @@ def sparse_engine(comm):
     ks, vs = comm.reduceSparse(torch.tensor([1, 2], dtype=torch.int64), torch.ones(2, 3), Operators.Float.SUM, 0)
     if r == 0:
         assert ks.tolist() == [1, 2] and torch.all(vs == p)
+    rsm = comm.reduceScatterMap([{f"t{j}": torch.ones(2)} for j in range(p)], Operands.FLOAT_OPERAND(),
+                                Operators.Float.SUM)
+    assert list(rsm) == [f"t{r}"] and torch.all(rsm[f"t{r}"] == p)
+    sm = comm.scatterMap([{f"q{j}": torch.full((2,), float(j))} for j in range(p)] if r == root else [{}] * p,
+                         Operands.FLOAT_OPERAND(), root)
+    assert list(sm) == [f"q{r}"] and torch.all(sm[f"q{r}"] == r)
     recv, rc = comm.alltoallArray(torch.full((p, 2), float(r)), [1] * p)
     assert rc == [1] * p and recv[:, 0].tolist() == [float(q) for q in range(p)]
     return "ok"

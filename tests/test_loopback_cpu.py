@@ -1,7 +1,7 @@
 """Device engine over the in-process loopback back-end, CPU tensors (no GPU needed)."""
 import pytest
 
-from loopback_cases import dense_cases, run_virtual, sparse_cases, zs_cases
+from loopback_cases import dense_cases, run_virtual, scatter_family_cases, sparse_cases, zs_cases
 
 
 @pytest.mark.parametrize("p", [2, 3, 5])
@@ -17,3 +17,8 @@ def test_loopback_sparse(p):
 @pytest.mark.parametrize("p", [2, 3])
 def test_loopback_zs_lossless(p):
     assert all(run_virtual(p, zs_cases))
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_loopback_scatter_maps(p):
+    assert all(run_virtual(p, scatter_family_cases))

@@ -2,7 +2,7 @@
 real HIP kernels — K1 rank-ordered reduce, K6 fp8 codec, K4/K5 sparse — without RCCL."""
 import pytest
 
-from loopback_cases import codec_cases, dense_cases, run_virtual, sparse_cases, zs_cases
+from loopback_cases import codec_cases, dense_cases, run_virtual, scatter_family_cases, sparse_cases, zs_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -25,3 +25,8 @@ def test_loopback_sparse_gpu(p):
 @pytest.mark.parametrize("p", [2, 4])
 def test_loopback_zs_lossless_gpu(p):
     assert all(run_virtual(p, zs_cases, device="cuda:0"))
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_loopback_scatter_maps_gpu(p):
+    assert all(run_virtual(p, scatter_family_cases, device="cuda:0"))
