@@ -177,6 +177,52 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
 }
 
+// ---------------------------------------------------------------- direct reduce-scatter / all-gather
+// The two halves of the two-shot as collectives of their own, over RAGGED per-rank ranges
+// (reduceScatterArray counts / allgatherArray froms-tos), in 16-byte vectors of the staged
+// buffers.  Reduce-scatter: rank r reads [lo_r, hi_r) from ALL p buffers at once and reduces
+// in registers (the fused peer-load + reduce of SURVEY C7).  All-gather: rank r pulls every
+// peer's segment, the same offset from all p-1 peers per step, so all links stream at once.
+struct Segs {
+  int64_t lo[kIpcMaxRanks];
+  int64_t hi[kIpcMaxRanks];
+};
+
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_reduce_range(IpcPtrs P, Signal* self, int rank, int64_t lo,
+                                                                   int64_t hi, u32x4* __restrict__ out,
+                                                                   uint32_t epoch, const uint32_t* epoch_dev) {
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && lo <= hi);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  for (int64_t v = lo + (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < hi; v += stride)
+    out[v - lo] = reduce_vec<DT, OP, NR>(P, v);
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+template <int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_gather(IpcPtrs P, Signal* self, int rank, Segs S,
+                                                             int64_t maxlen, u32x4* __restrict__ out, uint32_t epoch,
+                                                             const uint32_t* epoch_dev) {
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < maxlen; v += stride) {
+    u32x4 x[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (k != rank && S.lo[k] + v < S.hi[k]) x[k] = reinterpret_cast<const u32x4*>(P.data[k])[S.lo[k] + v];
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (k != rank && S.lo[k] + v < S.hi[k]) out[S.lo[k] + v] = x[k];
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
 // set per call by mp4x_ipc_allreduce (host-side, single-threaded use per communicator)
 static thread_local const uint32_t* g_epoch_dev = nullptr;
 
@@ -319,4 +365,108 @@ extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data
     case MP4X_F16: return ipc_dt<MP4X_F16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
     default: return MP4X_E_UNSUPPORTED;
   }
+}
+
+static int ipc_prepare(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p, IpcPtrs* P) {
+  if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p) return MP4X_E_BADARG;
+  for (int k = 0; k < kIpcMaxRanks; ++k) {
+    P->data[k] = k < p ? data_ptrs[k] : nullptr;
+    P->sig[k] = k < p ? (Signal*)signal_ptrs[k] : nullptr;
+    if (k < p && (((uintptr_t)P->data[k] & 15) || !P->sig[k])) return MP4X_E_BADARG;
+  }
+  return 0;
+}
+
+static int ipc_blocks(int blocks, int64_t nvec) {
+  if (blocks <= 0) {
+    int64_t b = (nvec + kIpcThreads - 1) / kIpcThreads;
+    blocks = (int)(b < 1 ? 1 : (b > kIpcMaxBlocks ? kIpcMaxBlocks : b));
+  }
+  return blocks > kIpcMaxBlocks ? kIpcMaxBlocks : blocks;
+}
+
+template <int DT, int OP>
+static int rs_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t lo, int64_t hi, void* out, uint32_t epoch,
+                 const uint32_t* edev, int blocks, hipStream_t st) {
+#define MP4X_RS_CASE(N)                                                                                 \
+  case N:                                                                                               \
+    hipLaunchKernelGGL((k_ipc_reduce_range<DT, OP, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, \
+                       rank, lo, hi, (u32x4*)out, epoch, edev);                                         \
+    return (int)hipGetLastError();
+  switch (p) {
+    MP4X_RS_CASE(2) MP4X_RS_CASE(3) MP4X_RS_CASE(4) MP4X_RS_CASE(5) MP4X_RS_CASE(6) MP4X_RS_CASE(7) MP4X_RS_CASE(8)
+    default: return MP4X_E_BADARG;
+  }
+#undef MP4X_RS_CASE
+}
+
+template <int DT>
+static int rs_dt(int op, const IpcPtrs& P, Signal* self, int rank, int p, int64_t lo, int64_t hi, void* out,
+                 uint32_t epoch, const uint32_t* edev, int blocks, hipStream_t st) {
+  switch (op) {
+    case MP4X_SUM: return rs_nr<DT, MP4X_SUM>(P, self, rank, p, lo, hi, out, epoch, edev, blocks, st);
+    case MP4X_MAX:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return rs_nr<DT, MP4X_MAX>(P, self, rank, p, lo, hi, out, epoch, edev, blocks, st);
+      return MP4X_E_UNSUPPORTED;
+    case MP4X_MIN:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return rs_nr<DT, MP4X_MIN>(P, self, rank, p, lo, hi, out, epoch, edev, blocks, st);
+      return MP4X_E_UNSUPPORTED;
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+// Reduce-scatter over staged buffers: out (16-B aligned) receives vectors [vec_lo, vec_hi) of
+// the op-reduction of all p buffers.  Every rank stages its WHOLE range before the call.
+extern "C" int mp4x_ipc_reduce_scatter(int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs, int rank,
+                                       int p, int64_t vec_lo, int64_t vec_hi, void* out, uint32_t epoch, int blocks,
+                                       const uint32_t* epoch_dev, void* stream) {
+  IpcPtrs P;
+  if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
+  if (vec_lo < 0 || vec_hi < vec_lo || ((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  blocks = ipc_blocks(blocks, vec_hi - vec_lo);
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case MP4X_F64: return rs_dt<MP4X_F64>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    case MP4X_F32: return rs_dt<MP4X_F32>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    case MP4X_I64: return rs_dt<MP4X_I64>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    case MP4X_I32: return rs_dt<MP4X_I32>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    case MP4X_BF16: return rs_dt<MP4X_BF16>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    case MP4X_F16: return rs_dt<MP4X_F16>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+// All-gather of ragged segments: seg_lo/seg_hi[p] (host arrays, 16-B vectors from the buffer
+// base); every rank stages its own segment at its offset; out (the same layout, 16-B aligned)
+// receives every peer's segment.
+extern "C" int mp4x_ipc_allgather(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
+                                  const int64_t* seg_lo, const int64_t* seg_hi, void* out, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream) {
+  IpcPtrs P;
+  if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
+  if ((uintptr_t)out & 15) return MP4X_E_BADARG;
+  Segs S;
+  int64_t maxlen = 0;
+  for (int k = 0; k < kIpcMaxRanks; ++k) {
+    S.lo[k] = k < p ? seg_lo[k] : 0;
+    S.hi[k] = k < p ? seg_hi[k] : 0;
+    if (k < p && (S.lo[k] < 0 || S.hi[k] < S.lo[k])) return MP4X_E_BADARG;
+    if (S.hi[k] - S.lo[k] > maxlen) maxlen = S.hi[k] - S.lo[k];
+  }
+  blocks = ipc_blocks(blocks, maxlen);
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+#define MP4X_AG_CASE(N)                                                                                     \
+  case N:                                                                                                   \
+    hipLaunchKernelGGL((k_ipc_gather<N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, S, maxlen, \
+                       (u32x4*)out, epoch, epoch_dev);                                                      \
+    return (int)hipGetLastError();
+  switch (p) {
+    MP4X_AG_CASE(2) MP4X_AG_CASE(3) MP4X_AG_CASE(4) MP4X_AG_CASE(5) MP4X_AG_CASE(6) MP4X_AG_CASE(7) MP4X_AG_CASE(8)
+    default: return MP4X_E_BADARG;
+  }
+#undef MP4X_AG_CASE
 }

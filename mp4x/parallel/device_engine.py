@@ -682,6 +682,10 @@ class DeviceEngine:
         algo = self.select("reduce_scatter", whole.numel() * whole.element_size(), op, whole.dtype, operand)
         if algo == "fp8":
             algo = "a2a"    # exact path for ragged RS; fp8 RS is used inside the compressed allreduce
+        if algo in ("rccl", "a2a") and self._ipc_direct_ok(op, whole):
+            if self._ipc_obj.reduce_scatter(flat, froms, tos, op):
+                self._count("reduce_scatter.ipc")
+                return arr
         self._count("reduce_scatter." + algo)
         equal = len(set(counts)) == 1
         if algo == "rccl" and equal and self.coll.reduce_scatter_ok:
@@ -703,9 +707,26 @@ class DeviceEngine:
     # ================================================================== allgather
     def allgather(self, arr: torch.Tensor, froms, tos):
         flat = self._flat(arr)
+        whole = flat[froms[0]:tos[-1]]
+        if whole.numel() and self._ipc_direct_ok(None, whole) and self._ipc_obj.allgather(flat, froms, tos):
+            self._count("allgather.ipc")
+            return arr
         self._count("allgather")
         self._allgather_any(flat, froms, tos)
         return arr
+
+    def _ipc_direct_ok(self, op, whole: torch.Tensor) -> bool:
+        """Direct IPC reduce-scatter / all-gather tier: up to the two-shot size, unless a schedule
+        is forced.  (The range alignment is checked by IpcAllreduce, rank-independently.)"""
+        nbytes = whole.numel() * whole.element_size()
+        if self.algo not in ("", "auto") or nbytes > self.ipc_twoshot_max or not self.ipc_enabled:
+            return False
+        if op is not None and not self._ipc_ok(op, whole.dtype, 16):
+            return False
+        if whole.is_cuda and torch.cuda.is_current_stream_capturing() and \
+                (self._ipc_obj is None or self._ipc_obj._epoch_dev is None):
+            return False
+        return self.ipc() is not None
 
     # ================================================================== broadcast / reduce
     def broadcast(self, arr: torch.Tensor, frm: int, to: int, root: int):

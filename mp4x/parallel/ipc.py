@@ -38,6 +38,10 @@ native.register_signatures({
                                    c_int, c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
     "mp4x_device_pci_id": (c_int, [ctypes.c_char_p, c_int]),
+    "mp4x_ipc_reduce_scatter": (c_int, [c_int, c_int, PP, PP, c_int, c_int, c_int64, c_int64, c_void_p,
+                                        ctypes.c_uint32, c_int, c_void_p, c_void_p]),
+    "mp4x_ipc_allgather": (c_int, [PP, PP, c_int, c_int, ctypes.POINTER(c_int64), ctypes.POINTER(c_int64),
+                                   c_void_p, ctypes.c_uint32, c_int, c_void_p, c_void_p]),
 })
 
 # Resident 512-thread blocks per MI355X: 256 CUs x 4 (2048 threads / CU).  Per-block barriers
@@ -206,6 +210,77 @@ class IpcAllreduce:
             off += m
             i += 1
         return out
+
+    # ---------------------------------------------------------------- RS / AG over ragged ranges
+    # Results are produced inside the staging buffer (always 16-byte aligned) and copied out, so
+    # whether a call qualifies depends only on the (rank-independent) ranges: every rank takes
+    # the same path without an extra agreement round.
+    def _range_ok(self, view: torch.Tensor, froms, tos) -> bool:
+        es = view.element_size()
+        base = froms[0]
+        if (tos[-1] - base) * es > self.nbytes:
+            return False
+        return all(((f - base) * es) % 16 == 0 and ((t - base) * es) % 16 == 0 for f, t in zip(froms, tos))
+
+    def _next_epoch(self, st):
+        if self._epoch_dev is not None:
+            check(self.lib.mp4x_ipc_bump_epoch(self._epoch_dev.data_ptr(), st), "ipc_bump_epoch")
+            return self._epoch_dev.data_ptr()
+        if torch.cuda.is_current_stream_capturing():
+            raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+        return None
+
+    def _blocks_for(self, nvec: int) -> int:
+        if not self.max_blocks:
+            return 0
+        return max(1, min(self.max_blocks, -(-nvec // 512)))
+
+    def reduce_scatter(self, view: torch.Tensor, froms, tos, op) -> bool:
+        """In place: ``view[froms[r]:tos[r]]`` <- op over all ranks of that range (ragged ranges
+        whose byte offsets are 16-byte multiples).  Returns False (nothing done) otherwise."""
+        if not self._range_ok(view, froms, tos) or not self.supports(view, op):
+            return False
+        es = view.element_size()
+        flat = view.view(-1)
+        base, r = froms[0], self.rank
+        st = stream_ptr()
+        n = (tos[-1] - base) * es
+        if n:
+            check(self.lib.mp4x_memcpy_async(self._data.value, flat[base:].data_ptr(), n, st), "ipc RS staging")
+        edev = self._next_epoch(st)
+        lo, hi = (froms[r] - base) * es // 16, (tos[r] - base) * es // 16
+        mine = self._data.value + lo * 16          # reduced in place inside the own buffer
+        check(self.lib.mp4x_ipc_reduce_scatter(int(dtype_of_torch(view.dtype)), int(op.code), self._pp_data[0],
+                                               self._pp_sig[0], r, self.p, lo, hi, mine, self.epoch,
+                                               self._blocks_for(hi - lo), edev, st), "mp4x_ipc_reduce_scatter")
+        if hi > lo:
+            check(self.lib.mp4x_memcpy_async(flat[froms[r]:].data_ptr(), mine, (hi - lo) * 16, st), "ipc RS out")
+        return True
+
+    def allgather(self, view: torch.Tensor, froms, tos) -> bool:
+        """In place: every rank's ``view[froms[j]:tos[j]]`` lands everywhere (ragged, 16-byte offsets)."""
+        if not self._range_ok(view, froms, tos):
+            return False
+        es = view.element_size()
+        flat = view.view(-1)
+        base, r = froms[0], self.rank
+        st = stream_ptr()
+        seg = (tos[r] - froms[r]) * es
+        if seg:
+            check(self.lib.mp4x_memcpy_async(self._data.value + (froms[r] - base) * es, flat[froms[r]:].data_ptr(),
+                                             seg, st), "ipc AG staging")
+        edev = self._next_epoch(st)
+        lo = (c_int64 * self.p)(*[(f - base) * es // 16 for f in froms])
+        hi = (c_int64 * self.p)(*[(t - base) * es // 16 for t in tos])
+        maxlen = max(h - l_ for l_, h in zip(lo, hi))
+        # peers' segments land in the OWN buffer (only the own segment is read remotely), then one copy out
+        check(self.lib.mp4x_ipc_allgather(self._pp_data[0], self._pp_sig[0], r, self.p, lo, hi, self._data.value,
+                                          self.epoch, self._blocks_for(maxlen), edev, st), "mp4x_ipc_allgather")
+        n = (tos[-1] - base) * es
+        if n:
+            check(self.lib.mp4x_memcpy_async(flat[base:].data_ptr(), self._data.value, n, st), "ipc AG out")
+        return True
 
     def prepare_graph(self):
         """Move the epoch counter to device memory so hipGraph replays get fresh epochs.

@@ -166,3 +166,72 @@ def test_ipc_allreduce_hipgraph_replay():
             if pr.is_alive():
                 pr.kill()
         m.stop(timeout=5)
+
+
+def _rsag_worker(port, q):
+    try:
+        import torch
+        from mp4x import Operators, ProcessCommSlave
+        from mp4x.parallel.ipc import IpcAllreduce
+        torch.cuda.set_device(0)
+        comm = ProcessCommSlave("t", "127.0.0.1", port, heartbeat=False)
+        r, p = comm.getRank(), comm.getSlaveNum()
+        ipc = IpcAllreduce(comm, nbytes=1 << 20)
+        errs = []
+        for dt, opname in ((torch.float32, "SUM"), (torch.bfloat16, "MAX"), (torch.int64, "SUM")):
+            es = torch.empty(0, dtype=dt).element_size()
+            q16 = 16 // es                                     # elements per 16 bytes
+            counts = [q16 * (3 + 5 * j) for j in range(p)]      # ragged, 16-byte multiples
+            base = 2 * q16
+            froms = [base + sum(counts[:j]) for j in range(p)]
+            tos = [f + c for f, c in zip(froms, counts)]
+            n = tos[-1] + 7
+            x = ((torch.arange(n, device="cuda") % 11) + r).to(dt)
+            ops = {torch.float32: Operators.Float, torch.bfloat16: Operators.BFloat16, torch.int64: Operators.Long}[dt]
+            y = x.clone()
+            assert ipc.reduce_scatter(y, froms, tos, getattr(ops, opname))
+            xs = [((torch.arange(n, device="cuda") % 11) + j).to(torch.float64) for j in range(p)]
+            ref = sum(xs) if opname == "SUM" else torch.stack(xs).max(0).values
+            if not torch.equal(y[froms[r]:tos[r]].double(), ref[froms[r]:tos[r]]):
+                errs.append(("rs", str(dt)))
+            if not torch.equal(y[:froms[0]], x[:froms[0]]) or not torch.equal(y[tos[-1]:], x[tos[-1]:]):
+                errs.append(("rs-outside", str(dt)))
+            z = torch.full((n,), -1, device="cuda").to(dt)
+            z[froms[r]:tos[r]] = r
+            assert ipc.allgather(z, froms, tos)
+            for j in range(p):
+                if not bool((z[froms[j]:tos[j]] == j).all()):
+                    errs.append(("ag", str(dt), j))
+            # a range whose byte offset is not a 16-byte multiple does not qualify (same on every rank)
+            assert not ipc.allgather(z, [froms[0] + 1] + froms[1:], tos)
+        torch.cuda.synchronize()
+        comm.barrier()
+        ew = ipc.error_word()
+        ipc.close()
+        comm.close(0)
+        q.put((r, "ok", (errs, ew)))
+    except BaseException:
+        q.put((-1, "err", traceback.format_exc()))
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_ipc_direct_reduce_scatter_allgather_ragged(p):
+    from mp4x import CommMaster
+    m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rsag_worker, args=(m.port, q)) for _ in range(p)]
+    for pr in procs:
+        pr.start()
+    try:
+        for _ in range(p):
+            r, st, val = q.get(timeout=240)
+            assert st == "ok", val
+            errs, ew = val
+            assert ew == 0 and not errs, (r, errs, ew)
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+        m.stop(timeout=5)
