@@ -441,16 +441,17 @@ class DeviceEngine:
             try:
                 self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
                 self._sync()
+                if c.startswith("ipc") and self._ipc_error():
+                    # a barrier timed out (bounded spins): agree on it and skip the timed calls
+                    raise Mp4jException("IPC barrier timeout during warm-up")
                 self.barrier()
                 t0 = time.perf_counter()
                 for _ in range(max(1, iters)):
                     self._run_allreduce(c, view, op)
                 self._sync()
                 dt = (time.perf_counter() - t0) / max(1, iters)
-                if c.startswith("ipc"):
-                    for inst in (self._ipc_obj, self._ipc_large):
-                        if inst is not None and inst.error_word():
-                            ok = False
+                if c.startswith("ipc") and self._ipc_error():
+                    ok = False
             except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
                 LOG.warning("autotune: %s failed: %s", c, e)
                 ok = False
@@ -462,6 +463,16 @@ class DeviceEngine:
         if best is not None and res[best] != float("inf"):
             self._tuned[_tune_key(view.dtype, op, nbytes)] = best
         return res
+
+    def _ipc_error(self) -> bool:
+        """Did any IPC barrier on ANY rank time out?  (Collective: MAX of the error words.)"""
+        mine = 0
+        for inst in (self._ipc_obj, self._ipc_large):
+            if inst is not None and inst.error_word():
+                mine = 1
+        t = torch.tensor([mine], dtype=torch.int32, device=self.device if self.backend == "nccl" else "cpu")
+        self.coll.all_reduce(t, OpCode.MAX)
+        return bool(t.item())
 
     def _sync(self):
         if self.device.type == "cuda":
