@@ -160,8 +160,8 @@ class DeviceEngine:
             host, port = addr.rsplit(":", 1)
             store = dist.TCPStore(host, int(port), self.p, False, timeout=timeout)
         kw = {}
-        if self.device.type == "cuda":
-            kw["device_id"] = self.device
+        if self.device.type == "cuda" and self.backend == "nccl":
+            kw["device_id"] = self.device       # eager RCCL communicator bound to this GPU
         dist.init_process_group(self.backend, store=store, rank=self.rank, world_size=self.p, timeout=timeout, **kw)
         self._store = store
         self.pg = dist.group.WORLD
@@ -432,6 +432,8 @@ class DeviceEngine:
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         op = self._op(operator, view)
         nbytes = view.numel() * view.element_size()
+        if candidates is None and os.environ.get("MP4X_AUTOTUNE_CANDIDATES"):
+            candidates = [c.strip() for c in os.environ["MP4X_AUTOTUNE_CANDIDATES"].split(",") if c.strip()]
         cands = [c for c in (candidates or self.allreduce_candidates(nbytes, op, view.dtype))
                  if self._algo_valid(c, op, view.dtype, nbytes)]
         times = []
