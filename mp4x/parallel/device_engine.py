@@ -745,6 +745,14 @@ class DeviceEngine:
     def broadcast(self, arr: torch.Tensor, frm: int, to: int, root: int):
         flat = self._flat(arr)
         if to > frm:
+            if self.algo == "composite" and to - frm >= self.p:
+                # van de Geijn, the reference's schedule (ProcessCommSlave.java:750-775): scatter
+                # from the root, then all-gather — kept for parity benchmarks (MP4X_DEVICE_ALGO)
+                self._count("broadcast.composite")
+                froms, tos, _ = CommUtils.even_split(frm, to, self.p)
+                self.scatter(flat, froms, tos, root)
+                self.allgather(flat, froms, tos)
+                return arr
             self._count("broadcast")
             self.coll.broadcast(flat[frm:to], root)
         return arr
@@ -755,7 +763,8 @@ class DeviceEngine:
         if view.numel() == 0:
             return arr
         op = self._op(operator, view)
-        if self.select("reduce", view.numel() * view.element_size(), op, view.dtype) == "rccl":
+        if self.algo != "composite" and \
+                self.select("reduce", view.numel() * view.element_size(), op, view.dtype) == "rccl":
             self._count("reduce.rccl")
             self.coll.reduce(view, root, op.code)
         else:   # reduce-scatter + gather (reference reduceArray composition, ProcessCommSlave.java:1390-1421)

@@ -87,12 +87,15 @@ def engine_matrix(comm, algo):
 
 
 @pytest.mark.parametrize("p", [2, 3, 4])
-@pytest.mark.parametrize("algo", ["rccl", "a2a", "rhd"])
+@pytest.mark.parametrize("algo", ["rccl", "a2a", "rhd", "composite"])
 def test_device_engine_gloo(p, algo):
     res, code, _ = run_ranks(p, engine_matrix, (algo,), timeout=180)
     st = res[0]
     if algo == "rhd":                            # forced RHD takes every op (K1 combines)
         assert st.get("allreduce.rhd", 0) >= 3
+        return
+    if algo == "composite":                      # reference schedules: scatter+AG, RS+gather
+        assert st.get("broadcast.composite", 0) >= 1 and st.get("reduce.a2a", 0) >= 1
         return
     assert st.get("allreduce.a2a", 0) >= 2      # bitwise + int16 always take the a2a schedule
     if algo == "rccl":
