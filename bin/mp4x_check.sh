@@ -12,6 +12,7 @@ ARR_SIZE=${ARR_SIZE:-1000000}
 OBJ_SIZE=${OBJ_SIZE:-1000}
 RUN_TIME=${RUN_TIME:-3}
 MODE=${MODE:-process}
+export MP4X_LOG_DIR=${MP4X_LOG_DIR:-log}
 COMPRESS=${COMPRESS:-false}
 TEST_RPC=${TEST_RPC:-false}
 DEVICE=${DEVICE:-cpu}

@@ -187,6 +187,11 @@ def main(argv=None) -> int:
     ap.add_argument("test_rpc", type=lambda s: s.lower() == "true")
     ap.add_argument("--device", default="cpu")
     a = ap.parse_args(argv)
+    # log/slave{,_warn,_error}.log when MP4X_LOG_DIR or MP4X_LOG_CONFIG is set (reference:
+    # config/log4j_slave.properties); stdout only otherwise
+    import os
+    from .utils.logconf import configure_logging
+    configure_logging("slave", log_dir=os.environ.get("MP4X_LOG_DIR", "-"))
     comm = None
     code = 0
     try:

@@ -451,8 +451,10 @@ def main(argv=None) -> int:
     if len(argv) < 2:
         print("Usage: python -m mp4x.control.master <slaveNum> <port>", file=sys.stderr)
         return 2
-    logging.basicConfig(level=os.environ.get("MP4X_LOG_LEVEL", "INFO"),
-                        format="%(asctime)s %(levelname)s [master] %(message)s")
+    # stdout + log/master{,_warn,_error}.log daily-rolling, or MP4X_LOG_CONFIG (reference:
+    # config/log4j_master.properties)
+    from ..utils.logconf import configure_logging
+    configure_logging("master")
     slave_num, port = int(argv[0]), int(argv[1])
     m = CommMaster(slave_num, port).start()
     print(f"mp4x master {m.host}:{m.port} slaveNum={slave_num}", flush=True)

@@ -38,3 +38,7 @@ def test_master_and_check_tool_cli(tmp_path, mode, p, threads):
     assert master.returncode == 0, mout
     assert "checks passed" in mout
     assert (tmp_path / f"kill_{port}.sh").exists()
+    # log4j-equivalent layout: log/master.log (+ _warn / _error), daily rolling
+    log = (tmp_path / "log" / "master.log").read_text()
+    assert "all slaves have sent close messages" in log and "master exit code 0" in log
+    assert (tmp_path / "log" / "master_error.log").exists()
