@@ -322,6 +322,18 @@ extern "C" int mp4x_ipc_read_error(void* signal, uint32_t* err) {
   return (int)hipMemcpy(err, (char*)signal + offsetof(Signal, error), 4, hipMemcpyDeviceToHost);
 }
 
+// The error word read on `stream` (a private non-blocking stream, so a poll from the collective
+// watchdog thread never serialises with the caller's streams); clear != 0 resets it after the
+// read, so one timed-out barrier is reported once instead of poisoning every later check.
+extern "C" int mp4x_ipc_error_word(void* signal, uint32_t* err, int clear, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  char* w = (char*)signal + offsetof(Signal, error);
+  hipError_t e = hipMemcpyAsync(err, w, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && clear) e = hipMemsetAsync(w, 0, 4, st);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipStreamSynchronize(st);
+}
+
 // algo 0 = one-shot, 1 = two-shot.  data_ptrs / signal_ptrs: p entries (own rank included,
 // peers as mapped by mp4x_ipc_open_handle).  nbytes must be a multiple of 16; the caller has
 // already placed this rank's input in data_ptrs[rank] (stream-ordered before this launch).

@@ -145,6 +145,9 @@ class DeviceEngine:
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
+        # fail-stop detector for hung / failed collectives (parallel/watchdog.py)
+        from . import watchdog
+        self.watchdog = watchdog.CollectiveWatchdog(self) if coll is None and watchdog.enabled() else None
 
     # ------------------------------------------------------------------ bootstrap
     def _init_pg(self):
@@ -171,6 +174,7 @@ class DeviceEngine:
     def abort(self):
         """Fail-stop teardown (``ncclCommAbort``): a rank blocked in a collective with a dead
         peer returns instead of hanging.  Called by ``ProcessCommSlave.close(code != 0)``."""
+        self._stop_watchdog()
         for name in ("_ipc_obj", "_ipc_large"):
             setattr(self, name, None)          # peers may be gone: no synchronising close
         if self._owns_pg and dist.is_initialized():
@@ -187,7 +191,13 @@ class DeviceEngine:
                     pass
             self._owns_pg = False
 
+    def _stop_watchdog(self):
+        wd = getattr(self, "watchdog", None)
+        if wd is not None:
+            wd.stop()
+
     def shutdown(self):
+        self._stop_watchdog()
         for name in ("_ipc_obj", "_ipc_large"):
             obj = getattr(self, name)
             if obj is not None:
@@ -437,27 +447,14 @@ class DeviceEngine:
         cands = [c for c in (candidates or self.allreduce_candidates(nbytes, op, view.dtype))
                  if self._algo_valid(c, op, view.dtype, nbytes)]
         times = []
-        for c in cands:
-            ok = True
-            dt = float("inf")
-            try:
-                self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
-                self._sync()
-                if c.startswith("ipc") and self._ipc_error():
-                    # a barrier timed out (bounded spins): agree on it and skip the timed calls
-                    raise Mp4jException("IPC barrier timeout during warm-up")
-                self.barrier()
-                t0 = time.perf_counter()
-                for _ in range(max(1, iters)):
-                    self._run_allreduce(c, view, op)
-                self._sync()
-                dt = (time.perf_counter() - t0) / max(1, iters)
-                if c.startswith("ipc") and self._ipc_error():
-                    ok = False
-            except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
-                LOG.warning("autotune: %s failed: %s", c, e)
-                ok = False
-            times.append(dt if ok else float("inf"))
+        if self.watchdog is not None:
+            self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
+        try:
+            for c in cands:
+                times.append(self._time_candidate(c, view, op, iters))
+        finally:
+            if self.watchdog is not None:
+                self.watchdog.paused -= 1
         tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
         self.coll.all_reduce(tt, OpCode.MAX)
         res = dict(zip(cands, tt.cpu().tolist()))
@@ -466,11 +463,35 @@ class DeviceEngine:
             self._tuned[_tune_key(view.dtype, op, nbytes)] = best
         return res
 
+    def _time_candidate(self, c: str, view: torch.Tensor, op, iters: int) -> float:
+        """Seconds per call of schedule ``c`` (inf when it failed on this rank).  Collective."""
+        ok = True
+        dt = float("inf")
+        try:
+            self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
+            self._sync()
+            if c.startswith("ipc") and self._ipc_error():
+                # a barrier timed out (bounded spins): agree on it and skip the timed calls
+                raise Mp4jException("IPC barrier timeout during warm-up")
+            self.barrier()
+            t0 = time.perf_counter()
+            for _ in range(max(1, iters)):
+                self._run_allreduce(c, view, op)
+            self._sync()
+            dt = (time.perf_counter() - t0) / max(1, iters)
+            if c.startswith("ipc") and self._ipc_error():
+                ok = False
+        except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
+            LOG.warning("autotune: %s failed: %s", c, e)
+            ok = False
+        return dt if ok else float("inf")
+
     def _ipc_error(self) -> bool:
         """Did any IPC barrier on ANY rank time out?  (Collective: MAX of the error words.)"""
         mine = 0
         for inst in (self._ipc_obj, self._ipc_large):
-            if inst is not None and inst.error_word():
+            # read-and-clear: a candidate that timed out must not poison the next one's check
+            if inst is not None and inst.error_word(clear=True):
                 mine = 1
         t = torch.tensor([mine], dtype=torch.int32, device=self.device if self.backend == "nccl" else "cpu")
         self.coll.all_reduce(t, OpCode.MAX)
@@ -659,11 +680,23 @@ class DeviceEngine:
         c = ((n + p - 1) // p + Q - 1) // Q * Q
         nblk = c // Q
         dev = view.device
-        padded = torch.zeros(p * c, dtype=view.dtype, device=dev)
-        padded[:n].copy_(view)
         q = torch.empty(p * c, dtype=torch.uint8, device=dev)
         s = torch.empty(p * nblk, dtype=torch.float32, device=dev)
-        K.quant_fp8(padded, q, s)     # one launch: chunks are whole quant blocks, so scales never straddle
+        # quantise straight from the caller's buffer when it is 16-byte aligned: a padded staging
+        # copy would move the payload through HBM twice more on each leg.  The quant kernel
+        # zero-fills a partial last block; whole blocks past n are zeroed here.
+        direct = n % 4 == 0 and view.data_ptr() % 16 == 0
+        if direct:
+            nb = (n + Q - 1) // Q
+            if nb < p * nblk:
+                q[nb * Q:].zero_()
+                s[nb:].zero_()
+            padded = None
+            K.quant_fp8(view, q, s)
+        else:
+            padded = torch.zeros(p * c, dtype=view.dtype, device=dev)
+            padded[:n].copy_(view)
+            K.quant_fp8(padded, q, s)   # one launch: chunks are whole quant blocks, so scales never straddle
         rq = torch.empty_like(q)
         rs = torch.empty_like(s)
         self.coll.all_to_all_single(rq, q)
@@ -678,8 +711,11 @@ class DeviceEngine:
         gs = torch.empty(p * nblk, dtype=torch.float32, device=dev)
         self.coll.all_gather_into_tensor(gq, mine_q)
         self.coll.all_gather_into_tensor(gs, mine_s)
-        K.dequant_fp8(gq, gs, p * c, padded)
-        view.copy_(padded[:n])
+        if direct:
+            K.dequant_fp8(gq, gs, n, view)
+        else:
+            K.dequant_fp8(gq, gs, p * c, padded)
+            view.copy_(padded[:n])
         return view
 
     # ================================================================== reduce-scatter
@@ -856,3 +892,28 @@ class DeviceEngine:
         if hasattr(self.coll, "_exchange"):
             return self.coll._exchange(obj)
         return self.comm.server.call("allgather_obj", self.rank, obj)
+
+
+def _watched(name, fn):
+    """Bracket a device collective for the watchdog (host time inside the call; a HIP event on
+    the stream when the outermost collective returns)."""
+    def wrapper(self, *args, **kwargs):
+        wd = self.watchdog
+        if wd is None:
+            return fn(self, *args, **kwargs)
+        tok = wd.begin(name)
+        try:
+            return fn(self, *args, **kwargs)
+        finally:
+            wd.end(tok, self.device)
+    wrapper.__name__ = fn.__name__
+    wrapper.__doc__ = fn.__doc__
+    wrapper.__wrapped__ = fn
+    return wrapper
+
+
+_WATCHED = ["allreduce", "autotune_allreduce", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",
+            "scatter", "allreduce_map", "all_to_all_v", "reduce_map", "gather_map", "allgather_map",
+            "reduce_scatter_map", "scatter_map", "broadcast_map", "barrier"]
+for _n in _WATCHED:
+    setattr(DeviceEngine, _n, _watched(_n, getattr(DeviceEngine, _n)))

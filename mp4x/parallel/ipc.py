@@ -33,6 +33,7 @@ native.register_signatures({
     "mp4x_ipc_open_handle": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
     "mp4x_ipc_close_handle": (c_int, [c_void_p]),
     "mp4x_ipc_read_error": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
+    "mp4x_ipc_error_word": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32), c_int, c_void_p]),
     "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
                                    c_int, c_void_p, c_void_p]),
@@ -109,6 +110,7 @@ class IpcAllreduce:
         self._pp_hi = None         # peer pointers of the upper half-buffers (pipelined large path)
         self._copy_stream = None
         self._epoch_dev = None     # device epoch counter for graph-captured calls (lazy)
+        self._sig_stream = None    # private stream for error-word reads (lazy)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -291,9 +293,16 @@ class IpcAllreduce:
             self._epoch_dev = torch.full((1,), self.epoch, dtype=torch.int32, device="cuda")
         return self
 
-    def error_word(self) -> int:
+    def error_word(self, clear: bool = False) -> int:
+        """This rank's barrier-timeout word (0 = fine, 1/2/3 = start/mid/end barrier timed out).
+
+        Read on a private stream (never serialises with the caller's streams; safe from the
+        watchdog thread); ``clear`` resets it so the next check starts clean."""
+        if self._sig_stream is None:
+            self._sig_stream = torch.cuda.Stream(device=self.device)
         v = ctypes.c_uint32(0)
-        check(self.lib.mp4x_ipc_read_error(self._sig, ctypes.byref(v)), "ipc_read_error")
+        check(self.lib.mp4x_ipc_error_word(self._sig, ctypes.byref(v), int(bool(clear)),
+                                           stream_ptr(self._sig_stream)), "ipc_error_word")
         return int(v.value)
 
     def close(self, sync: bool = True):

@@ -562,26 +562,39 @@ class ProcessCommSlave:
             return listData if self.slaveNum == 1 else list_concat(self.device, listData)
         return self.allreduceMapListConcat({"key": listData}, elementSerializer, elementType).get("key")
 
-    def allreduceSparse(self, keys, vals, operator):
+    @staticmethod
+    def _check_key_bits(keys, keyBits):
+        if keyBits is None:
+            return None
+        keyBits = int(keyBits)
+        if not 1 <= keyBits <= 63:
+            raise Mp4jException(f"keyBits {keyBits} outside [1, 63]")
+        if keys.numel() and (int(keys.min()) < 0 or int(keys.max()) >= (1 << keyBits)):
+            raise Mp4jException(f"keys outside [0, 2**{keyBits}) with keyBits={keyBits}")
+        return keyBits
+
+    def allreduceSparse(self, keys, vals, operator, keyBits: Optional[int] = None):
         """Sparse allreduce of (int64 id, value-row) pairs on the device engine (extension).
 
         Every rank returns ``(keys, vals)`` holding the op-reduction over all ranks of the rows
         sharing an id (the tensor form of ``allreduceMap`` for ``Map<String, float[]>``).
+        ``keyBits``: ids are known to lie in [0, 2**keyBits) (e.g. embedding rows), so the
+        reduce-by-key radix sort covers only those bits.
         """
         self._tick("allreduceSparse")
         if self.slaveNum == 1:
             return keys, vals
         from .sparse import allreduce_sparse
-        return allreduce_sparse(self.device, keys, vals, operator)
+        return allreduce_sparse(self.device, keys, vals, operator, self._check_key_bits(keys, keyBits))
 
-    def reduceSparse(self, keys, vals, operator, rootRank: int):
+    def reduceSparse(self, keys, vals, operator, rootRank: int, keyBits: Optional[int] = None):
         """Tensor form of ``reduceMap``: root gets the op-reduced union (others: their owned share)."""
         self._tick("reduceSparse")
         if self.slaveNum == 1:
             return keys, vals
         self._check_root(rootRank)
         from .sparse import reduce_sparse
-        return reduce_sparse(self.device, keys, vals, operator, rootRank)
+        return reduce_sparse(self.device, keys, vals, operator, rootRank, self._check_key_bits(keys, keyBits))
 
     def gatherSparse(self, keys, vals, rootRank: int):
         """Tensor form of ``gatherMap``: union at root, duplicate ids keep the lowest rank's row (K8)."""

@@ -6,10 +6,9 @@ maps → ring allgather → merge (ProcessCommSlave.java:2053-2088); set/list sp
 
 Device design (one process per GPU):
 
-* string keys become stable 64-bit ids (xxh64, :mod:`mp4x.utils.hashing`); a per-communicator
-  :class:`KeyDictionary` maps ids back to strings.  Only keys a rank has never seen before
-  are exchanged (host allgather), so a steady-state embedding / histogram sync moves no
-  strings at all;
+* keys become dense, rank-consistent ids (:class:`KeyDictionary`, numbered in sync rounds);
+  only keys a rank has never seen are exchanged (host allgather), so a steady-state embedding
+  / histogram sync moves no strings at all, and the id sort runs over ``bits`` bits only;
 * values live in one ``[n, dim]`` device tensor (``Map<String, float[]>`` rows);
 * owner of a key = ``(uint64)id % p``; kernel K4b partitions keys AND rows by owner in one
   fused LDS-multisplit pass (stable, deterministic; the hipCUB radix-sort K4 path remains
@@ -30,39 +29,48 @@ import numpy as np
 import torch
 
 from ..operators import dtype_of_torch, for_dtype
-from ..utils.hashing import key_id
 
 
 class KeyDictionary:
-    """id <-> string dictionary shared (incrementally) by all ranks of a communicator."""
+    """Rank-consistent DENSE ids for map keys (one dictionary per communicator).
+
+    Ids are handed out in sync rounds (:func:`_sync_new_keys`, one control-plane allgather):
+    every rank publishes the keys it has never seen, and every rank then numbers the union in
+    the same order — rank 0's new keys in its first-seen order, then rank 1's not yet numbered,
+    and so on — so all ranks agree with no coordinator and no hash collisions.  Dense ids keep
+    the sort keys short: K5's radix sort only covers :attr:`bits` = the bit length of the
+    largest id (3 onesweep passes instead of 8 for a million keys), and the owner ``id % p``
+    deals keys round-robin over the ranks.  Keys may be any hashable (the reference's are
+    ``String``)."""
 
     def __init__(self):
-        self.id2key: Dict[int, str] = {}
-        self.key2id: Dict[str, int] = {}
+        self.id2key: List = []
+        self.key2id: Dict = {}
 
-    def ids_for(self, keys) -> Tuple[List[int], Dict[str, int]]:
-        ids = []
-        new = {}
+    def unknown(self, keys) -> List:
+        """Keys this rank has never numbered (first-seen order, de-duplicated)."""
+        seen = set()
+        out = []
         for k in keys:
-            i = self.key2id.get(k)
-            if i is None:
-                i = key_id(k)
-                self.key2id[k] = i
-                other = self.id2key.get(i)
-                if other is not None and other != k:
-                    raise RuntimeError(f"64-bit key id collision: {k!r} vs {other!r}")
-                self.id2key[i] = k
-                new[k] = i
-            ids.append(i)
-        return ids, new
+            if k not in self.key2id and k not in seen:
+                seen.add(k)
+                out.append(k)
+        return out
 
-    def learn(self, pairs: Dict[str, int]) -> None:
-        for k, i in pairs.items():
-            other = self.id2key.get(i)
-            if other is not None and other != k:
-                raise RuntimeError(f"64-bit key id collision: {k!r} vs {other!r}")
-            self.id2key[i] = k
-            self.key2id[k] = i
+    def learn_round(self, proposals) -> None:
+        """Number the union of one sync round's proposals (every rank passes the same list)."""
+        for block in proposals:
+            for k in block or ():
+                if k not in self.key2id:
+                    self.key2id[k] = len(self.id2key)
+                    self.id2key.append(k)
+
+    def ids(self, keys) -> List[int]:
+        return [self.key2id[k] for k in keys]
+
+    @property
+    def bits(self) -> int:
+        return max(1, (len(self.id2key) - 1).bit_length())
 
 
 def _dictionary(engine) -> KeyDictionary:
@@ -72,20 +80,19 @@ def _dictionary(engine) -> KeyDictionary:
     return d
 
 
-def _sync_new_keys(engine, new: Dict[str, int]) -> None:
-    """Allgather (through the control plane) of the (string, id) pairs not published yet."""
-    blocks = engine.all_gather_object(new)
-    d = _dictionary(engine)
-    for r, m in enumerate(blocks):
-        if r != engine.rank and m:
-            d.learn(m)
+def _sync_new_keys(engine, new: List) -> None:
+    """One sync round: allgather (control plane) of every rank's unseen keys, numbered in rank
+    order on every rank.  Collective — ranks with nothing new still take part."""
+    _dictionary(engine).learn_round(engine.all_gather_object(list(new)))
 
 
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins
-def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op):
+def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bits: Optional[int] = None):
+    """``key_bits``: every key is in [0, 2**key_bits) (dense dictionary ids) — the radix sort
+    covers those bits only."""
     if keys.is_cuda:
         from ..ops.device_ops import reduce_by_key
-        return reduce_by_key(keys, vals, int(op.code) if vals is not None else 0)
+        return reduce_by_key(keys, vals, int(op.code) if vals is not None else 0, key_bits=key_bits)
     # CPU twin for the gloo test configuration only
     uk, inv, cnt = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)
     if vals is None:
@@ -191,7 +198,7 @@ def _allgather_v(engine, t: torch.Tensor, sizes: Optional[List[int]] = None) -> 
     return torch.cat([o[:s] for o, s in zip(outs, sizes)], 0)
 
 
-def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator):
+def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, key_bits: Optional[int] = None):
     """All ranks end with the op-reduction of every rank's (key, row) pairs, keys ascending per owner.
 
     ``keys`` int64 [n] (unique per rank), ``vals`` [n, dim] (or [n]).
@@ -200,7 +207,7 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator):
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
     rkeys, rvals = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
     all_k = _allgather_v(engine, uk)
     all_v = _allgather_v(engine, uv)
     return all_k, (all_v.view(-1) if squeeze else all_v)
@@ -209,11 +216,11 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator):
 OP_FIRST = 11     # native MP4X_FIRST: keep the first row of every key (K8 map merge)
 
 
-def _dedupe_first(keys: torch.Tensor, vals: Optional[torch.Tensor]):
+def _dedupe_first(keys: torch.Tensor, vals: Optional[torch.Tensor], key_bits: Optional[int] = None):
     """K8: unique keys ascending, each with its FIRST row in input (= rank) order."""
     if keys.is_cuda:
         from ..ops.device_ops import reduce_by_key
-        uk, uv, _ = reduce_by_key(keys, vals, OP_FIRST)
+        uk, uv, _ = reduce_by_key(keys, vals, OP_FIRST, key_bits=key_bits)
         return uk, uv
     uk, inv = torch.unique(keys, sorted=True, return_inverse=True)
     first = torch.full((uk.numel(),), keys.numel(), dtype=torch.int64)
@@ -227,7 +234,7 @@ def allgather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor):
     return _allgather_v(engine, keys, sizes), _allgather_v(engine, vals, sizes), sizes
 
 
-def gather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, root: int):
+def gather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, root: int, key_bits: Optional[int] = None):
     """Root receives every rank's pairs (grouped p2p, all links at once) and merges them with
     K8 (duplicate key: the lowest rank's row survives).  Non-root ranks get their input back."""
     sizes = _row_counts(engine, keys.shape[0], keys.device)
@@ -252,7 +259,7 @@ def gather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, root: int):
             if vb.numel():
                 recvs.append((vb, j))
     engine.coll.p2p([], recvs)
-    return _dedupe_first(torch.cat(ks), torch.cat(vs))
+    return _dedupe_first(torch.cat(ks), torch.cat(vs), key_bits)
 
 
 def broadcast_sparse(engine, keys: Optional[torch.Tensor], vals: Optional[torch.Tensor], root: int):
@@ -272,14 +279,15 @@ def broadcast_sparse(engine, keys: Optional[torch.Tensor], vals: Optional[torch.
     return keys, vals
 
 
-def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root: int):
+def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root: int,
+                  key_bits: Optional[int] = None):
     """Owner exchange + K5 reduce-by-key, then the owner-disjoint pieces go to ``root``."""
     squeeze = vals.dim() == 1
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
     rkeys, rvals = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op)
-    gk, gv = gather_sparse(engine, uk, uv, root)    # disjoint owners: K8 dedupe is a no-op
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
+    gk, gv = gather_sparse(engine, uk, uv, root, key_bits)    # disjoint owners: K8 dedupe is a no-op
     return gk, (gv.view(-1) if squeeze else gv)
 
 
@@ -311,8 +319,8 @@ def _map_tensors(engine, mapData: Dict):
     """Dict[str, Tensor] -> (ids int64[n], rows [n, numel], value shape); syncs new keys."""
     d = _dictionary(engine)
     keys = list(mapData.keys())
-    ids, new = d.ids_for(keys)
-    _sync_new_keys(engine, new)
+    _sync_new_keys(engine, d.unknown(keys))
+    ids = d.ids(keys)
     vals = list(mapData.values())
     dev = vals[0].device if vals else engine.device
     if vals:
@@ -332,21 +340,21 @@ def _tensors_map(engine, k: torch.Tensor, v: torch.Tensor, shape) -> Dict:
 def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
     """``allreduceMap`` for ``Dict[str, torch.Tensor]`` values on the GPU."""
     k, v, shape = _map_tensors(engine, mapData)
-    rk, rv = allreduce_sparse(engine, k, v, operator)
+    rk, rv = allreduce_sparse(engine, k, v, operator, _dictionary(engine).bits)
     return _tensors_map(engine, rk, rv, shape)
 
 
 def reduce_map_device(engine, mapData: Dict, operator, root: int) -> Dict:
     """``reduceMap``: the op-reduced union at ``root`` (non-root: its owned share)."""
     k, v, shape = _map_tensors(engine, mapData)
-    rk, rv = reduce_sparse(engine, k, v, operator, root)
+    rk, rv = reduce_sparse(engine, k, v, operator, root, _dictionary(engine).bits)
     return _tensors_map(engine, rk, rv, shape)
 
 
 def gather_map_device(engine, mapData: Dict, root: int) -> Dict:
     """``gatherMap``: union at root, duplicate keys keep the lowest rank's value (K8)."""
     k, v, shape = _map_tensors(engine, mapData)
-    gk, gv = gather_sparse(engine, k, v, root)
+    gk, gv = gather_sparse(engine, k, v, root, _dictionary(engine).bits)
     return _tensors_map(engine, gk, gv, shape) if engine.rank == root else mapData
 
 
@@ -365,13 +373,8 @@ def _maps_by_dest(engine, maps: List[Dict]):
     """A list of p maps (map j -> rank j) as per-dest (ids, rows) + counts + value shape; ONE
     dictionary sync for all of them."""
     d = _dictionary(engine)
-    new_all: Dict[str, int] = {}
-    id_lists = []
-    for m in maps:
-        ids, new = d.ids_for(list(m.keys()))
-        id_lists.append(ids)
-        new_all.update(new)
-    _sync_new_keys(engine, new_all)
+    _sync_new_keys(engine, d.unknown(k for m in maps for k in m.keys()))
+    id_lists = [d.ids(list(m.keys())) for m in maps]
     ks, vs, counts, shape = [], [], [], None
     for m, ids in zip(maps, id_lists):
         vals = list(m.values())
@@ -411,7 +414,7 @@ def reduce_scatter_map_device(engine, mapDataList: List[Dict], operator) -> Dict
     rv = torch.empty((sum(rc), vals.shape[1]), dtype=vals.dtype, device=vals.device)
     engine.coll.all_to_all_single(rv, vals, rc, counts)
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(rv.dtype))
-    uk, uv, _ = _reduce_by_key(rk, rv, op)
+    uk, uv, _ = _reduce_by_key(rk, rv, op, _dictionary(engine).bits)
     return _tensors_map(engine, uk, uv, shape)
 
 
@@ -423,7 +426,7 @@ def scatter_map_device(engine, mapDataList: Optional[List[Dict]], root: int) -> 
         dt = next((v.dtype for v in vs if v.numel()), torch.float32)
         meta = (counts, shape or (1,), str(dt).replace("torch.", ""))
     else:
-        _sync_new_keys(engine, {})        # matches the root's one dictionary sync
+        _sync_new_keys(engine, [])        # matches the root's one dictionary sync
         meta = None
     counts, shape, dt = engine.all_gather_object(meta)[root]
     width = 1
@@ -449,7 +452,7 @@ def broadcast_map_device(engine, mapData: Dict, root: int) -> Dict:
     if engine.rank == root:
         k, v, shape = _map_tensors(engine, mapData)
     else:
-        _sync_new_keys(engine, {})
+        _sync_new_keys(engine, [])
         k = v = None
     bk, bv = broadcast_sparse(engine, k, v, root)
     shape = engine.all_gather_object(shape if engine.rank == root else None)[root]

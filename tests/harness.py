@@ -9,6 +9,9 @@ import traceback
 
 from mp4x.control.master import CommMaster
 
+# exit codes of the rank processes and the master's remote-log lines of the last run_ranks call
+LAST = {}
+
 
 def _worker(fn, rank_hint, port, args, q, kind, threads):
     try:
@@ -79,6 +82,8 @@ def run_ranks(p, fn, args=(), timeout=120, kind="process", threads=1, master_kwa
                 pr.kill()
                 pr.join(timeout=5)
         code = master.stop(timeout=5)
+        LAST["exitcodes"] = [pr.exitcode for pr in procs]
+        LAST["logs"] = list(master.logs)
     if errors and not expect_fail:
         raise AssertionError("rank failed:\n" + "\n".join(errors))
     if not expect_fail and len(results) != p:

@@ -114,6 +114,11 @@ def codec_cases(eng, r, p):
     assert eng.stats.get("allreduce.fp8", 0) == 1
     err = (y - ref).abs().max().item()
     assert err < 0.25 * p, err                   # e4m3: ~2^-4 relative per block, twice quantised
+    # unaligned [from, to) view: the staged (padded) form; the aligned call above quantised in place
+    w = x.clone()
+    eng.allreduce(w, 1, n - 2, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="fp8"))
+    assert (w[1:n - 2] - ref[1:n - 2]).abs().max().item() < 0.25 * p
+    assert w[0] == x[0] and torch.equal(w[n - 2:], x[n - 2:])
     z = x.clone()
     eng.allreduce(z, 0, n, Operators.Float.SUM, Operands.FLOAT_OPERAND(codec="bf16"))
     assert (z - ref).abs().max().item() < 0.05 * p

@@ -199,6 +199,18 @@ def test_reduce_by_key_matches_torch(dim):
     torch.testing.assert_close(uv2, ref_m)
 
 
+@pytest.mark.parametrize("bits", [12, 21])
+def test_reduce_by_key_key_bits_matches_full_sort(bits):
+    """Dense ids: sorting only the low ``bits`` bits gives the identical result."""
+    K = _native()
+    n = 50_000
+    keys = torch.randint(0, 1 << bits, (n,), device=DEV, dtype=torch.int64)
+    vals = torch.randn(n, 16, device=DEV)
+    uk, uv, cnt = K.reduce_by_key(keys, vals, int(OpCode.SUM))
+    uk2, uv2, cnt2 = K.reduce_by_key(keys, vals, int(OpCode.SUM), key_bits=bits)
+    assert torch.equal(uk, uk2) and torch.equal(uv, uv2) and torch.equal(cnt, cnt2)
+
+
 def test_key_owner_hist():
     K = _native()
     keys = torch.randint(0, 1 << 62, (50_000,), device=DEV, dtype=torch.int64)

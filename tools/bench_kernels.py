@@ -93,6 +93,10 @@ def main():
     vals = torch.randn(1_600_000, 64, device=dev)
     ms = timeit(lambda: K.reduce_by_key(keys, vals, int(OpCode.SUM)), max(3, a.iters // 4))
     res["k5_reduce_by_key_1.6Mx64"] = {"ms": ms, "GBps": (vals.numel() * 4 * 2 + keys.numel() * 8 * 4) / ms / 1e6}
+    # the same keys as dense dictionary ids (< 2**19): the radix sort covers 19 bits (3 passes, not 8)
+    ms = timeit(lambda: K.reduce_by_key(keys, vals, int(OpCode.SUM), key_bits=19), max(3, a.iters // 4))
+    res["k5_reduce_by_key_1.6Mx64_bits19"] = {"ms": ms,
+                                              "GBps": (vals.numel() * 4 * 2 + keys.numel() * 8 * 4) / ms / 1e6}
     idx = torch.randperm(1_600_000, device=dev)
     ms = timeit(lambda: K.gather_rows(vals, idx), a.iters)
     res["k3_gather_rows_1.6Mx64"] = {"ms": ms, "GBps": vals.numel() * 4 * 2 / ms / 1e6}
