@@ -349,8 +349,15 @@ class DeviceEngine:
         self._sync()
         self.barrier()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=side):
-            fn()
+        wd = self.watchdog
+        if wd is not None:
+            wd.quiet += 1        # no device polls from the watchdog thread during the capture
+        try:
+            with torch.cuda.graph(g, stream=side):
+                fn()
+        finally:
+            if wd is not None:
+                wd.quiet -= 1
         self._sync()
         return g
 

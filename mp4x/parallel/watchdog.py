@@ -66,6 +66,7 @@ class CollectiveWatchdog:
         self.on_failure = on_failure
         self.failure: Optional[str] = None
         self.paused = 0                      # > 0: skip the IPC error-word check (autotune probes)
+        self.quiet = 0                       # > 0: no device API calls at all (hipGraph capture)
         self._lock = threading.Lock()
         self._inflight: Dict[int, Tuple[str, float]] = {}
         self._next = 0
@@ -130,6 +131,10 @@ class CollectiveWatchdog:
         for name, t0 in inflight:
             if now - t0 > self.timeout:
                 return f"{name} blocked on the host for {now - t0:.1f} s (timeout {self.timeout:g} s)"
+        if self.quiet:
+            # a global-mode graph capture is running: a query or synchronise from this thread
+            # would invalidate it, so only the host-side check runs
+            return None
         for dq in streams:
             while dq:
                 name, t0, ev = dq[0]
