@@ -13,91 +13,9 @@
 //                   re-quantised in the same pass for the all-gather leg.
 #include <hipcub/hipcub.hpp>
 
-#include "common.hpp"
+#include "fp8.hpp"
 
 namespace mp4x {
-
-constexpr int kQBlock = 256;        // elements per scale
-constexpr float kFp8Max = 448.0f;   // e4m3fn max finite
-
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  return v;
-}
-
-template <int DT>
-__device__ __forceinline__ void load4(const void* p, int64_t e, int64_t n, float (&x)[4]) {
-  using E = Elem<DT>;
-  using S = typename E::S;
-  const S* s = reinterpret_cast<const S*>(p);
-  if (e + 3 < n) {
-    if constexpr (sizeof(S) == 4) {
-      u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + e));   // streamed once
-      S t[4];
-      __builtin_memcpy(t, &v, 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = (float)E::load(t[j]);
-    } else if constexpr (sizeof(S) == 2) {
-      uint2 v = *reinterpret_cast<const uint2*>(s + e);
-      S t[4];
-      __builtin_memcpy(t, &v, 8);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = (float)E::load(t[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) x[j] = (float)E::load(s[e + j]);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) x[j] = (e + j < n) ? (float)E::load(s[e + j]) : 0.0f;
-  }
-}
-
-template <int DT>
-__device__ __forceinline__ void store4(void* p, int64_t e, int64_t n, const float (&x)[4]) {
-  using E = Elem<DT>;
-  using S = typename E::S;
-  S* s = reinterpret_cast<S*>(p);
-  if (e + 3 < n) {
-    S t[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) t[j] = E::store((typename E::A)x[j]);
-    if constexpr (sizeof(S) == 4) {
-      u32x4 v;
-      __builtin_memcpy(&v, t, 16);
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(s + e));
-    } else if constexpr (sizeof(S) == 2) {
-      uint2 v;
-      __builtin_memcpy(&v, t, 8);
-      *reinterpret_cast<uint2*>(s + e) = v;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) s[e + j] = t[j];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (e + j < n) s[e + j] = E::store((typename E::A)x[j]);
-  }
-}
-
-__device__ __forceinline__ uint32_t pack_fp8(const float (&x)[4], float inv) {
-  float a[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) a[j] = fminf(fmaxf(x[j] * inv, -kFp8Max), kFp8Max);
-  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a[0], a[1], 0, false);
-  w = __builtin_amdgcn_cvt_pk_fp8_f32(a[2], a[3], w, true);
-  return (uint32_t)w;
-}
-
-__device__ __forceinline__ void quant_block(const float (&x)[4], uint32_t* q, float* scales, int64_t blk, int lane) {
-  float m = fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3])));
-  m = wave_max(m);
-  const float scale = m > 0.0f ? m / kFp8Max : 1.0f;
-  __builtin_nontemporal_store(pack_fp8(x, 1.0f / scale), q + blk * 64 + lane);
-  if (lane == 0) scales[blk] = scale;
-}
 
 // One wave per quant block; QU consecutive blocks per wave iteration so each lane keeps QU
 // 16-byte loads in flight before the first amax reduction.
@@ -143,12 +61,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_reduce(void* __restrict__ ou
       s[k] = in.s[k][b];
     }
 #pragma unroll
-    for (int k = 0; k < NIN; ++k) {
-      acc[0] += __builtin_amdgcn_cvt_f32_fp8((int)w[k], 0) * s[k];
-      acc[1] += __builtin_amdgcn_cvt_f32_fp8((int)w[k], 1) * s[k];
-      acc[2] += __builtin_amdgcn_cvt_f32_fp8((int)w[k], 2) * s[k];
-      acc[3] += __builtin_amdgcn_cvt_f32_fp8((int)w[k], 3) * s[k];
-    }
+    for (int k = 0; k < NIN; ++k) fp8_fma_acc(w[k], s[k], acc);
     if (out) store4<DT>(out, e, n, acc);
     if (q_out) quant_block(acc, q_out, s_out, b, lane);
   }

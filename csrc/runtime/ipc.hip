@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../kernels/common.hpp"
+#include "../kernels/fp8.hpp"
 
 namespace mp4x {
 
@@ -221,6 +222,101 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_gather(IpcPtrs P, Signal* s
       if (k != rank && S.lo[k] + v < S.hi[k]) out[S.lo[k] + v] = x[k];
   }
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+// ---------------------------------------------------------------- fused fp8 two-shot (K6 on xGMI)
+// Compressed allreduce with the block-scaled e4m3 codec on the links, in ONE kernel per piece
+// (the quantise of this rank's input into its own IPC buffer runs just before, stream-ordered):
+//   RS: for every 256-element quant block of chunk `rank`, each wave pulls the block's 256 fp8
+//       bytes + scale from ALL p buffers at once (every xGMI link busy), dequantises and sums in
+//       f32 registers, re-quantises (wave amax -> scale) into its OWN buffer, and writes the
+//       dequantised result of that re-quantised block to `out` (so this rank's chunk holds
+//       exactly what the peers will decode);
+//   AG: every wave pulls the same block offset of every peer's chunk at once, dequantises
+//       straight into `out`.
+// Versus the RCCL form (all-to-all + fused dequant-reduce-requant + all-gather + dequant) no
+// landing buffers are written and read back, and p-1 scale messages disappear.  Layout of the
+// buffers: q bytes [0, M) then f32 scales at `soff` bytes, one per quant block; block j of chunk
+// k is global quant block k * cb + j.  Block b of every rank visits the same chunk-relative j
+// values in both phases, so the per-block barriers are the two-shot's.
+template <int DT, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Signal* self, int rank, int64_t cb,
+                                                                  int64_t soff, void* __restrict__ out, int64_t n,
+                                                                  uint32_t epoch, const uint32_t* epoch_dev) {
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int lane = threadIdx.x & 63;
+  constexpr int kWaves = kIpcThreads / 64;
+  const int64_t w0 = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  {
+    uint32_t* myq = reinterpret_cast<uint32_t*>(const_cast<void*>(P.data[rank]));
+    float* mys = reinterpret_cast<float*>(reinterpret_cast<char*>(myq) + soff);
+    for (int64_t j = w0; j < cb; j += nw) {
+      const int64_t b = (int64_t)rank * cb + j;          // global quant block
+      uint32_t w[NR];
+      float sc[NR];
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {                      // every peer's block in flight at once
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(P.data[k]);
+        w[k] = q[b * 64 + lane];
+        sc[k] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b];
+      }
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NR; ++k) fp8_fma_acc(w[k], sc[k], acc);   // rank order: deterministic
+      float m = fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3])));
+      m = wave_max(m);
+      const float scale = m > 0.0f ? m / kFp8Max : 1.0f;
+      const uint32_t qq = pack_fp8(acc, 1.0f / scale);
+      myq[b * 64 + lane] = qq;                            // read by the peers after the mid barrier
+      if (lane == 0) mys[b] = scale;
+      float y[4];
+      unpack_fp8(qq, scale, y);
+      store4<DT>(out, b * kQBlock + lane * 4, n, y);
+    }
+  }
+  if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
+  for (int64_t j = w0; j < cb; j += nw) {
+    uint32_t w[NR];
+    float sc[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      if (k == rank) continue;
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(P.data[k]);
+      const int64_t b = (int64_t)k * cb + j;
+      w[k] = q[b * 64 + lane];
+      sc[k] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      if (k == rank) continue;
+      const int64_t b = (int64_t)k * cb + j;
+      if (b * kQBlock >= n) continue;
+      float y[4];
+      unpack_fp8(w[k], sc[k], y);
+      store4<DT>(out, b * kQBlock + lane * 4, n, y);
+    }
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+template <int DT>
+static int fp8_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t cb, int64_t soff, void* out, int64_t n,
+                  uint32_t epoch, const uint32_t* edev, int blocks, hipStream_t st) {
+#define MP4X_FP8_CASE(N)                                                                                     \
+  case N:                                                                                                    \
+    hipLaunchKernelGGL((k_ipc_fp8_twoshot<DT, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, cb, \
+                       soff, out, n, epoch, edev);                                                           \
+    return (int)hipGetLastError();
+  switch (p) {
+    MP4X_FP8_CASE(2) MP4X_FP8_CASE(3) MP4X_FP8_CASE(4) MP4X_FP8_CASE(5) MP4X_FP8_CASE(6) MP4X_FP8_CASE(7)
+    MP4X_FP8_CASE(8)
+    default: return MP4X_E_BADARG;
+  }
+#undef MP4X_FP8_CASE
 }
 
 // set per call by mp4x_ipc_allreduce (host-side, single-threaded use per communicator)
@@ -481,4 +577,35 @@ extern "C" int mp4x_ipc_allgather(void* const* data_ptrs, void* const* signal_pt
     default: return MP4X_E_BADARG;
   }
 #undef MP4X_AG_CASE
+}
+
+// Fused fp8 two-shot allreduce of one piece.  Every rank has already quantised its input into
+// its own buffer (q bytes at 0, f32 scales at `soff`, p * cb quant blocks, blocks past the input
+// zeroed); `out` (dtype = f32 / bf16 / f16, 16-B aligned) receives n elements.
+extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
+                                      int64_t cb, int64_t soff, void* out, int64_t n, uint32_t epoch, int blocks,
+                                      const uint32_t* epoch_dev, void* stream) {
+  IpcPtrs P;
+  if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
+  if (cb <= 0 || n <= 0 || n > (int64_t)p * cb * kQBlock || (soff & 15) || ((uintptr_t)out & 15))
+    return MP4X_E_BADARG;
+  if (soff < (int64_t)p * cb * kQBlock) return MP4X_E_BADARG;     // scales after the q bytes
+  if (blocks <= 0) {
+    const int64_t waves = cb;                                       // one wave per quant block
+    int64_t b = (waves + kIpcThreads / 64 - 1) / (kIpcThreads / 64);
+    blocks = (int)(b < 1 ? 1 : (b > kIpcMaxBlocks ? kIpcMaxBlocks : b));
+  }
+  if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case MP4X_F32: return fp8_nr<MP4X_F32>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
+    case MP4X_BF16: return fp8_nr<MP4X_BF16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
+    case MP4X_F16: return fp8_nr<MP4X_F16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+extern "C" int mp4x_memset_async(void* dst, int value, size_t bytes, void* stream) {
+  return (int)hipMemsetAsync(dst, value, bytes, (hipStream_t)stream);
 }

@@ -400,7 +400,12 @@ class DeviceEngine:
         elif algo == "zs":
             self._allreduce_zs(view, op)
         elif algo == "fp8":
-            self._allreduce_fp8(view)
+            inst = self._ipc_fp8(view)
+            if inst is not None:
+                self._count("allreduce.fp8.ipc")
+                inst.allreduce_fp8(view)          # fused quant-on-the-links two-shot over xGMI
+            else:
+                self._allreduce_fp8(view)
         elif algo == "bf16":
             # 2x-compressed wire: bf16 all-to-all, f32 accumulation inside the K1 kernel
             # (bf16 inputs, one rounding), bf16 all-gather, widened back in place
@@ -409,6 +414,20 @@ class DeviceEngine:
             view.copy_(w)
         else:
             self._allreduce_a2a(view, op)
+
+    def _ipc_fp8(self, view: torch.Tensor):
+        """The IPC instance that runs the fused fp8 two-shot for ``view``, or None (RCCL form).
+        ``MP4X_FP8_TRANSPORT``: auto (IPC when available) | ipc | rccl."""
+        mode = os.environ.get("MP4X_FP8_TRANSPORT", "auto").lower()
+        if mode == "rccl" or not self.ipc_enabled or view.device.type != "cuda":
+            return None
+        if self.ipc() is None or not self._ipc_obj.fp8_ok(view):
+            return None
+        if torch.cuda.is_current_stream_capturing() and self._ipc_obj._epoch_dev is None:
+            return None
+        if view.numel() * 260 // 256 <= self._ipc_obj.nbytes:
+            return self._ipc_obj
+        return self.ipc_large()
 
     # ------------------------------------------------------------------ autotuning
     def _algo_valid(self, algo: str, op, dtype, nbytes: int) -> bool:

@@ -34,6 +34,9 @@ native.register_signatures({
     "mp4x_ipc_close_handle": (c_int, [c_void_p]),
     "mp4x_ipc_read_error": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "mp4x_ipc_error_word": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32), c_int, c_void_p]),
+    "mp4x_ipc_fp8_allreduce": (c_int, [c_int, PP, PP, c_int, c_int, c_int64, c_int64, c_void_p, c_int64,
+                                       ctypes.c_uint32, c_int, c_void_p, c_void_p]),
+    "mp4x_memset_async": (c_int, [c_void_p, c_int, c_size_t, c_void_p]),
     "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
                                    c_int, c_void_p, c_void_p]),
@@ -283,6 +286,64 @@ class IpcAllreduce:
         if n:
             check(self.lib.mp4x_memcpy_async(flat[base:].data_ptr(), self._data.value, n, st), "ipc AG out")
         return True
+
+    # ---------------------------------------------------------------- fused fp8 two-shot
+    QBLOCK = 256
+    FP8_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+
+    def fp8_ok(self, view: torch.Tensor) -> bool:
+        return view.dtype in self.FP8_DTYPES and view.is_contiguous() and view.data_ptr() % 16 == 0 \
+            and view.numel() % 4 == 0 and view.numel() > 0
+
+    def _fp8_piece_blocks(self) -> int:
+        """Quant blocks per rank chunk per piece: p * cb blocks of 256 fp8 bytes + 4-byte scales
+        must fit the buffer (scales 16-byte aligned after the q bytes)."""
+        per_block = self.QBLOCK + 4
+        cb = (self.nbytes - 16) // (self.p * per_block)
+        if cb < 1:
+            raise Mp4jException("IPC buffer too small for the fp8 two-shot")
+        return int(cb)
+
+    def allreduce_fp8(self, view: torch.Tensor) -> torch.Tensor:
+        """In-place SUM allreduce with the block-scaled e4m3 codec on the xGMI links, one fused
+        kernel per piece (csrc/runtime/ipc.hip ``k_ipc_fp8_twoshot``): quantise this rank's
+        piece into its own buffer (K6), then pull + dequantise + f32-sum + requantise the own
+        chunk from every peer at once, then pull + dequantise every peer's chunk.  Same numerics
+        as the RCCL fp8 schedule (two quantisations, f32 accumulation in rank order).  Needs
+        :meth:`fp8_ok`."""
+        if not self.fp8_ok(view):
+            raise Mp4jException("fp8 IPC allreduce needs a contiguous 16-byte aligned f32/bf16/f16 tensor, n % 4 == 0")
+        Q = self.QBLOCK
+        n = view.numel()
+        es = view.element_size()
+        dt = int(dtype_of_torch(view.dtype))
+        cbmax = self._fp8_piece_blocks()
+        st = stream_ptr()
+        base = view.data_ptr()
+        off = 0
+        while off < n:
+            m = min(n - off, self.p * cbmax * Q)
+            cb = -(-m // (self.p * Q))                   # quant blocks per rank chunk
+            nq = self.p * cb * Q                         # q bytes of this piece
+            soff = (nq + 15) // 16 * 16
+            own = self._data.value
+            used = -(-m // Q)                            # blocks the quantiser writes
+            if used < self.p * cb:                       # zero the blocks past the input
+                check(self.lib.mp4x_memset_async(own + used * Q, 0, (self.p * cb - used) * Q, st), "fp8 q tail")
+                check(self.lib.mp4x_memset_async(own + soff + used * 4, 0, (self.p * cb - used) * 4, st),
+                      "fp8 scale tail")
+            check(self.lib.mp4x_quant_fp8(dt, base + off * es, m, own, own + soff, st), "fp8 quant")
+            edev = self._next_epoch(st)
+            check(self.lib.mp4x_ipc_fp8_allreduce(dt, self._pp_data[0], self._pp_sig[0], self.rank, self.p, cb, soff,
+                                                  base + off * es, m, self.epoch, self._blocks_for_waves(cb), edev,
+                                                  st), "mp4x_ipc_fp8_allreduce")
+            off += m
+        return view
+
+    def _blocks_for_waves(self, waves: int) -> int:
+        if not self.max_blocks:
+            return 0
+        return max(1, min(self.max_blocks, -(-waves // 8)))
 
     def prepare_graph(self):
         """Move the epoch counter to device memory so hipGraph replays get fresh epochs.
