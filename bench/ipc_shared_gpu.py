@@ -28,15 +28,20 @@ def worker(port, q, sizes, iters, buf_bytes=64 << 20, algos=(0, 1)):
     for nbytes in sizes:
         x = torch.randn(nbytes // 4, device="cuda")
         for algo in algos:
+            def call():
+                if algo == 2:
+                    ipc.allreduce_fp8(x)      # fused fp8 two-shot (K6 codec on the links)
+                else:
+                    ipc.allreduce(x, Operators.Float.SUM, algo=algo)
             for _ in range(5):
-                ipc.allreduce(x, Operators.Float.SUM, algo=algo)
+                call()
             torch.cuda.synchronize()
             comm.barrier()
             s = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
             e = [torch.cuda.Event(enable_timing=True) for _ in range(iters)]
             for i in range(iters):
                 s[i].record()
-                ipc.allreduce(x, Operators.Float.SUM, algo=algo)
+                call()
                 e[i].record()
             torch.cuda.synchronize()
             ts = sorted(a.elapsed_time(b) for a, b in zip(s, e))
@@ -45,7 +50,7 @@ def worker(port, q, sizes, iters, buf_bytes=64 << 20, algos=(0, 1)):
             gs.wait_stream(torch.cuda.current_stream())
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=gs):
-                ipc.allreduce(x, Operators.Float.SUM, algo=algo)
+                call()
             torch.cuda.synchronize()
             comm.barrier()
             for i in range(iters):
@@ -54,7 +59,7 @@ def worker(port, q, sizes, iters, buf_bytes=64 << 20, algos=(0, 1)):
                 e[i].record()
             torch.cuda.synchronize()
             tg = sorted(a.elapsed_time(b) for a, b in zip(s, e))
-            out.append({"bytes": nbytes, "algo": ["oneshot", "twoshot"][algo], "p50_us": ts[len(ts) // 2] * 1e3,
+            out.append({"bytes": nbytes, "algo": ["oneshot", "twoshot", "fp8_twoshot"][algo], "p50_us": ts[len(ts) // 2] * 1e3,
                         "p99_us": ts[min(len(ts) - 1, int(0.99 * len(ts)))] * 1e3,
                         "graph_p50_us": tg[len(tg) // 2] * 1e3, "err": ipc.error_word()})
             comm.barrier()
@@ -69,7 +74,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--sizes", default="4096,65536,262144,1048576,8388608,33554432", help="message bytes, comma list")
     ap.add_argument("--buf-mib", type=int, default=64, help="IPC buffer size (larger messages go in pieces)")
-    ap.add_argument("--algos", default="0,1", help="0 = one-shot, 1 = two-shot")
+    ap.add_argument("--algos", default="0,1", help="0 = one-shot, 1 = two-shot, 2 = fused fp8 two-shot")
     a = ap.parse_args()
     from mp4x import CommMaster
     m = CommMaster(a.procs, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()

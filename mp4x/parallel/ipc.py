@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import socket
 from typing import List, Optional
 
 import torch
@@ -64,6 +65,11 @@ class IpcAllreduce:
         if not (2 <= self.p <= 8):
             raise Mp4jException("IPC allreduce supports 2..8 ranks")
         self.lib = native.hip()
+        # IPC handles only open on the same node: a job spanning hosts keeps RCCL (decided from
+        # the exchanged host names, identically on every rank, before anything is allocated)
+        hosts = comm.server.call("allgather_obj", self.rank, socket.gethostname())
+        if len(set(hosts)) != 1:
+            raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
         self.device = torch.cuda.current_device()
