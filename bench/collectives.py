@@ -127,10 +127,16 @@ def main():
         def step():
             comm.reduceScatterArray(x, B, Operators.BFloat16.SUM, 0, counts)
             comm.allgatherArray(x, B, froms, tos)
+        tuned = None
+        if p > 1:   # untimed: RCCL vs piecewise IPC vs a2a / p2p, pinned per size class (MAX over ranks)
+            tuned = {"reduce_scatter": eng.autotune_reduce_scatter(x, Operators.BFloat16.SUM, iters=2),
+                     "allgather": eng.autotune_allgather(x, iters=2)}
+            tuned = {k: {c: round(t * 1e3, 3) for c, t in v.items()} for k, v in tuned.items()}
         p50, p99 = timed(step, a.iters, a.warmup, sync)
         nb = n * 2
         emit({"config": "reduceScatter + allgather of 4 GB bf16 (ZeRO)", "p": p, "p50_ms": p50, "p99_ms": p99,
-              "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None})
+              "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None,
+              "autotune_ms": tuned})
     if a.config == "sparse_map":  # BASELINE config 4: sparse Map<String, float[]> allreduce
         dim, nkeys = 64, 200_000
         shared = nkeys // 2

@@ -489,6 +489,71 @@ class DeviceEngine:
             self._tuned[_tune_key(view.dtype, op, nbytes)] = best
         return res
 
+    def autotune_reduce_scatter(self, like: torch.Tensor, operator, iters: int = 3) -> Dict[str, float]:
+        """Reduce-scatter twin of :meth:`autotune_allreduce` (equal split of ``like``): times RCCL
+        ``reduce_scatter_tensor``, the piecewise IPC kernels and the a2a schedule, MAX over ranks,
+        and pins the fastest for this (dtype, op, size class).  Collective."""
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        op = self._op(operator, view)
+        froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
+        cands = ["rccl", "a2a"] + (["ipc"] if self.ipc_enabled and self._ipc_ok(op, view.dtype, 16) else [])
+        return self._autotune_kind("reduce_scatter", view, op, cands,
+                                   lambda: self.reduce_scatter(view, froms, tos, op), iters)
+
+    def autotune_allgather(self, like: torch.Tensor, iters: int = 3) -> Dict[str, float]:
+        """All-gather twin of :meth:`autotune_allreduce` (equal split): RCCL
+        ``all_gather_into_tensor`` vs the piecewise IPC kernels vs grouped p2p.  Collective."""
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
+        cands = ["rccl", "p2p"] + (["ipc"] if self.ipc_enabled else [])
+        return self._autotune_kind("allgather", view, None, cands, lambda: self.allgather(view, froms, tos), iters)
+
+    def _autotune_kind(self, kind: str, view: torch.Tensor, op, cands, run, iters: int) -> Dict[str, float]:
+        key = self._rsag_key(kind, view, op)
+        times = []
+        if self.watchdog is not None:
+            self.watchdog.paused += 1
+        try:
+            for c in cands:
+                if c == "rccl":
+                    self._tuned.pop(key, None)
+                else:
+                    self._tuned[key] = c
+                times.append(self._time_fn(run, uses_ipc=c == "ipc", iters=iters, name=f"{kind}:{c}"))
+        finally:
+            self._tuned.pop(key, None)
+            if self.watchdog is not None:
+                self.watchdog.paused -= 1
+        tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
+        self.coll.all_reduce(tt, OpCode.MAX)
+        res = dict(zip(cands, tt.cpu().tolist()))
+        best = min(res, key=res.get) if res else None
+        if best is not None and best != "rccl" and res[best] != float("inf"):
+            self._tuned[key] = best
+        return res
+
+    def _time_fn(self, run, uses_ipc: bool, iters: int, name: str) -> float:
+        """Seconds per call of ``run`` (inf when it failed on this rank).  Collective."""
+        ok = True
+        dt = float("inf")
+        try:
+            run()                                # warm-up (lazy IPC / RCCL setup)
+            self._sync()
+            if uses_ipc and self._ipc_error():
+                raise Mp4jException("IPC barrier timeout during warm-up")
+            self.barrier()
+            t0 = time.perf_counter()
+            for _ in range(max(1, iters)):
+                run()
+            self._sync()
+            dt = (time.perf_counter() - t0) / max(1, iters)
+            if uses_ipc and self._ipc_error():
+                ok = False
+        except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
+            LOG.warning("autotune: %s failed: %s", name, e)
+            ok = False
+        return dt if ok else float("inf")
+
     def _time_candidate(self, c: str, view: torch.Tensor, op, iters: int) -> float:
         """Seconds per call of schedule ``c`` (inf when it failed on this rank).  Collective."""
         ok = True
@@ -761,6 +826,15 @@ class DeviceEngine:
             if self._ipc_obj.reduce_scatter(flat, froms, tos, op):
                 self._count("reduce_scatter.ipc")
                 return arr
+        if algo in ("rccl", "a2a"):
+            big = self._large_choice("reduce_scatter", whole, op)
+            if big == "ipc":
+                inst = self.ipc_large()
+                if inst is not None and inst.reduce_scatter_large(flat, froms, tos, op):
+                    self._count("reduce_scatter.ipc_large")
+                    return arr
+            elif big == "a2a":
+                algo = "a2a"
         self._count("reduce_scatter." + algo)
         equal = len(set(counts)) == 1
         if algo == "rccl" and equal and self.coll.reduce_scatter_ok:
@@ -786,9 +860,34 @@ class DeviceEngine:
         if whole.numel() and self._ipc_direct_ok(None, whole) and self._ipc_obj.allgather(flat, froms, tos):
             self._count("allgather.ipc")
             return arr
+        big = self._large_choice("allgather", whole, None) if whole.numel() else None
+        if big == "ipc":
+            inst = self.ipc_large()
+            if inst is not None and inst.allgather_large(flat, froms, tos):
+                self._count("allgather.ipc_large")
+                return arr
+        elif big == "p2p":
+            self._count("allgather.p2p")
+            self._allgather_p2p(flat, froms, tos)
+            return arr
         self._count("allgather")
         self._allgather_any(flat, froms, tos)
         return arr
+
+    def _large_choice(self, kind: str, whole: torch.Tensor, op) -> Optional[str]:
+        """Schedule for a reduce-scatter / all-gather above the direct-IPC tier: forced by
+        ``MP4X_DEVICE_ALGO=ipc2`` (IPC pieces), or pinned by :meth:`autotune_reduce_scatter` /
+        :meth:`autotune_allgather` for this (dtype, op, size class); None = RCCL."""
+        if self.algo in ("ipc2", "ipc"):
+            return "ipc" if self.ipc_enabled and (op is None or self._ipc_ok(op, whole.dtype, 16)) else None
+        if self.algo not in ("", "auto") or not self._tuned:
+            return None
+        return self._tuned.get(self._rsag_key(kind, whole, op))
+
+    @staticmethod
+    def _rsag_key(kind: str, whole: torch.Tensor, op) -> tuple:
+        return (kind, whole.dtype, int(op.code) if op is not None else -1,
+                max(0, whole.numel() * whole.element_size() - 1).bit_length())
 
     def _ipc_direct_ok(self, op, whole: torch.Tensor) -> bool:
         """Direct IPC reduce-scatter / all-gather tier: up to the two-shot size, unless a schedule
@@ -938,7 +1037,7 @@ def _watched(name, fn):
     return wrapper
 
 
-_WATCHED = ["allreduce", "autotune_allreduce", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",
+_WATCHED = ["allreduce", "autotune_allreduce", "autotune_reduce_scatter", "autotune_allgather", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",
             "scatter", "allreduce_map", "all_to_all_v", "reduce_map", "gather_map", "allgather_map",
             "reduce_scatter_map", "scatter_map", "broadcast_map", "barrier"]
 for _n in _WATCHED:

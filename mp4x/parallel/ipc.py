@@ -247,6 +247,13 @@ class IpcAllreduce:
             return 0
         return max(1, min(self.max_blocks, -(-nvec // 512)))
 
+    def _grid(self, nvec: int) -> int:
+        """Explicit grid for a per-block-barrier kernel.  ``nvec`` must be RANK-INDEPENDENT (the
+        largest segment of any rank): block b of every rank has to exist to meet block b of the
+        peers, so ragged segments may not size the grid per rank."""
+        cap = self.max_blocks or 256                   # kIpcMaxBlocks
+        return max(1, min(cap, -(-nvec // 512)))
+
     def reduce_scatter(self, view: torch.Tensor, froms, tos, op) -> bool:
         """In place: ``view[froms[r]:tos[r]]`` <- op over all ranks of that range (ragged ranges
         whose byte offsets are 16-byte multiples).  Returns False (nothing done) otherwise."""
@@ -262,9 +269,10 @@ class IpcAllreduce:
         edev = self._next_epoch(st)
         lo, hi = (froms[r] - base) * es // 16, (tos[r] - base) * es // 16
         mine = self._data.value + lo * 16          # reduced in place inside the own buffer
+        maxv = max((t - f) * es // 16 for f, t in zip(froms, tos))
         check(self.lib.mp4x_ipc_reduce_scatter(int(dtype_of_torch(view.dtype)), int(op.code), self._pp_data[0],
                                                self._pp_sig[0], r, self.p, lo, hi, mine, self.epoch,
-                                               self._blocks_for(hi - lo), edev, st), "mp4x_ipc_reduce_scatter")
+                                               self._grid(maxv), edev, st), "mp4x_ipc_reduce_scatter")
         if hi > lo:
             check(self.lib.mp4x_memcpy_async(flat[froms[r]:].data_ptr(), mine, (hi - lo) * 16, st), "ipc RS out")
         return True
@@ -287,10 +295,85 @@ class IpcAllreduce:
         maxlen = max(h - l_ for l_, h in zip(lo, hi))
         # peers' segments land in the OWN buffer (only the own segment is read remotely), then one copy out
         check(self.lib.mp4x_ipc_allgather(self._pp_data[0], self._pp_sig[0], r, self.p, lo, hi, self._data.value,
-                                          self.epoch, self._blocks_for(maxlen), edev, st), "mp4x_ipc_allgather")
+                                          self.epoch, self._grid(maxlen), edev, st), "mp4x_ipc_allgather")
         n = (tos[-1] - base) * es
         if n:
             check(self.lib.mp4x_memcpy_async(flat[base:].data_ptr(), self._data.value, n, st), "ipc AG out")
+        return True
+
+    # ---------------------------------------------------------------- piecewise large RS / AG
+    # Messages beyond the staging buffer (e.g. the ZeRO reduce-scatter + all-gather of a 4 GB
+    # bf16 tensor, BASELINE config 3): piece i covers slab i of EVERY rank's segment, staged at
+    # offset j * slab in the buffer, so the direct kernels above run unchanged per piece (all
+    # links busy, fused peer-load + reduce for RS).  Segments must be whole 16-byte vectors.
+    def _slab(self, es: int) -> int:
+        """Elements of each rank's segment per piece (a 16-byte multiple)."""
+        return (self.nbytes // self.p) // 16 * 16 // es
+
+    def large_ok(self, view: torch.Tensor, froms, tos) -> bool:
+        es = view.element_size()
+        if self._slab(es) <= 0 or not view.is_contiguous():
+            return False
+        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+            return False
+        return all(((t - f) * es) % 16 == 0 for f, t in zip(froms, tos))
+
+    def reduce_scatter_large(self, view: torch.Tensor, froms, tos, op) -> bool:
+        """In place ``view[froms[r]:tos[r]]`` <- op over all ranks, any message size, in pieces."""
+        if not self.supports(view, op) or not self.large_ok(view, froms, tos):
+            return False
+        es = view.element_size()
+        flat = view.view(-1)
+        p, r = self.p, self.rank
+        counts = [t - f for f, t in zip(froms, tos)]
+        s = self._slab(es)
+        sv = s * es // 16
+        buf = self._data.value
+        dt = int(dtype_of_torch(view.dtype))
+        st = stream_ptr()
+        for i in range(-(-max(counts) // s)):
+            lens = [max(0, min(c - i * s, s)) for c in counts]
+            for j in range(p):
+                if lens[j]:
+                    check(self.lib.mp4x_memcpy_async(buf + j * s * es, flat[froms[j] + i * s:].data_ptr(), lens[j] * es,
+                                                     st), "ipc RS-large staging")
+            edev = self._next_epoch(st)
+            lo = r * sv
+            hi = lo + lens[r] * es // 16
+            check(self.lib.mp4x_ipc_reduce_scatter(dt, int(op.code), self._pp_data[0], self._pp_sig[0], r, p, lo, hi,
+                                                   buf + lo * 16, self.epoch, self._grid(max(lens) * es // 16), edev,
+                                                   st), "mp4x_ipc_reduce_scatter")
+            if lens[r]:
+                check(self.lib.mp4x_memcpy_async(flat[froms[r] + i * s:].data_ptr(), buf + lo * 16, lens[r] * es, st),
+                      "ipc RS-large out")
+        return True
+
+    def allgather_large(self, view: torch.Tensor, froms, tos) -> bool:
+        """In place: every rank's ``view[froms[j]:tos[j]]`` lands everywhere, any size, in pieces."""
+        if not self.large_ok(view, froms, tos):
+            return False
+        es = view.element_size()
+        flat = view.view(-1)
+        p, r = self.p, self.rank
+        counts = [t - f for f, t in zip(froms, tos)]
+        s = self._slab(es)
+        sv = s * es // 16
+        buf = self._data.value
+        st = stream_ptr()
+        for i in range(-(-max(counts) // s)):
+            lens = [max(0, min(c - i * s, s)) for c in counts]
+            if lens[r]:
+                check(self.lib.mp4x_memcpy_async(buf + r * s * es, flat[froms[r] + i * s:].data_ptr(), lens[r] * es,
+                                                 st), "ipc AG-large staging")
+            edev = self._next_epoch(st)
+            lo = (c_int64 * p)(*[j * sv for j in range(p)])
+            hi = (c_int64 * p)(*[j * sv + lens[j] * es // 16 for j in range(p)])
+            check(self.lib.mp4x_ipc_allgather(self._pp_data[0], self._pp_sig[0], r, p, lo, hi, buf, self.epoch,
+                                              self._grid(max(lens) * es // 16), edev, st), "mp4x_ipc_allgather")
+            for j in range(p):
+                if j != r and lens[j]:
+                    check(self.lib.mp4x_memcpy_async(flat[froms[j] + i * s:].data_ptr(), buf + j * s * es,
+                                                     lens[j] * es, st), "ipc AG-large out")
         return True
 
     # ---------------------------------------------------------------- fused fp8 two-shot

@@ -197,3 +197,34 @@ def test_failure_close_aborts_device_communicator():
     res, code, errs = run_ranks(2, _abort_job, timeout=60, expect_fail=True)
     assert res.get(0) == "aborted" and not errs
     assert code == 1                  # the master aggregates the non-zero close
+
+
+def rsag_autotune_job(comm):
+    eng = comm.device
+    p, r = comm.getSlaveNum(), comm.getRank()
+    t = torch.ones(4096, dtype=torch.float32)
+    rs = eng.autotune_reduce_scatter(t, Operators.Float.SUM, iters=2)
+    ag = eng.autotune_allgather(t, iters=2)
+    assert set(rs) == {"rccl", "a2a"} and set(ag) == {"rccl", "p2p"}     # no IPC on CPU tensors
+    eng.stats.clear()
+    froms, tos, _ = CommUtils.even_split(0, 4000, p)                        # same size class
+    x = torch.full((4000,), float(r + 1))
+    eng.reduce_scatter(x, froms, tos, Operators.Float.SUM)
+    assert torch.all(x[froms[r]:tos[r]] == p * (p + 1) / 2)
+    y = torch.full((4000,), -1.0)
+    y[froms[r]:tos[r]] = r
+    eng.allgather(y, froms, tos)
+    for j in range(p):
+        assert torch.all(y[froms[j]:tos[j]] == j)
+    best_rs = min(rs, key=rs.get)
+    best_ag = min(ag, key=ag.get)
+    return best_rs, best_ag, dict(eng.stats)
+
+
+def test_rs_ag_autotune_consistent_and_applied():
+    res, code, _ = run_ranks(2, rsag_autotune_job, timeout=120)
+    assert code == 0
+    assert len({(a, b) for a, b, _ in res.values()}) == 1
+    for best_rs, best_ag, st in res.values():
+        assert st.get("reduce_scatter." + ("a2a" if best_rs == "a2a" else "rccl")) == 1
+        assert st.get("allgather.p2p" if best_ag == "p2p" else "allgather") == 1
