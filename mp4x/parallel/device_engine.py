@@ -145,6 +145,13 @@ class DeviceEngine:
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
+        tune_file = os.environ.get("MP4X_TUNE_FILE")
+        if tune_file and os.path.exists(tune_file):
+            try:
+                n = self.load_tuning(tune_file)
+                LOG.info("rank %d: %d pinned schedules from %s", self.rank, n, tune_file)
+            except Exception as e:   # noqa: BLE001 — a stale or foreign table is ignored, not fatal
+                LOG.warning("ignoring tuning table %s: %s", tune_file, e)
         # fail-stop detector for hung / failed collectives (parallel/watchdog.py)
         from . import watchdog
         self.watchdog = watchdog.CollectiveWatchdog(self) if coll is None and watchdog.enabled() else None
@@ -487,6 +494,7 @@ class DeviceEngine:
         best = min(res, key=res.get) if res else None
         if best is not None and res[best] != float("inf"):
             self._tuned[_tune_key(view.dtype, op, nbytes)] = best
+            self._autosave()
         return res
 
     def autotune_reduce_scatter(self, like: torch.Tensor, operator, iters: int = 3) -> Dict[str, float]:
@@ -530,6 +538,7 @@ class DeviceEngine:
         best = min(res, key=res.get) if res else None
         if best is not None and best != "rccl" and res[best] != float("inf"):
             self._tuned[key] = best
+        self._autosave()
         return res
 
     def _time_fn(self, run, uses_ipc: bool, iters: int, name: str) -> float:
@@ -553,6 +562,64 @@ class DeviceEngine:
             LOG.warning("autotune: %s failed: %s", name, e)
             ok = False
         return dt if ok else float("inf")
+
+    # ------------------------------------------------------------------ persisted tuning table
+    _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "a2a", "rhd"},
+                    "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"}}
+
+    def _topology(self) -> dict:
+        dev = torch.cuda.get_device_name(self.device) if self.device.type == "cuda" else "cpu"
+        return {"p": self.p, "device": dev, "backend": self.backend}
+
+    def tuning_table(self) -> dict:
+        """The schedules pinned by the autotuners, JSON-able, with the topology they were measured
+        on (rank count, device, backend).  A table only applies to the same topology."""
+        rows = []
+        for k, v in sorted(self._tuned.items(), key=lambda kv: str(kv[0])):
+            kind, dt, code, cls = k if isinstance(k[0], str) else ("allreduce",) + tuple(k)
+            rows.append({"kind": kind, "dtype": str(dt).replace("torch.", ""), "op": int(code),
+                         "size_class": int(cls), "algo": v})
+        return {"topology": self._topology(), "rows": rows}
+
+    def save_tuning(self, path: str) -> None:
+        """Rank 0 writes :meth:`tuning_table` to ``path`` (atomic rename); other ranks no-op."""
+        if self.rank != 0:
+            return
+        import json
+        tmp = f"{path}.tmp{os.getpid()}"
+        with open(tmp, "w") as f:
+            json.dump(self.tuning_table(), f, indent=1)
+        os.replace(tmp, path)
+
+    def load_tuning(self, src) -> int:
+        """Pin the schedules of a saved table (path or dict).  Refuses a table measured on another
+        topology; skips rows naming unknown schedules.  Every rank must load the same table (a
+        shared file), so the choices stay rank-consistent.  Returns the number of rows pinned."""
+        import json
+        table = src
+        if not isinstance(src, dict):
+            with open(src) as f:
+                table = json.load(f)
+        if table.get("topology") != self._topology():
+            raise Mp4jException(f"tuning table for {table.get('topology')}, this job is {self._topology()}")
+        n = 0
+        for row in table.get("rows", []):
+            kind, algo = row["kind"], row["algo"]
+            if algo not in self._KNOWN_ALGOS.get(kind, ()):
+                continue
+            dt = getattr(torch, row["dtype"])
+            key = (dt, int(row["op"]), int(row["size_class"]))
+            self._tuned[key if kind == "allreduce" else (kind,) + key] = algo
+            n += 1
+        return n
+
+    def _autosave(self) -> None:
+        path = os.environ.get("MP4X_TUNE_FILE")
+        if path:
+            try:
+                self.save_tuning(path)
+            except OSError as e:
+                LOG.warning("could not save the tuning table to %s: %s", path, e)
 
     def _time_candidate(self, c: str, view: torch.Tensor, op, iters: int) -> float:
         """Seconds per call of schedule ``c`` (inf when it failed on this rank).  Collective."""

@@ -228,3 +228,31 @@ def test_rs_ag_autotune_consistent_and_applied():
     for best_rs, best_ag, st in res.values():
         assert st.get("reduce_scatter." + ("a2a" if best_rs == "a2a" else "rccl")) == 1
         assert st.get("allgather.p2p" if best_ag == "p2p" else "allgather") == 1
+
+
+def tuning_roundtrip_job(comm, path):
+    import os
+    eng = comm.device
+    t = torch.ones(4096, dtype=torch.float32)
+    eng.autotune_allreduce(t, Operators.Float.SUM, iters=1)
+    eng.autotune_reduce_scatter(t, Operators.Float.SUM, iters=1)
+    comm.peer_barrier()                       # rank 0 has written the table (MP4X_TUNE_FILE)
+    assert os.path.exists(path)
+    table = eng.tuning_table()
+    before = dict(eng._tuned)
+    eng._tuned.clear()
+    n = eng.load_tuning(path)
+    assert dict(eng._tuned) == before and n == len(table["rows"])
+    bad = dict(table, topology=dict(table["topology"], p=99))
+    try:
+        eng.load_tuning(bad)
+        raise AssertionError("foreign topology accepted")
+    except Exception as e:                    # noqa: BLE001
+        assert "tuning table for" in str(e)
+    return n
+
+
+def test_tuning_table_persists_and_reloads(tmp_path):
+    path = str(tmp_path / "tune.json")
+    res, code, _ = run_ranks(2, tuning_roundtrip_job, args=(path,), timeout=120, env={"MP4X_TUNE_FILE": path})
+    assert code == 0 and len(set(res.values())) == 1 and res[0] >= 1
