@@ -12,6 +12,7 @@
 //                   registers (the two-shot compressed allreduce's reduce step), optionally
 //                   re-quantised in the same pass for the all-gather leg.
 #include <hipcub/hipcub.hpp>
+#include <stdlib.h>
 
 #include "fp8.hpp"
 
@@ -26,7 +27,7 @@ __global__ __launch_bounds__(kBlock) void k_quant(const void* __restrict__ in, i
                                                   float* __restrict__ scales) {
   const int lane = threadIdx.x & 63;
   const int64_t nblk = (n + kQBlock - 1) / kQBlock;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t b0 = wave * QU; b0 < nblk; b0 += nwaves * QU) {
     float x[QU][4];
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(kBlock) void k_dequant_reduce(void* __restrict__ ou
                                                            float* __restrict__ s_out) {
   const int lane = threadIdx.x & 63;
   const int64_t nblk = (n + kQBlock - 1) / kQBlock;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t b = wave; b < nblk; b += nwaves) {
     const int64_t e = b * kQBlock + lane * 4;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_zs_mask(const W* __restrict__ in, co
   __shared__ int64_t lt_tab[3 * kZsMaxLdsChunks + 1];
   const int64_t* tab = zs_table_lds(table, nchunk, lt_tab);
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
     ZsChunk c[ZU];
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_zs_compact(const W* __restrict__ in,
   const int lane = threadIdx.x & 63;
   W* st = stage[threadIdx.x >> 6];
   const uint64_t lt = (1ull << lane) - 1;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
     ZsChunk c[ZU];
@@ -297,6 +298,164 @@ __global__ __launch_bounds__(kBlock) void k_zs_compact(const W* __restrict__ in,
   }
 }
 
+// Single-pass encode (replaces mask -> scan -> compact, which read the input twice): every
+// wave takes the next tile of ZU blocks from an atomic ticket, computes masks and counts,
+// publishes its tile total, and finds its exclusive prefix by DECOUPLED LOOK-BACK over the
+// predecessors' status words (64 predecessors per step, one per lane); then it stages its
+// non-zero words through LDS and stores them as one coalesced run.  Status word = 2-bit flag
+// (1 = tile total, 2 = inclusive prefix) + 62-bit value, written with ONE relaxed agent-scope
+// 64-bit atomic (the data is the flag: no fence, cdna guide G16 R2).  Tickets are handed out
+// in order, so every predecessor a wave waits on is already running and never waits on a
+// later tile: progress is guaranteed.  The output is identical to the three-kernel form.
+constexpr uint64_t kZsAgg = 1ull << 62, kZsInc = 2ull << 62, kZsVal = (1ull << 62) - 1;
+
+__device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Workgroup tiles: 8 waves x ZU blocks (8192 words at ZU = 4).  Wave totals combine in LDS;
+// ONE decoupled look-back per tile reads 512 predecessor status words per step (one per
+// thread), so the inclusive-prefix frontier advances 512 tiles per memory round trip.
+constexpr int kZsEncThreads = 512;
+constexpr int kZsEncWaves = kZsEncThreads / 64;
+
+template <typename W, int ZU>
+__global__ __launch_bounds__(kZsEncThreads) void k_zs_encode1(const W* __restrict__ in,
+                                                              const int64_t* __restrict__ table, int nchunk,
+                                                              int64_t nblk, int64_t ntiles,
+                                                              uint64_t* __restrict__ masks,
+                                                              int32_t* __restrict__ counts,
+                                                              int64_t* __restrict__ offs, W* __restrict__ vals,
+                                                              uint64_t* __restrict__ status,
+                                                              uint32_t* __restrict__ ticket) {
+  __shared__ int64_t lt_tab[3 * kZsMaxLdsChunks + 1];
+  __shared__ W stage[kZsEncWaves][ZU * kZsBlock];
+  __shared__ int64_t s_wave[kZsEncWaves];       // wave totals -> exclusive prefixes in the tile
+  __shared__ int64_t s_red[kZsEncWaves];        // look-back partial sums per wave
+  __shared__ uint64_t s_inc[kZsEncWaves], s_inv[kZsEncWaves];
+  __shared__ int64_t s_tile, s_excl;
+  __shared__ int s_done;
+  for (int i = threadIdx.x; i < 3 * nchunk + 1; i += kZsEncThreads) lt_tab[i] = table[i];
+  __syncthreads();
+  const int64_t* tab = lt_tab;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  W* st = stage[wv];
+  const uint64_t lt = (1ull << lane) - 1;
+  for (;;) {
+    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t t = s_tile;
+    if (t >= ntiles) break;
+    const int64_t b0 = (t * kZsEncWaves + wv) * ZU;   // this wave's first block
+    ZsChunk c[ZU];
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) c[u] = (b0 + u < nblk) ? zs_locate(tab, nchunk, b0 + u) : ZsChunk{0, 0};
+    W v[ZU][4];
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) zs_load4<W>(in, c[u].base, c[u].len, lane, v[u]);   // ZU loads in flight
+    uint64_t mk[ZU][4];
+    int cnt[ZU];
+    int agg = 0;
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      cnt[u] = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        mk[u][k] = (b0 + u < nblk) ? __ballot(v[u][k] != (W)0) : 0ull;
+        cnt[u] += __popcll(mk[u][k]);
+      }
+      agg += cnt[u];
+    }
+    if (lane == 0) s_wave[wv] = agg;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t run = 0;
+      for (int w = 0; w < kZsEncWaves; ++w) {
+        const int64_t x = s_wave[w];
+        s_wave[w] = run;
+        run += x;
+      }
+      s_excl = run;                                     // tile total until the look-back
+      __hip_atomic_store(&status[t], (t == 0 ? kZsInc : kZsAgg) | (uint64_t)run, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const int64_t tile_total = s_excl;
+    int64_t excl = 0;
+    if (t > 0) {                                        // workgroup-wide decoupled look-back
+      int64_t j = t - 1;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        const int64_t idx = j - threadIdx.x;
+        const uint64_t sw = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                     : kZsInc;
+        const uint32_t flag = (uint32_t)(sw >> 62);
+        const uint64_t inc = __ballot(flag == 2), inv = __ballot(flag == 0);
+        if (lane == 0) {
+          s_inc[wv] = inc;
+          s_inv[wv] = inv;
+        }
+        __syncthreads();
+        int first = kZsEncThreads;                      // nearest inclusive (thread index)
+        for (int w = 0; w < kZsEncWaves; ++w)
+          if (s_inc[w]) {
+            first = w * 64 + __ffsll((long long)s_inc[w]) - 1;
+            break;
+          }
+        bool wait = false;                              // any unpublished word at or before `first`
+        for (int w = 0; w < kZsEncWaves && w * 64 <= first; ++w) {
+          const int hi = first - w * 64;                // lanes 0..hi of wave w are needed
+          const uint64_t need = hi >= 63 ? ~0ull : ((2ull << hi) - 1);
+          if (s_inv[w] & need) wait = true;
+        }
+        if (wait) {
+          // one thread decides the give-up (10 s: never hang) so every wave leaves together
+          if (threadIdx.x == 0) s_done = __builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull;
+          __syncthreads();                              // also: s_inc / s_inv are rewritten next pass
+          if (s_done) break;
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const int64_t part = wave_sum_i64((int)threadIdx.x <= first ? (int64_t)(sw & kZsVal) : 0);
+        if (lane == 0) s_red[wv] = part;
+        __syncthreads();
+        for (int w = 0; w < kZsEncWaves; ++w) excl += s_red[w];
+        __syncthreads();
+        if (first < kZsEncThreads) break;
+        j -= kZsEncThreads;                             // 512 tile totals: look further back
+      }
+      if (threadIdx.x == 0)
+        __hip_atomic_store(&status[t], kZsInc | (uint64_t)(excl + tile_total), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int64_t pos = excl + s_wave[wv];                    // this wave's first word in vals
+    const int64_t wbase = pos;
+#pragma unroll
+    for (int u = 0; u < ZU; ++u) {
+      if (b0 + u >= nblk) break;
+      if (lane == 0) {
+        counts[b0 + u] = cnt[u];
+        offs[b0 + u] = pos;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) masks[(b0 + u) * 4 + k] = mk[u][k];
+      }
+      int q = (int)(pos - wbase);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) q += __popcll(mk[u][k] & lt);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (v[u][k] != (W)0) st[q++] = v[u][k];
+      pos += cnt[u];
+    }
+    if (b0 < nblk && b0 + ZU >= nblk && lane == 0) offs[nblk] = pos;   // the last block's wave
+    wave_lds_sync();
+    for (int i = lane; i < agg; i += 64) vals[wbase + i] = st[i];
+    __syncthreads();                                    // stage / s_wave reused by the next tile
+  }
+}
+
 template <typename W, int ZU>
 __global__ __launch_bounds__(kBlock) void k_zs_expand(const uint64_t* __restrict__ masks,
                                                       const int64_t* __restrict__ offs, const W* __restrict__ vals,
@@ -308,7 +467,7 @@ __global__ __launch_bounds__(kBlock) void k_zs_expand(const uint64_t* __restrict
   const int lane = threadIdx.x & 63;
   W* st = stage[threadIdx.x >> 6];
   const uint64_t lt = (1ull << lane) - 1;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t b0 = wave * ZU; b0 < nblk; b0 += nwaves * ZU) {
     ZsChunk c[ZU];
@@ -352,9 +511,31 @@ __global__ void k_zs_total(const int64_t* __restrict__ offs, const int32_t* __re
   *total = nblk ? offs[nblk - 1] + counts[nblk - 1] : 0;
 }
 
+static int64_t zs_tiles(int64_t nblk) { return (nblk + ZU2 * kZsEncWaves - 1) / (ZU2 * kZsEncWaves); }
+static size_t zs_status_bytes(int64_t nblk) { return (size_t)(zs_tiles(nblk) + 2) * sizeof(uint64_t); }
+
 template <typename W>
 static int zs_encode_t(const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,
                        int32_t* counts, int64_t* offs, void* vals, void* temp, size_t temp_bytes, hipStream_t st) {
+  const int64_t ntiles = zs_tiles(nblk);
+  if (temp_bytes < zs_status_bytes(nblk)) return MP4X_E_BADARG;
+  uint64_t* status = (uint64_t*)temp;
+  uint32_t* ticket = (uint32_t*)(status + ntiles);
+  int e = (int)hipMemsetAsync(temp, 0, zs_status_bytes(nblk), st);    // re-initialised every call
+  if (e) return e;
+  // enough workgroups to fill the chip (4 x 512 threads per CU); each loops over tickets
+  const int g = (int)(ntiles < 1024 ? ntiles : 1024);
+  hipLaunchKernelGGL((k_zs_encode1<W, ZU2>), dim3(g), dim3(kZsEncThreads), 0, st, (const W*)in, table, nchunk, nblk,
+                     ntiles, masks, counts, offs, (W*)vals, status, ticket);
+  return (int)hipGetLastError();
+}
+
+// The three-kernel form (mask pass, hipCUB scan, compaction): the default (see zs_twopass) and
+// the reference the single-pass kernel is tested against.
+template <typename W>
+static int zs_encode_twopass_t(const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,
+                               int32_t* counts, int64_t* offs, void* vals, void* temp, size_t temp_bytes,
+                               hipStream_t st) {
   const int g = grid_for((nblk + ZU - 1) / ZU * 64, 1);
   hipLaunchKernelGGL(k_zs_mask<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, masks, counts);
   int e = (int)hipGetLastError();
@@ -423,7 +604,28 @@ extern "C" size_t mp4x_zs_temp_bytes(int64_t nblk) {
   size_t bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int64_t*)nullptr,
                                          (int)(nblk < 1 ? 1 : nblk), (hipStream_t)0);
-  return bytes;
+  const size_t sb = zs_status_bytes(nblk < 1 ? 1 : nblk);      // single-pass encode: tile status words
+  return bytes > sb ? bytes : sb;
+}
+
+static int g_zs_twopass = -1;
+
+// Default: the three-kernel form.  Measured on MI355X, 256 MiB f32 (profiles/r1/kbench9.json):
+// 0.213 ms against 0.324 ms for the single-pass kernel — every workgroup serialises ticket ->
+// loads -> look-back per tile, so the second read the single pass saves costs less than the
+// latency it exposes.  MP4X_ZS_ONEPASS=1 selects the single pass.
+static int zs_twopass() {
+  if (g_zs_twopass < 0) {
+    const char* e = getenv("MP4X_ZS_ONEPASS");
+    g_zs_twopass = (e && e[0] == '1') ? 0 : 1;
+  }
+  return g_zs_twopass;
+}
+
+// A/B switch: 1 = mask + scan + compact (two reads of the input), 0 = single-pass encode
+extern "C" int mp4x_zs_set_twopass(int on) {
+  g_zs_twopass = on ? 1 : 0;
+  return 0;
 }
 
 // table (device int64): elem_start[nchunk], elem_len[nchunk], blk_start[nchunk + 1] (blk_start[j]
@@ -435,6 +637,15 @@ extern "C" int mp4x_zs_encode(int elem_bytes, const void* in, const int64_t* tab
   if (nblk <= 0) return 0;
   if (nchunk <= 0 || nchunk > kZsMaxLdsChunks) return MP4X_E_BADARG;
   hipStream_t st = (hipStream_t)stream;
+  if (zs_twopass()) {
+    switch (elem_bytes) {
+      case 1: return zs_encode_twopass_t<uint8_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+      case 2: return zs_encode_twopass_t<uint16_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+      case 4: return zs_encode_twopass_t<uint32_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+      case 8: return zs_encode_twopass_t<uint64_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
+      default: return MP4X_E_UNSUPPORTED;
+    }
+  }
   switch (elem_bytes) {
     case 1: return zs_encode_t<uint8_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);
     case 2: return zs_encode_t<uint16_t>(in, table, nchunk, nblk, masks, counts, offs, vals, temp, temp_bytes, st);

@@ -25,6 +25,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 #endif
 
 constexpr int kBlock = 256;          // 4 wave64 per workgroup
+
+// Global wave index of a kBlock-thread workgroup, made provably wave-uniform
+// (readfirstlane): everything derived from it (block indices, mask / offset loads) then
+// lives in SGPRs and is fetched with scalar loads instead of 64 copies in VGPRs.
+__device__ __forceinline__ int64_t wave_id() {
+  return (int64_t)blockIdx.x * (kBlock / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+}
 constexpr int kMaxGrid = 256 * 8;    // 256 CUs x 8 resident blocks: grid-stride beyond this
 
 inline int grid_for(int64_t work_items, int per_thread = 1) {

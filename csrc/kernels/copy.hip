@@ -39,7 +39,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows_vec(u32x4* __restrict__ 
                                                             int G) {
   const int lane = threadIdx.x & 63;
   const int grp = lane / G, sub = lane % G, R = 64 / G;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t r0 = wave * R; r0 < nrows; r0 += nwaves * R) {
     const int64_t r = r0 + grp;
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(char* __restrict__ out, 
                                                         const int64_t* __restrict__ idx, int64_t nrows,
                                                         int64_t row_bytes) {
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   const bool vec = ((row_bytes & 15) == 0) && ((((uintptr_t)out | (uintptr_t)in) & 15) == 0);
   for (int64_t r = wave; r < nrows; r += nwaves) {

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce(const int64_t* __rest
   S* out_vals = reinterpret_cast<S*>(out_vals_);
   const int lane = threadIdx.x & 63;
   const int64_t nruns = *nruns_dev;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t u = wave; u < nruns; u += nwaves) {
     const int64_t s = starts[u];
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void k_segment_reduce_vec(const int64_t* __
   const int lane = threadIdx.x & 63;
   const int grp = lane / G, sub = lane % G, R = 64 / G;
   const int64_t nruns = *nruns_dev;
-  const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
   for (int64_t u0 = wave * R; u0 < nruns; u0 += nwaves * R) {
     const int64_t u = u0 + grp;

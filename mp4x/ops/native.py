@@ -46,6 +46,7 @@ _HIP_SIGS = {
     "mp4x_dequant_reduce_fp8": (c_int, [c_int, c_void_p, PP, PP, c_int, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "mp4x_dequant_fp8": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_int64, c_void_p]),
     "mp4x_zs_temp_bytes": (c_size_t, [c_int64]),
+    "mp4x_zs_set_twopass": (c_int, [c_int]),
     "mp4x_zs_encode": (c_int, [c_int, c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),
     "mp4x_zs_decode": (c_int, [c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int64, c_void_p, c_void_p,

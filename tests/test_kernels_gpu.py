@@ -272,6 +272,34 @@ def test_reduce_by_key_first_is_k8_dedupe(dim, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16, torch.int8])
+@pytest.mark.parametrize("density", [0.0, 0.03, 0.5, 1.0])
+def test_zs_single_pass_encode_matches_three_kernel_form(dtype, density):
+    """Single-pass encode (decoupled look-back) == mask + scan + compact, word for word, over
+    several chunks (many tiles, so the look-back crosses 64-tile windows)."""
+    K = _native()
+    from mp4x.ops import native
+    n = 3_000_000 + 77
+    x = (torch.randn(n, device=DEV) * 10).to(dtype)
+    x[torch.rand(n, device=DEV) >= density] = 0
+    chunks = [(0, 1_000_003), (1_000_003, 999_000), (1_999_003, n - 1_999_003)]
+    lib = native.hip()
+    try:
+        lib.mp4x_zs_set_twopass(1)
+        ref = K.zs_encode(x, chunks)
+        lib.mp4x_zs_set_twopass(0)
+        got = K.zs_encode(x, chunks)
+    finally:
+        lib.mp4x_zs_set_twopass(1)       # back to the default
+    for a, b in zip(ref[:3], got[:3]):
+        assert torch.equal(a.view(torch.uint8) if a.dtype.is_floating_point else a,
+                           b.view(torch.uint8) if b.dtype.is_floating_point else b)
+    assert ref[3] == got[3] and ref[4] == got[4]
+    out = torch.empty_like(x)
+    K.zs_decode(got[0], got[1], got[2], chunks, out)
+    assert torch.equal(out.view(torch.uint8), x.view(torch.uint8))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16, torch.int8])
 def test_zs_codec_roundtrip_bits(dtype):
     """K6b: masks / counts / compacted words decode to the identical bit pattern (-0.0, NaN kept)."""
     K = _native()

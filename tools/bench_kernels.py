@@ -120,6 +120,11 @@ def main():
         zx = torch.randn(zn, device=dev)
         if dens < 1:
             zx *= (torch.rand(zn, device=dev) < dens)
+        from mp4x.ops import native
+        native.hip().mp4x_zs_set_twopass(0)
+        ms = timeit(lambda: K.zs_encode(zx), max(3, a.iters // 4))
+        res[f"k6b_zs_encode_1pass_256MiB_d{dens}"] = {"ms": ms, "GBps": zn * 4 / ms / 1e6}
+        native.hip().mp4x_zs_set_twopass(1)     # the default three-kernel form
         ms = timeit(lambda: K.zs_encode(zx), max(3, a.iters // 4))
         res[f"k6b_zs_encode_256MiB_d{dens}"] = {"ms": ms, "GBps": zn * 4 / ms / 1e6}
         m_, c_, v_, _, _ = K.zs_encode(zx)
