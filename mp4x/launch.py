@@ -31,8 +31,9 @@ def init_from_env(thread_num: int = 0, heartbeat: bool = True, timeout: float = 
     key = "mp4x/master_addr"
     host = "127.0.0.1" if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost") \
         else os.environ["MASTER_ADDR"]
+    host_master = None
     if world == 1:
-        _embedded = CommMaster(1, 0, host=host, exit_on_timeout=False,
+        _embedded = host_master = CommMaster(1, 0, host=host, exit_on_timeout=False,
                                heartbeat_timeout=None if heartbeat else float("inf")).start()
         mhost, mport = host, _embedded.port
     else:
@@ -42,15 +43,21 @@ def init_from_env(thread_num: int = 0, heartbeat: bool = True, timeout: float = 
         if rank == 0:
             os.environ["MP4X_EMBEDDED_MASTER"] = "1"
             bind = "127.0.0.1" if host == "127.0.0.1" else "0.0.0.0"
-            _embedded = CommMaster(world, 0, host=bind, exit_on_timeout=True,
+            _embedded = host_master = CommMaster(world, 0, host=bind, exit_on_timeout=True,
                                    heartbeat_timeout=None if heartbeat else float("inf")).start()
             store.set(key, f"{host}:{_embedded.port}")
         addr = store.get(key).decode()
         mhost, mport = addr.rsplit(":", 1)
         mport = int(mport)
     if thread_num and thread_num >= 1:
-        return ThreadCommSlave("mp4x", thread_num, mhost, mport, rank=rank, heartbeat=heartbeat)
-    return ProcessCommSlave("mp4x", mhost, mport, rank=rank, heartbeat=heartbeat)
+        comm = ThreadCommSlave("mp4x", thread_num, mhost, mport, rank=rank, heartbeat=heartbeat)
+        pc = comm.processCommSlave
+    else:
+        comm = pc = ProcessCommSlave("mp4x", mhost, mport, rank=rank, heartbeat=heartbeat)
+    if host_master is not None:
+        # this process hosts the master: its close() must outlive every other rank's close
+        pc._embedded_master = host_master
+    return comm
 
 
 def embedded_master() -> Optional[CommMaster]:

@@ -175,6 +175,12 @@ class ProcessCommSlave:
         LOG.info("close code=%s", code)
         try:
             self.server.call("close", self.rank, int(code))
+            master = getattr(self, "_embedded_master", None)
+            if master is not None:
+                # the master lives in this process (mp4x.launch): returning — and letting the
+                # process exit — before every other rank's close message arrived would reset their
+                # connections mid-close.  A failure close ends the wait at once.
+                master.stop(timeout=float(os.environ.get("MP4X_MASTER_LINGER", 300.0)))
         finally:
             self.closed = True
             self._hb_stop.set()
