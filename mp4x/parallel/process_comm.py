@@ -775,7 +775,11 @@ def _nbytes(x) -> int:
 def _traced(name, fn):
     def wrapper(self, *args, **kwargs):
         a0 = args[0] if args else None
-        with self.tracer.span(name, _nbytes(a0), a0 if _is_device_tensor(a0) else None):
+        tr = self.tracer
+        if not tr.enabled:                       # counters only: keep the latency tier lean
+            tr.count(name, _nbytes(a0))
+            return fn(self, *args, **kwargs)
+        with tr.span(name, _nbytes(a0), a0 if _is_device_tensor(a0) else None):
             return fn(self, *args, **kwargs)
     wrapper.__name__ = fn.__name__
     wrapper.__doc__ = fn.__doc__

@@ -11,10 +11,13 @@ This watchdog is the missing detector, one daemon thread per device engine:
   still inside after ``MP4X_WATCHDOG_TIMEOUT`` seconds (default 600, the reference's
   heartbeat gap, Server.java:82-83) is a hang (gloo / p2p / host-synchronising schedules
   block the calling thread);
-* device side — when an outermost collective returns, a HIP event is recorded on the stream
-  it ran on; an event still pending after the timeout means that stream is stuck.  This is
-  the asynchronous-error check ``ncclCommGetAsyncError`` polling gives an RCCL job (torch's
-  ProcessGroupNCCL watchdog does it for RCCL alone), extended to mp4x's own kernels;
+* device side — when an outermost collective returns and no earlier event is still
+  outstanding, a HIP event is recorded on the stream it ran on; an event still pending after
+  the timeout means that stream is stuck.  This is the asynchronous-error check
+  ``ncclCommGetAsyncError`` polling gives an RCCL job (torch's ProcessGroupNCCL watchdog does it
+  for RCCL alone), extended to mp4x's own kernels.  One outstanding event at a time keeps the
+  latency tier cheap (a record per watchdog period at most, not per call; measured: a 4 KiB
+  public-API allreduce went from 20 to 29 us with an event per call);
 * IPC error words — the bounded spins of ``csrc/runtime/ipc.hip`` record a timed-out
   barrier in the signal block and exit; the watchdog reads that word on a private stream
   and treats a set word as a failure: that collective's result is invalid.
@@ -35,6 +38,7 @@ the shared client's lock inside a blocked RPC.  ``MP4X_WATCHDOG=0`` disables the
 from __future__ import annotations
 
 import collections
+import itertools
 import logging
 import os
 import threading
@@ -68,9 +72,10 @@ class CollectiveWatchdog:
         self.paused = 0                      # > 0: skip the IPC error-word check (autotune probes)
         self.quiet = 0                       # > 0: no device API calls at all (hipGraph capture)
         self._lock = threading.Lock()
-        self._inflight: Dict[int, Tuple[str, float]] = {}
-        self._next = 0
+        self._inflight: Dict[int, Tuple[str, float]] = {}   # GIL-atomic dict ops, no lock
+        self._tokens = itertools.count()
         self._pending: Dict[int, Deque] = {}   # stream handle -> deque[(name, t_enqueued, event)]
+        self._npending = 0                     # events recorded and not yet seen complete
         self._pool = []                        # completed events, reused
         self._stop = threading.Event()
         self._thread = threading.Thread(target=self._loop, daemon=True, name="mp4x-watchdog")
@@ -80,18 +85,15 @@ class CollectiveWatchdog:
     def begin(self, name: str) -> int:
         if self.failure is not None and self.action == "abort":
             raise Mp4jException(f"collective watchdog: {self.failure}")
-        with self._lock:
-            tok = self._next
-            self._next += 1
-            self._inflight[tok] = (name, time.monotonic())
+        tok = next(self._tokens)
+        self._inflight[tok] = (name, time.monotonic())
         return tok
 
     def end(self, tok: int, device=None) -> None:
-        with self._lock:
-            ent = self._inflight.pop(tok, None)
-            outer = not self._inflight
-        if ent is None or not outer or device is None or getattr(device, "type", None) != "cuda":
-            return
+        ent = self._inflight.pop(tok, None)
+        if ent is None or self._inflight or self._npending or device is None or \
+                getattr(device, "type", None) != "cuda":
+            return                       # nested call, or an outstanding event already covers the stream
         import torch
         if torch.cuda.is_current_stream_capturing():
             return                       # graph capture: nothing may be recorded outside the graph
@@ -103,6 +105,7 @@ class CollectiveWatchdog:
         ev.record(stream)
         with self._lock:
             self._pending.setdefault(stream.cuda_stream, collections.deque()).append((ent[0], time.monotonic(), ev))
+            self._npending += 1
 
     def stop(self) -> None:
         self._stop.set()
@@ -125,8 +128,8 @@ class CollectiveWatchdog:
     def check(self) -> Optional[str]:
         """One poll: the failure message, or None."""
         now = time.monotonic()
+        inflight = list(self._inflight.values())
         with self._lock:
-            inflight = list(self._inflight.values())
             streams = list(self._pending.values())
         for name, t0 in inflight:
             if now - t0 > self.timeout:
@@ -142,6 +145,7 @@ class CollectiveWatchdog:
                     dq.popleft()
                     with self._lock:
                         self._pool.append(ev)
+                        self._npending -= 1
                     continue
                 if now - t0 > self.timeout:
                     return (f"{name} not complete on the device {now - t0:.1f} s after it was issued "

@@ -56,6 +56,12 @@ class Tracer:
         self._events = []
         self._lock = threading.Lock()
 
+    def count(self, name: str, nbytes: int = 0) -> None:
+        """Counters only (the untraced fast path: no context manager, no roctx, no events)."""
+        with self._lock:
+            self.calls[name] += 1
+            self.bytes[name] += int(nbytes)
+
     @contextmanager
     def span(self, name: str, nbytes: int = 0, device_tensor=None):
         with self._lock:

@@ -123,9 +123,10 @@ def test_stuck_stream_is_detected_on_device():
     try:
         dev = torch.device("cuda", 0)
         torch.cuda.set_device(dev)
-        tok = wd.begin("allreduce")
+        torch.cuda._sleep(1)                # warm the launch path: the host bracket below stays short
+        torch.cuda.synchronize()
         torch.cuda._sleep(500_000_000)      # >= 0.2 s at any shader clock the box runs
-        wd.end(tok, dev)
+        wd.end(wd.begin("allreduce"), dev)  # the stream's event lands behind the long kernel
         assert _wait(lambda: hits, 10.0)
         assert "allreduce not complete on the device" in hits[0]
         torch.cuda.synchronize()
