@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(port, q, sizes, iters):
+def worker(port, q, sizes, iters, profile=None):
     import torch
     from mp4x import Operands, Operators, ProcessCommSlave
     torch.cuda.set_device(0)
@@ -33,11 +33,24 @@ def worker(port, q, sizes, iters):
             comm.allreduceArray(x, opnd, op, 0, x.numel())
         torch.cuda.synchronize()
         eng.barrier()
+        prof = None
+        if profile and comm.getRank() == 0:
+            import cProfile
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         for _ in range(iters):
             comm.allreduceArray(x, opnd, op, 0, x.numel())
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / iters
+        if prof is not None:
+            prof.disable()
+            import io
+            import pstats
+            buf = io.StringIO()
+            pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(25)
+            with open(f"{profile}.{nb}.txt", "w") as f:
+                f.write(buf.getvalue())
         out.append({"bytes": nb, "us_per_call": dt * 1e6, "algo": eng.select("allreduce", nb, op, x.dtype, opnd)})
         eng.barrier()
     comm.close(0)
@@ -49,6 +62,7 @@ def main():
     ap.add_argument("--procs", type=int, default=2)
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--sizes", default="4096,65536")
+    ap.add_argument("--profile", default=None, help="cProfile rank 0's timed loop into <prefix>.<bytes>.txt")
     a = ap.parse_args()
     os.environ.setdefault("MP4X_DEVICE_BACKEND", "gloo")
     from mp4x import CommMaster
@@ -56,7 +70,7 @@ def main():
     sizes = [int(x) for x in a.sizes.split(",")]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters)) for _ in range(a.procs)]
+    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters, a.profile)) for _ in range(a.procs)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=600) for _ in range(a.procs))
     [p.join(timeout=30) for p in ps]

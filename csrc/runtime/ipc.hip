@@ -123,14 +123,22 @@ __global__ void k_ipc_bump_epoch(uint32_t* epoch_dev) {
   *epoch_dev = e ? e : 1;
 }
 
+// src != nullptr: the kernel stages its own input (fused copy-in, one launch instead of a
+// memcpy + kernel): block b copies exactly the vectors block b of every peer will read, then
+// meets them at the start barrier (whose release fence publishes the copies).
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
-                                                              const uint32_t* epoch_dev) {
+                                                              const uint32_t* epoch_dev,
+                                                              const u32x4* __restrict__ src) {
   constexpr int p = NR;
   epoch = resolve_epoch(epoch, epoch_dev);
-  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  if (src) {
+    u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+    for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride) mine[v] = src[v];
+  }
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
     out[v] = reduce_vec<DT, OP, NR>(P, v);
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
@@ -140,15 +148,24 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* 
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
-                                                              const uint32_t* epoch_dev) {
+                                                              const uint32_t* epoch_dev,
+                                                              const u32x4* __restrict__ src) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
   epoch = resolve_epoch(epoch, epoch_dev);
-  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t chunk = (nvec + p - 1) / p;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
   const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
   u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  if (src) {   // fused copy-in: block b stages the chunk offsets block b of every peer reads
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t b = (int64_t)k * chunk;
+      const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+      for (int64_t v = b + off0; v < e; v += stride) mine[v] = src[v];
+    }
+  }
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   {
     const int64_t b = (int64_t)rank * chunk;
     const int64_t e = b + chunk < nvec ? b + chunk : nvec;
@@ -321,17 +338,19 @@ static int fp8_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t cb, i
 
 // set per call by mp4x_ipc_allreduce (host-side, single-threaded use per communicator)
 static thread_local const uint32_t* g_epoch_dev = nullptr;
+static thread_local const void* g_src = nullptr;     // fused copy-in source (nullptr: pre-staged)
 
 template <int DT, int OP, int NR>
 static int launch_nr(int algo, const IpcPtrs& P, Signal* self, int rank, int64_t nvec, void* out, uint32_t epoch,
                      int blocks, hipStream_t st) {
   const uint32_t* edev = g_epoch_dev;
+  const u32x4* src = (const u32x4*)g_src;
   if (algo == 0)
     hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch, edev);
+                       (u32x4*)out, epoch, edev, src);
   else
     hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch, edev);
+                       (u32x4*)out, epoch, edev, src);
   return (int)hipGetLastError();
 }
 
@@ -440,6 +459,23 @@ extern "C" int mp4x_ipc_bump_epoch(uint32_t* epoch_dev, void* stream) {
 
 // epoch_dev == NULL: `epoch` (host counter) is used.  epoch_dev != NULL: graph-capturable form,
 // the kernel reads the epoch from device memory (bump it with mp4x_ipc_bump_epoch first).
+extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream);
+
+// Same, with the copy of this rank's input (`src`, 16-byte aligned) into its own buffer fused
+// into the kernel: one launch per call instead of hipMemcpyAsync + kernel.
+extern "C" int mp4x_ipc_allreduce_from(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                       int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
+                                       int blocks, const uint32_t* epoch_dev, void* stream) {
+  if (!src || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
+  g_src = src;
+  int e = mp4x_ipc_allreduce(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, out, epoch, blocks, epoch_dev,
+                             stream);
+  g_src = nullptr;
+  return e;
+}
+
 extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                   int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
                                   const uint32_t* epoch_dev, void* stream) {

@@ -140,7 +140,22 @@ def ptr_array(ptrs: Sequence[int]):
     return ctypes.cast(arr, PP), arr
 
 
+_current_raw_stream = None
+
+
 def stream_ptr(stream=None) -> int:
-    import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return int(s.cuda_stream)
+    """hipStream_t of ``stream`` (default: torch's current stream on the current device).  The
+    default case is on every launch's path, so it goes straight to torch's raw-stream query
+    instead of building a ``torch.cuda.Stream`` object (measured ~4 us per call)."""
+    if stream is not None:
+        return int(stream.cuda_stream)
+    global _current_raw_stream
+    if _current_raw_stream is None:
+        import torch
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        dev = getattr(torch._C, "_cuda_getDevice", None)
+        if raw is not None and dev is not None:
+            _current_raw_stream = lambda: raw(dev())      # noqa: E731
+        else:
+            _current_raw_stream = lambda: torch.cuda.current_stream().cuda_stream   # noqa: E731
+    return int(_current_raw_stream())

@@ -41,6 +41,8 @@ native.register_signatures({
     "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
                                    c_int, c_void_p, c_void_p]),
+    "mp4x_ipc_allreduce_from": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
+                                        ctypes.c_uint32, c_int, c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
     "mp4x_device_pci_id": (c_int, [ctypes.c_char_p, c_int]),
     "mp4x_ipc_reduce_scatter": (c_int, [c_int, c_int, PP, PP, c_int, c_int, c_int64, c_int64, c_void_p,
@@ -120,6 +122,8 @@ class IpcAllreduce:
         self._copy_stream = None
         self._epoch_dev = None     # device epoch counter for graph-captured calls (lazy)
         self._sig_stream = None    # private stream for error-word reads (lazy)
+        self._overlap_default = os.environ.get("MP4X_IPC_OVERLAP", "0") == "1"
+        self._fuse_copy = os.environ.get("MP4X_IPC_FUSED_COPY", "1") == "1"
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -153,7 +157,7 @@ class IpcAllreduce:
         src = view.view(torch.uint8)
         dst = out.view(torch.uint8)
         if overlap is None:
-            overlap = os.environ.get("MP4X_IPC_OVERLAP", "0") == "1"
+            overlap = self._overlap_default
         if total > self.nbytes and overlap and not torch.cuda.is_current_stream_capturing():
             return self._allreduce_pipelined(src, dst, total, dt, op, algo, blocks, out)
         piece = self.nbytes - self.nbytes % 16
@@ -164,16 +168,23 @@ class IpcAllreduce:
         if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
+        fused = src.data_ptr() % 16 == 0 and self._fuse_copy   # copy-in inside the kernel: one launch
         while off < total:
             m = min(piece, total - off)
-            check(self.lib.mp4x_memcpy_async(self._data.value, src.data_ptr() + off, m, st), "ipc input copy")
+            if not fused:
+                check(self.lib.mp4x_memcpy_async(self._data.value, src.data_ptr() + off, m, st), "ipc input copy")
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
-            check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0], self.rank,
-                                              self.p, m, dst.data_ptr() + off, self.epoch, blocks, edev, st),
-                  "mp4x_ipc_allreduce")
+            if fused:
+                check(self.lib.mp4x_ipc_allreduce_from(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
+                                                       self.rank, self.p, m, src.data_ptr() + off, dst.data_ptr() + off,
+                                                       self.epoch, blocks, edev, st), "mp4x_ipc_allreduce_from")
+            else:
+                check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
+                                                  self.rank, self.p, m, dst.data_ptr() + off, self.epoch, blocks,
+                                                  edev, st), "mp4x_ipc_allreduce")
             off += m
         return out
 
