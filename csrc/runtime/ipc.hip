@@ -241,6 +241,52 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_gather(IpcPtrs P, Signal* s
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
 }
 
+// ---------------------------------------------------------------- copy plans (bcast / scatter / gather)
+// The data-movement collectives as ONE kernel per call: a plan of up to kIpcMaxRanks "stage"
+// items (this rank's input -> its own buffer, fused copy-in) and up to kIpcMaxRanks "pull" items
+// (a peer's buffer -> this rank's output, over xGMI, all pulls interleaved so every link
+// streams).  Every item is walked with the same grid-stride relative index on every rank, so
+// the vectors block b stages are exactly the vectors block b of the peers pull: per-block
+// barriers suffice, as in the two-shot.  Units: 16-byte vectors.
+struct CopyItem {
+  int64_t src_off, dst_off, len;
+  int64_t peer;          // pull: source rank; stage: unused
+};
+struct CopyPlan {
+  CopyItem stage[kIpcMaxRanks];
+  CopyItem pull[kIpcMaxRanks];
+  int nstage, npull;
+};
+
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_copy_plan(IpcPtrs P, Signal* self, int rank, int p,
+                                                                CopyPlan plan, const u32x4* __restrict__ src,
+                                                                u32x4* __restrict__ out, uint32_t epoch,
+                                                                const uint32_t* epoch_dev) {
+  epoch = resolve_epoch(epoch, epoch_dev);
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
+  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  for (int i = 0; i < plan.nstage; ++i) {
+    const CopyItem it = plan.stage[i];
+    MP4X_DASSERT(it.len >= 0);
+    for (int64_t v = off0; v < it.len; v += stride) mine[it.dst_off + v] = src[it.src_off + v];
+  }
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  int64_t maxlen = 0;
+  for (int i = 0; i < plan.npull; ++i) maxlen = plan.pull[i].len > maxlen ? plan.pull[i].len : maxlen;
+  for (int64_t v = off0; v < maxlen; v += stride) {
+    u32x4 x[kIpcMaxRanks];
+#pragma unroll
+    for (int i = 0; i < kIpcMaxRanks; ++i)           // every pull's vector in flight at once
+      if (i < plan.npull && v < plan.pull[i].len)
+        x[i] = reinterpret_cast<const u32x4*>(P.data[plan.pull[i].peer])[plan.pull[i].src_off + v];
+#pragma unroll
+    for (int i = 0; i < kIpcMaxRanks; ++i)
+      if (i < plan.npull && v < plan.pull[i].len) out[plan.pull[i].dst_off + v] = x[i];
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
 // ---------------------------------------------------------------- fused fp8 two-shot (K6 on xGMI)
 // Compressed allreduce with the block-scaled e4m3 codec on the links, in ONE kernel per piece
 // (the quantise of this rank's input into its own IPC buffer runs just before, stream-ordered):
@@ -644,4 +690,35 @@ extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* c
 
 extern "C" int mp4x_memset_async(void* dst, int value, size_t bytes, void* stream) {
   return (int)hipMemsetAsync(dst, value, bytes, (hipStream_t)stream);
+}
+
+// Copy plan (see k_ipc_copy_plan).  stage / pull: n x {src_off, dst_off, len, peer} int64
+// quadruples in 16-byte vectors; `grid_len` (vectors) must be rank-independent — the largest
+// item of any rank — so every rank launches the same grid.
+extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
+                                  const int64_t* stage, int nstage, const int64_t* pull, int npull, const void* src,
+                                  void* out, int64_t grid_len, int64_t buf_vecs, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream) {
+  IpcPtrs P;
+  if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
+  if (nstage < 0 || nstage > kIpcMaxRanks || npull < 0 || npull > kIpcMaxRanks) return MP4X_E_BADARG;
+  if ((nstage && (!src || ((uintptr_t)src & 15))) || (npull && (!out || ((uintptr_t)out & 15)))) return MP4X_E_BADARG;
+  CopyPlan plan;
+  plan.nstage = nstage;
+  plan.npull = npull;
+  for (int i = 0; i < kIpcMaxRanks; ++i) {
+    plan.stage[i] = i < nstage ? CopyItem{stage[4 * i], stage[4 * i + 1], stage[4 * i + 2], 0} : CopyItem{0, 0, 0, 0};
+    plan.pull[i] = i < npull ? CopyItem{pull[4 * i], pull[4 * i + 1], pull[4 * i + 2], pull[4 * i + 3]}
+                             : CopyItem{0, 0, 0, 0};
+    if (i < nstage && (plan.stage[i].len < 0 || plan.stage[i].dst_off < 0 ||
+                       plan.stage[i].dst_off + plan.stage[i].len > buf_vecs))
+      return MP4X_E_BADARG;                               // staging stays inside the own buffer
+    if (i < npull && (plan.pull[i].len < 0 || plan.pull[i].peer < 0 || plan.pull[i].peer >= p ||
+                      plan.pull[i].src_off < 0 || plan.pull[i].src_off + plan.pull[i].len > buf_vecs))
+      return MP4X_E_BADARG;                               // pulls stay inside the peer's buffer
+  }
+  blocks = ipc_blocks(blocks, grid_len);
+  hipLaunchKernelGGL(k_ipc_copy_plan, dim3(blocks), dim3(kIpcThreads), 0, (hipStream_t)stream, P,
+                     (Signal*)signal_ptrs[rank], rank, p, plan, (const u32x4*)src, (u32x4*)out, epoch, epoch_dev);
+  return (int)hipGetLastError();
 }

@@ -981,9 +981,23 @@ class DeviceEngine:
                 self.scatter(flat, froms, tos, root)
                 self.allgather(flat, froms, tos)
                 return arr
+            if self._ipc_small_ok(flat, (to - frm) * flat.element_size()) and \
+                    self._ipc_obj.broadcast(flat, frm, to, root):
+                self._count("broadcast.ipc")
+                return arr
             self._count("broadcast")
             self.coll.broadcast(flat[frm:to], root)
         return arr
+
+    def _ipc_small_ok(self, flat: torch.Tensor, nbytes: int) -> bool:
+        """The IPC copy-plan tier for broadcast / scatter / gather: up to the two-shot size, schedule
+        not forced.  (Alignment and buffer fit are checked by IpcAllreduce, rank-independently.)"""
+        if self.algo not in ("", "auto") or nbytes > self.ipc_twoshot_max or not self.ipc_enabled:
+            return False
+        if flat.is_cuda and torch.cuda.is_current_stream_capturing() and \
+                (self._ipc_obj is None or self._ipc_obj._epoch_dev is None):
+            return False
+        return self.ipc() is not None
 
     def reduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand, root: int):
         flat = self._flat(arr)
@@ -1006,6 +1020,10 @@ class DeviceEngine:
     def gather(self, arr: torch.Tensor, froms, tos, root: int):
         flat = self._flat(arr)
         r = self.rank
+        if self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
+                self._ipc_obj.gather(flat, froms, tos, root):
+            self._count("gather.ipc")
+            return arr
         self._count("gather")
         if r == root:
             self.coll.p2p([], [(flat[froms[j]:tos[j]], j) for j in range(self.p) if j != r and tos[j] > froms[j]])
@@ -1016,6 +1034,10 @@ class DeviceEngine:
     def scatter(self, arr: torch.Tensor, froms, tos, root: int):
         flat = self._flat(arr)
         r = self.rank
+        if self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
+                self._ipc_obj.scatter(flat, froms, tos, root):
+            self._count("scatter.ipc")
+            return arr
         self._count("scatter")
         if r == root:
             self.coll.p2p([(flat[froms[j]:tos[j]], j) for j in range(self.p) if j != r and tos[j] > froms[j]], [])

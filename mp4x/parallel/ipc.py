@@ -44,6 +44,8 @@ native.register_signatures({
     "mp4x_ipc_allreduce_from": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
                                         ctypes.c_uint32, c_int, c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
+    "mp4x_ipc_copy_plan": (c_int, [PP, PP, c_int, c_int, ctypes.POINTER(c_int64), c_int, ctypes.POINTER(c_int64), c_int,
+                                   c_void_p, c_void_p, c_int64, c_int64, ctypes.c_uint32, c_int, c_void_p, c_void_p]),
     "mp4x_device_pci_id": (c_int, [ctypes.c_char_p, c_int]),
     "mp4x_ipc_reduce_scatter": (c_int, [c_int, c_int, PP, PP, c_int, c_int, c_int64, c_int64, c_void_p,
                                         ctypes.c_uint32, c_int, c_void_p, c_void_p]),
@@ -310,6 +312,80 @@ class IpcAllreduce:
         n = (tos[-1] - base) * es
         if n:
             check(self.lib.mp4x_memcpy_async(flat[base:].data_ptr(), self._data.value, n, st), "ipc AG out")
+        return True
+
+    # ---------------------------------------------------------------- broadcast / scatter / gather
+    # One copy-plan kernel per call (csrc/runtime/ipc.hip k_ipc_copy_plan): the owning ranks stage
+    # their data into their own buffers inside the kernel, the receivers pull it over xGMI.  For
+    # messages up to the buffer size; ranges must be whole 16-byte vectors from a 16-byte aligned
+    # tensor (checked identically on every rank from the shared arguments).
+    def _plan(self, stage, pull, src_ptr, out_ptr, grid_len) -> None:
+        st = stream_ptr()
+        edev = self._next_epoch(st)
+        sa = (c_int64 * (4 * max(1, len(stage))))(*[x for it in stage for x in it])
+        pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
+        check(self.lib.mp4x_ipc_copy_plan(self._pp_data[0], self._pp_sig[0], self.rank, self.p, sa, len(stage), pa,
+                                          len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, self.epoch,
+                                          self._grid(grid_len), edev, st), "mp4x_ipc_copy_plan")
+
+    def _vec_ok(self, view: torch.Tensor, bounds) -> bool:
+        es = view.element_size()
+        if not view.is_contiguous() or view.data_ptr() % 16:
+            return False
+        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+            return False
+        return all((b * es) % 16 == 0 for b in bounds)
+
+    def broadcast(self, view: torch.Tensor, frm: int, to: int, root: int) -> bool:
+        es = view.element_size()
+        if to <= frm or (to - frm) * es > self.nbytes or not self._vec_ok(view, (frm, to)):
+            return False
+        base = view.data_ptr()
+        L = (to - frm) * es // 16
+        off = frm * es // 16
+        if self.rank == root:
+            self._plan([(off, 0, L, 0)], [], base, None, L)
+        else:
+            self._plan([], [(0, off, L, root)], None, base, L)
+        return True
+
+    def scatter(self, view: torch.Tensor, froms, tos, root: int) -> bool:
+        es = view.element_size()
+        p, r = self.p, self.rank
+        lens = [(t - f) * es // 16 for f, t in zip(froms, tos)]
+        if sum(ln for j, ln in enumerate(lens) if j != root) * 16 > self.nbytes or \
+                not self._vec_ok(view, list(froms) + list(tos)):
+            return False
+        grid = max([ln for j, ln in enumerate(lens) if j != root] or [0])
+        if grid == 0:
+            return True
+        boff, o = [0] * p, 0
+        for j in range(p):
+            if j != root:
+                boff[j] = o
+                o += lens[j]
+        base = view.data_ptr()
+        if r == root:
+            self._plan([(froms[j] * es // 16, boff[j], lens[j], 0) for j in range(p) if j != root], [], base, None,
+                       grid)
+        else:
+            self._plan([], [(boff[r], froms[r] * es // 16, lens[r], root)], None, base, grid)
+        return True
+
+    def gather(self, view: torch.Tensor, froms, tos, root: int) -> bool:
+        es = view.element_size()
+        p, r = self.p, self.rank
+        lens = [(t - f) * es // 16 for f, t in zip(froms, tos)]
+        if max(lens) * 16 > self.nbytes or not self._vec_ok(view, list(froms) + list(tos)):
+            return False
+        grid = max([ln for j, ln in enumerate(lens) if j != root] or [0])
+        if grid == 0:
+            return True
+        base = view.data_ptr()
+        if r == root:
+            self._plan([], [(0, froms[j] * es // 16, lens[j], j) for j in range(p) if j != root], None, base, grid)
+        else:
+            self._plan([(froms[r] * es // 16, 0, lens[r], 0)], [], base, None, grid)
         return True
 
     # ---------------------------------------------------------------- piecewise large RS / AG
