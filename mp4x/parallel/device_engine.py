@@ -1005,8 +1005,16 @@ class DeviceEngine:
         if view.numel() == 0:
             return arr
         op = self._op(operator, view)
-        if self.algo != "composite" and \
-                self.select("reduce", view.numel() * view.element_size(), op, view.dtype) == "rccl":
+        nbytes = view.numel() * view.element_size()
+        if self.algo in ("", "auto") and nbytes <= self.ipc_oneshot_max and self._ipc_ok(op, view.dtype, nbytes) \
+                and self._ipc_small_ok(flat, nbytes):
+            # latency tier: the one-shot allreduce kernel (non-root results are unspecified by the
+            # reduce contract, ProcessCommSlave.java:1390-1421, so every rank may receive the sum)
+            self._count("reduce.ipc1")
+            from .ipc import ONESHOT
+            self._ipc_obj.allreduce(view, op, algo=ONESHOT)
+            return arr
+        if self.algo != "composite" and self.select("reduce", nbytes, op, view.dtype) == "rccl":
             self._count("reduce.rccl")
             self.coll.reduce(view, root, op.code)
         else:   # reduce-scatter + gather (reference reduceArray composition, ProcessCommSlave.java:1390-1421)

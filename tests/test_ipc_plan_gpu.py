@@ -121,6 +121,11 @@ def _engine_worker(port, q):
         comm.gatherArray(z, F, froms, tos, p - 1)
         if r == p - 1:
             ok &= all(bool(torch.all(z[froms[j]:tos[j]] == j * 2)) for j in range(p))
+        from mp4x import Operators
+        w = torch.full((n,), float(r + 1), device="cuda")
+        comm.reduceArray(w, F, Operators.Float.SUM, 0, n, 0)
+        if r == 0:
+            ok &= bool(torch.all(w == p * (p + 1) / 2))
         st = dict(comm.device.stats)
         comm.close(0)
         q.put((r, "ok", (ok, st)))
@@ -128,7 +133,7 @@ def _engine_worker(port, q):
         q.put((-1, "err", traceback.format_exc()))
 
 
-def test_engine_routes_small_bcast_scatter_gather_through_ipc():
+def test_engine_routes_small_bcast_scatter_gather_reduce_through_ipc():
     from mp4x import CommMaster
     p = 2
     m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
@@ -151,5 +156,5 @@ def test_engine_routes_small_bcast_scatter_gather_through_ipc():
         m.stop(timeout=5)
     for r, (ok, stats) in res.items():
         assert ok, r
-        for k in ("broadcast.ipc", "scatter.ipc", "gather.ipc"):
+        for k in ("broadcast.ipc", "scatter.ipc", "gather.ipc", "reduce.ipc1"):
             assert stats.get(k) == 1, (r, stats)
