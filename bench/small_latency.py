@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def worker(port, q, sizes, iters, profile=None):
+def worker(port, q, sizes, iters, profile=None, ops=False):
     import torch
     from mp4x import Operands, Operators, ProcessCommSlave
     torch.cuda.set_device(0)
@@ -26,6 +26,35 @@ def worker(port, q, sizes, iters, profile=None):
     comm = ProcessCommSlave("b", "127.0.0.1", port, heartbeat=False)
     eng = comm.device            # gloo stands in for RCCL on a shared GPU; the IPC tier is real
     out = []
+    if ops:
+        from mp4x import CommUtils
+        p, r = comm.getSlaveNum(), comm.getRank()
+        for nb in sizes:
+            n = nb // 8                                  # double[] like the reference's table
+            x = torch.randn(n, device="cuda", dtype=torch.float64)
+            D, SUM = Operands.DOUBLE_OPERAND(), Operators.Double.SUM
+            fr, to = CommUtils.createProcessArrayFroms(n, p), CommUtils.createProcessArrayTos(n, p)
+            calls = {"gather": lambda: comm.gatherArray(x, D, fr, to, 0),
+                     "scatter": lambda: comm.scatterArray(x, D, fr, to, 0),
+                     "allgather": lambda: comm.allgatherArray(x, D, fr, to),
+                     "reduce_scatter": lambda: comm.reduceScatterArray(x, D, SUM, 0, [t - f for f, t in zip(fr, to)]),
+                     "broadcast": lambda: comm.broadcastArray(x, D, 0, n, 0),
+                     "reduce": lambda: comm.reduceArray(x, D, SUM, 0, n, 0),
+                     "allreduce": lambda: comm.allreduceArray(x, D, SUM, 0, n)}
+            for name, fn in calls.items():
+                for _ in range(20):
+                    fn()
+                torch.cuda.synchronize()
+                eng.barrier()
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    fn()
+                torch.cuda.synchronize()
+                out.append({"op": name, "bytes": n * 8, "us_per_call": (time.perf_counter() - t0) / iters * 1e6})
+                eng.barrier()
+        comm.close(0)
+        q.put((comm.getRank(), out))
+        return
     for nb in sizes:
         x = torch.randn(nb // 4, device="cuda")
         opnd, op = Operands.FLOAT_OPERAND(), Operators.Float.SUM
@@ -63,6 +92,8 @@ def main():
     ap.add_argument("--iters", type=int, default=2000)
     ap.add_argument("--sizes", default="4096,65536")
     ap.add_argument("--profile", default=None, help="cProfile rank 0's timed loop into <prefix>.<bytes>.txt")
+    ap.add_argument("--all-ops", action="store_true",
+                    help="every collective of the reference's table on double[] (sizes in bytes)")
     a = ap.parse_args()
     os.environ.setdefault("MP4X_DEVICE_BACKEND", "gloo")
     from mp4x import CommMaster
@@ -70,13 +101,16 @@ def main():
     sizes = [int(x) for x in a.sizes.split(",")]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters, a.profile)) for _ in range(a.procs)]
+    ps = [ctx.Process(target=worker, args=(m.port, q, sizes, a.iters, a.profile, a.all_ops)) for _ in range(a.procs)]
     [p.start() for p in ps]
     res = dict(q.get(timeout=600) for _ in range(a.procs))
     [p.join(timeout=30) for p in ps]
     m.stop(timeout=5)
     for i, row in enumerate(res[0]):
         worst = max(res[r][i]["us_per_call"] for r in res)
+        if a.all_ops:
+            print(json.dumps({"procs_on_one_gpu": a.procs, **row, "us_per_call_max_rank": worst}))
+            continue
         print(json.dumps({"procs_on_one_gpu": a.procs, "watchdog": os.environ.get("MP4X_WATCHDOG", "1"),
                           **row, "us_per_call_max_rank": worst}))
 

@@ -1006,13 +1006,13 @@ class DeviceEngine:
             return arr
         op = self._op(operator, view)
         nbytes = view.numel() * view.element_size()
-        if self.algo in ("", "auto") and nbytes <= self.ipc_oneshot_max and self._ipc_ok(op, view.dtype, nbytes) \
-                and self._ipc_small_ok(flat, nbytes):
-            # latency tier: the one-shot allreduce kernel (non-root results are unspecified by the
+        if self.algo in ("", "auto") and self._ipc_ok(op, view.dtype, nbytes) and self._ipc_small_ok(flat, nbytes):
+            # latency tier: the IPC allreduce kernels (non-root results are unspecified by the
             # reduce contract, ProcessCommSlave.java:1390-1421, so every rank may receive the sum)
-            self._count("reduce.ipc1")
-            from .ipc import ONESHOT
-            self._ipc_obj.allreduce(view, op, algo=ONESHOT)
+            from .ipc import ONESHOT, TWOSHOT
+            one = nbytes <= self.ipc_oneshot_max
+            self._count("reduce.ipc1" if one else "reduce.ipc2")
+            self._ipc_obj.allreduce(view, op, algo=ONESHOT if one else TWOSHOT)
             return arr
         if self.algo != "composite" and self.select("reduce", nbytes, op, view.dtype) == "rccl":
             self._count("reduce.rccl")
