@@ -206,15 +206,25 @@ struct Segs {
   int64_t hi[kIpcMaxRanks];
 };
 
+// src != nullptr: fused staging — block b copies, for EVERY rank's segment k, the vectors block b
+// of rank k will read from this buffer (segment-relative grid stride), then meets the peers.
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_reduce_range(IpcPtrs P, Signal* self, int rank, int64_t lo,
                                                                    int64_t hi, u32x4* __restrict__ out,
-                                                                   uint32_t epoch, const uint32_t* epoch_dev) {
+                                                                   uint32_t epoch, const uint32_t* epoch_dev,
+                                                                   const u32x4* __restrict__ src, Segs S) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && lo <= hi);
   epoch = resolve_epoch(epoch, epoch_dev);
-  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  if (src) {
+    u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+    const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      for (int64_t v = S.lo[k] + off0; v < S.hi[k]; v += stride) mine[v] = src[v];
+  }
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   for (int64_t v = lo + (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < hi; v += stride)
     out[v - lo] = reduce_vec<DT, OP, NR>(P, v);
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
@@ -575,13 +585,18 @@ static int ipc_blocks(int blocks, int64_t nvec) {
   return blocks > kIpcMaxBlocks ? kIpcMaxBlocks : blocks;
 }
 
+static thread_local const void* g_rs_src = nullptr;   // fused RS staging source (nullptr: pre-staged)
+static thread_local Segs g_rs_segs;
+
 template <int DT, int OP>
 static int rs_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t lo, int64_t hi, void* out, uint32_t epoch,
                  const uint32_t* edev, int blocks, hipStream_t st) {
+  const u32x4* src = (const u32x4*)g_rs_src;
+  const Segs S = g_rs_segs;
 #define MP4X_RS_CASE(N)                                                                                 \
   case N:                                                                                               \
     hipLaunchKernelGGL((k_ipc_reduce_range<DT, OP, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, \
-                       rank, lo, hi, (u32x4*)out, epoch, edev);                                         \
+                       rank, lo, hi, (u32x4*)out, epoch, edev, src, S);                                 \
     return (int)hipGetLastError();
   switch (p) {
     MP4X_RS_CASE(2) MP4X_RS_CASE(3) MP4X_RS_CASE(4) MP4X_RS_CASE(5) MP4X_RS_CASE(6) MP4X_RS_CASE(7) MP4X_RS_CASE(8)
@@ -627,6 +642,29 @@ extern "C" int mp4x_ipc_reduce_scatter(int dtype, int op, void* const* data_ptrs
     case MP4X_F16: return rs_dt<MP4X_F16>(op, P, self, rank, p, vec_lo, vec_hi, out, epoch, epoch_dev, blocks, st);
     default: return MP4X_E_UNSUPPORTED;
   }
+}
+
+// Reduce-scatter with fused staging: `src` (16-B aligned) holds this rank's whole range laid out
+// like the buffer (vector offsets seg_lo/seg_hi per rank, relative to src and to the buffer);
+// this rank's reduced segment goes straight to `out` (16-B aligned).  One launch, no copies.
+extern "C" int mp4x_ipc_reduce_scatter_from(int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                            int rank, int p, const int64_t* seg_lo, const int64_t* seg_hi,
+                                            const void* src, void* out, uint32_t epoch, int blocks,
+                                            const uint32_t* epoch_dev, void* stream) {
+  if (!src || ((uintptr_t)src & 15) || p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p) return MP4X_E_BADARG;
+  Segs S;
+  for (int k = 0; k < kIpcMaxRanks; ++k) {
+    S.lo[k] = k < p ? seg_lo[k] : 0;
+    S.hi[k] = k < p ? seg_hi[k] : 0;
+    if (k < p && (S.lo[k] < 0 || S.hi[k] < S.lo[k])) return MP4X_E_BADARG;
+  }
+  g_rs_src = src;
+  g_rs_segs = S;
+  // `out` receives vectors [lo, hi) at out[v - lo]
+  int e = mp4x_ipc_reduce_scatter(dtype, op, data_ptrs, signal_ptrs, rank, p, S.lo[rank], S.hi[rank], out, epoch,
+                                  blocks, epoch_dev, stream);
+  g_rs_src = nullptr;
+  return e;
 }
 
 // All-gather of ragged segments: seg_lo/seg_hi[p] (host arrays, 16-B vectors from the buffer

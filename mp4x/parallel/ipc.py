@@ -43,6 +43,9 @@ native.register_signatures({
                                    c_int, c_void_p, c_void_p]),
     "mp4x_ipc_allreduce_from": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
                                         ctypes.c_uint32, c_int, c_void_p, c_void_p]),
+    "mp4x_ipc_reduce_scatter_from": (c_int, [c_int, c_int, PP, PP, c_int, c_int, ctypes.POINTER(c_int64),
+                                             ctypes.POINTER(c_int64), c_void_p, c_void_p, ctypes.c_uint32, c_int,
+                                             c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
     "mp4x_ipc_copy_plan": (c_int, [PP, PP, c_int, c_int, ctypes.POINTER(c_int64), c_int, ctypes.POINTER(c_int64), c_int,
                                    c_void_p, c_void_p, c_int64, c_int64, ctypes.c_uint32, c_int, c_void_p, c_void_p]),
@@ -277,6 +280,18 @@ class IpcAllreduce:
         base, r = froms[0], self.rank
         st = stream_ptr()
         n = (tos[-1] - base) * es
+        if self._fuse_copy and flat[base:].data_ptr() % 16 == 0 and n:
+            # one launch: the kernel stages this rank's range and writes its segment in place
+            edev = self._next_epoch(st)
+            lo_a = (c_int64 * self.p)(*[(f - base) * es // 16 for f in froms])
+            hi_a = (c_int64 * self.p)(*[(t - base) * es // 16 for t in tos])
+            maxv = max(h - l_ for l_, h in zip(lo_a, hi_a))
+            check(self.lib.mp4x_ipc_reduce_scatter_from(int(dtype_of_torch(view.dtype)), int(op.code),
+                                                        self._pp_data[0], self._pp_sig[0], r, self.p, lo_a, hi_a,
+                                                        flat[base:].data_ptr(), flat[froms[r]:].data_ptr(),
+                                                        self.epoch, self._grid(maxv), edev, st),
+                  "mp4x_ipc_reduce_scatter_from")
+            return True
         if n:
             check(self.lib.mp4x_memcpy_async(self._data.value, flat[base:].data_ptr(), n, st), "ipc RS staging")
         edev = self._next_epoch(st)
@@ -297,6 +312,19 @@ class IpcAllreduce:
         es = view.element_size()
         flat = view.view(-1)
         base, r = froms[0], self.rank
+        if self._fuse_copy and flat[base:].data_ptr() % 16 == 0 and \
+                (not torch.cuda.is_current_stream_capturing() or self._epoch_dev is not None):
+            # one copy-plan launch: stage the own segment in-kernel, pull every peer's segment
+            # straight into the output (no staging copy, no copy-out)
+            b16 = flat[base:].data_ptr()
+            lo = [(f - base) * es // 16 for f in froms]
+            ln = [(t - f) * es // 16 for f, t in zip(froms, tos)]
+            grid = max(ln)
+            if grid == 0:
+                return True
+            pulls = [(lo[j], lo[j], ln[j], j) for j in range(self.p) if j != r and ln[j]]
+            self._plan([(lo[r], lo[r], ln[r], 0)] if ln[r] else [], pulls, b16, b16, grid)
+            return True
         st = stream_ptr()
         seg = (tos[r] - froms[r]) * es
         if seg:
