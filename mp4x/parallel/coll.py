@@ -55,9 +55,17 @@ class TorchColl:
     def p2p(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
         ops = [dist.P2POp(dist.isend, t, j, group=self.pg) for t, j in sends]
         ops += [dist.P2POp(dist.irecv, t, j, group=self.pg) for t, j in recvs]
+        # gloo's send/recv of a DEVICE tensor is not ordered after the kernels queued on the
+        # current stream (one-GPU rehearsals stand gloo in for RCCL): drain the stream first.
+        # RCCL orders its own stream after the current one, so the production path never waits.
+        gloo_dev = self.backend == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs))
         if ops:
+            if gloo_dev:
+                torch.cuda.current_stream().synchronize()
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+            if gloo_dev:
+                torch.cuda.current_stream().synchronize()
 
     def barrier(self):
         dist.barrier(group=self.pg)

@@ -505,8 +505,20 @@ class DeviceEngine:
         op = self._op(operator, view)
         froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
         cands = ["rccl", "a2a"] + (["ipc"] if self.ipc_enabled and self._ipc_ok(op, view.dtype, 16) else [])
+        r = self.rank
+
+        def probe():
+            exp = self._fill_probe(view, op)
+            if exp is None:
+                return None
+
+            def check():
+                bad = int((view[froms[r]:tos[r]] != exp[froms[r]:tos[r]]).sum())
+                view.zero_()
+                return bad
+            return check
         return self._autotune_kind("reduce_scatter", view, op, cands,
-                                   lambda: self.reduce_scatter(view, froms, tos, op), iters)
+                                   lambda: self.reduce_scatter(view, froms, tos, op), iters, probe)
 
     def autotune_allgather(self, like: torch.Tensor, iters: int = 3) -> Dict[str, float]:
         """All-gather twin of :meth:`autotune_allreduce` (equal split): RCCL
@@ -514,9 +526,26 @@ class DeviceEngine:
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
         cands = ["rccl", "p2p"] + (["ipc"] if self.ipc_enabled else [])
-        return self._autotune_kind("allgather", view, None, cands, lambda: self.allgather(view, froms, tos), iters)
+        def probe():
+            # owner j's segment holds i % 97 + j; after the call every rank holds every segment
+            idt = torch.int32 if view.numel() < (1 << 31) else torch.int64
+            exp = torch.arange(view.numel(), device=view.device, dtype=idt).remainder_(97)
+            for j in range(self.p):
+                exp[froms[j]:tos[j]] += j
+            exp = exp.to(view.dtype)
+            view.fill_(-1)
+            view[froms[self.rank]:tos[self.rank]] = exp[froms[self.rank]:tos[self.rank]]
 
-    def _autotune_kind(self, kind: str, view: torch.Tensor, op, cands, run, iters: int) -> Dict[str, float]:
+            def check():
+                bad = int((view != exp).sum())
+                view.zero_()
+                return bad
+            return check
+        return self._autotune_kind("allgather", view, None, cands, lambda: self.allgather(view, froms, tos), iters,
+                                   probe)
+
+    def _autotune_kind(self, kind: str, view: torch.Tensor, op, cands, run, iters: int,
+                       probe=None) -> Dict[str, float]:
         key = self._rsag_key(kind, view, op)
         times = []
         if self.watchdog is not None:
@@ -527,7 +556,8 @@ class DeviceEngine:
                     self._tuned.pop(key, None)
                 else:
                     self._tuned[key] = c
-                times.append(self._time_fn(run, uses_ipc=c == "ipc", iters=iters, name=f"{kind}:{c}"))
+                times.append(self._time_fn(run, uses_ipc=c == "ipc", iters=iters, name=f"{kind}:{c}",
+                                           probe=probe))
         finally:
             self._tuned.pop(key, None)
             if self.watchdog is not None:
@@ -541,15 +571,23 @@ class DeviceEngine:
         self._autosave()
         return res
 
-    def _time_fn(self, run, uses_ipc: bool, iters: int, name: str) -> float:
-        """Seconds per call of ``run`` (inf when it failed on this rank).  Collective."""
+    def _time_fn(self, run, uses_ipc: bool, iters: int, name: str, probe=None) -> float:
+        """Seconds per call of ``run`` (inf when it failed on this rank).  Collective.
+
+        ``probe()`` (optional) fills the operand with an exact pattern and returns a function
+        that counts wrong elements after the warm-up call (see :meth:`_fill_probe`)."""
         ok = True
         dt = float("inf")
         try:
+            check = probe() if probe is not None and self._verify_autotune else None
             run()                                # warm-up (lazy IPC / RCCL setup)
             self._sync()
-            if uses_ipc and self._ipc_error():
+            wrong = check() if check is not None else 0
+            timeout, nwrong = self._agree([self._ipc_error_local() if uses_ipc else 0, wrong])
+            if timeout:
                 raise Mp4jException("IPC barrier timeout during warm-up")
+            if nwrong:
+                raise Mp4jException(f"wrong result on the probe pattern (up to {nwrong} elements differ)")
             self.barrier()
             t0 = time.perf_counter()
             for _ in range(max(1, iters)):
@@ -626,11 +664,21 @@ class DeviceEngine:
         ok = True
         dt = float("inf")
         try:
+            expect = self._fill_probe(view, op) if self._verify_autotune else None
             self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
             self._sync()
-            if c.startswith("ipc") and self._ipc_error():
-                # a barrier timed out (bounded spins): agree on it and skip the timed calls
+            # the warm-up doubles as a correctness probe: a schedule whose result differs from
+            # the exact answer (e.g. a peer-visibility bug on some topology) is never pinned.
+            # Both verdicts are agreed (MAX over ranks) so every rank skips the timed calls together.
+            wrong = 0
+            if expect is not None:
+                wrong = int((view != expect).sum())
+                view.zero_()
+            timeout, nwrong = self._agree([self._ipc_error_local() if c.startswith("ipc") else 0, wrong])
+            if timeout:
                 raise Mp4jException("IPC barrier timeout during warm-up")
+            if nwrong:
+                raise Mp4jException(f"wrong result on the probe pattern (up to {nwrong} elements differ)")
             self.barrier()
             t0 = time.perf_counter()
             for _ in range(max(1, iters)):
@@ -644,16 +692,45 @@ class DeviceEngine:
             ok = False
         return dt if ok else float("inf")
 
-    def _ipc_error(self) -> bool:
-        """Did any IPC barrier on ANY rank time out?  (Collective: MAX of the error words.)"""
+    def _ipc_error_local(self) -> int:
         mine = 0
         for inst in (self._ipc_obj, self._ipc_large):
             # read-and-clear: a candidate that timed out must not poison the next one's check
             if inst is not None and inst.error_word(clear=True):
                 mine = 1
-        t = torch.tensor([mine], dtype=torch.int32, device=self.device if self.backend == "nccl" else "cpu")
+        return mine
+
+    def _agree(self, flags: List[int]) -> List[int]:
+        """Element-wise MAX of small integer flags over all ranks (collective)."""
+        t = torch.tensor(flags, dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
         self.coll.all_reduce(t, OpCode.MAX)
-        return bool(t.item())
+        return [int(v) for v in t.tolist()]
+
+    def _ipc_error(self) -> bool:
+        """Did any IPC barrier on ANY rank time out?  (Collective: MAX of the error words.)"""
+        return bool(self._agree([self._ipc_error_local()])[0])
+
+    _verify_autotune = os.environ.get("MP4X_AUTOTUNE_VERIFY", "1") != "0"
+
+    def _fill_probe(self, view: torch.Tensor, op) -> Optional[torch.Tensor]:
+        """Fill ``view`` with this rank's probe pattern ``i % m + (rank & 1)`` and return the exact
+        allreduce of every rank's pattern (None for ops without a closed form).  Values stay
+        small integers (``p * m <= ~100``), so every schedule's result is exact in any order and
+        for every dtype down to int8 / bf16: the comparison is bit-exact."""
+        if op.code not in (OpCode.SUM, OpCode.MAX, OpCode.MIN) or getattr(op, "is_custom", False):
+            return None
+        m = max(2, min(16, 100 // self.p))
+        idt = torch.int32 if view.numel() < (1 << 31) else torch.int64
+        base = torch.arange(view.numel(), device=view.device, dtype=idt).remainder_(m)
+        odd = sum(r & 1 for r in range(self.p))
+        view.copy_(base + (self.rank & 1))
+        if op.code == OpCode.SUM:
+            exp = base * self.p + odd
+        elif op.code == OpCode.MAX:
+            exp = base + (1 if odd else 0)
+        else:
+            exp = base + (0 if odd < self.p else 1)
+        return exp.to(view.dtype)
 
     def _sync(self):
         if self.device.type == "cuda":

@@ -23,7 +23,7 @@ take int64 id tensors directly and are what a training loop should call.
 """
 from __future__ import annotations
 
-from typing import Dict, List, Optional, Tuple
+from typing import Dict, List, Optional
 
 import numpy as np
 import torch

@@ -182,6 +182,32 @@ def test_autotune_pins_fastest_schedule_consistently(p):
     assert all(st.get("allreduce." + best) == 1 for _, st in res.values())
 
 
+def broken_candidate_job(comm, dtype_name, opname):
+    """rank 1's "a2a" result is corrupted in one element: the probe catches it on that rank
+    only, the verdict is agreed, and every rank rules a2a out (inf) without a hang."""
+    eng = comm.device
+    dt = getattr(torch, dtype_name)
+    orig = eng._run_allreduce
+
+    def sabotaged(c, view, op):
+        orig(c, view, op)
+        if c == "a2a" and comm.getRank() == 1:
+            view[7] += 1
+    eng._run_allreduce = sabotaged
+    res = eng.autotune_allreduce(torch.ones(4096, dtype=dt), getattr(Operators.Float, opname), iters=1)
+    eng._run_allreduce = orig
+    return res
+
+
+@pytest.mark.parametrize("dtype_name,opname", [("float32", "SUM"), ("bfloat16", "MAX"), ("float32", "MIN")])
+def test_autotune_probe_rejects_a_wrong_schedule(dtype_name, opname):
+    res, code, _ = run_ranks(3, broken_candidate_job, (dtype_name, opname), timeout=120)
+    assert code == 0
+    for r in res.values():
+        assert r["a2a"] == float("inf") and len(r) >= 2
+        assert all(v < float("inf") for c, v in r.items() if c != "a2a")   # exact on the probe pattern
+
+
 def _abort_job(comm):
     t = torch.ones(64)
     comm.device.allreduce(t, 0, 64, Operators.Float.SUM)
@@ -256,3 +282,34 @@ def test_tuning_table_persists_and_reloads(tmp_path):
     path = str(tmp_path / "tune.json")
     res, code, _ = run_ranks(2, tuning_roundtrip_job, args=(path,), timeout=120, env={"MP4X_TUNE_FILE": path})
     assert code == 0 and len(set(res.values())) == 1 and res[0] >= 1
+
+
+def broken_rsag_job(comm):
+    """every reduce-scatter result is corrupted on rank 1 and every all-gather on rank 0: all
+    candidates are ruled out on all ranks (agreed verdict, no hang) and nothing is pinned."""
+    eng = comm.device
+    r = comm.getRank()
+    rs0, ag0 = eng.reduce_scatter, eng.allgather
+
+    def rs(view, froms, tos, op):
+        rs0(view, froms, tos, op)
+        if r == 1:
+            view[froms[r]] += 1
+
+    def ag(view, froms, tos):
+        ag0(view, froms, tos)
+        if r == 0:
+            view[-1] += 1
+    eng.reduce_scatter, eng.allgather = rs, ag
+    t = torch.ones(4096, dtype=torch.float32)
+    a = eng.autotune_reduce_scatter(t, Operators.Float.SUM, iters=1)
+    b = eng.autotune_allgather(t, iters=1)
+    return a, b, dict(eng._tuned)
+
+
+def test_rsag_autotune_probe_rejects_wrong_results():
+    res, code, _ = run_ranks(2, broken_rsag_job, timeout=120)
+    assert code == 0
+    for a, b, tuned in res.values():
+        assert all(v == float("inf") for v in a.values()) and all(v == float("inf") for v in b.values())
+        assert not tuned
