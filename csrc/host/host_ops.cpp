@@ -22,7 +22,11 @@
 #include <type_traits>
 #include <vector>
 
+#include <cerrno>
 #include <climits>
+#include <csignal>
+#include <cstdio>
+#include <cstdlib>
 
 #include <linux/futex.h>
 #include <sched.h>
@@ -212,6 +216,9 @@ struct BarrierWords {
   uint32_t n;
   double timeout_s;
   bool shared;
+  // optional liveness probe, polled while sleeping (shm engine: did a peer PROCESS exit?)
+  bool (*peer_dead)(const void*) = nullptr;
+  const void* ctx = nullptr;
 };
 
 static inline long futex_op(std::atomic<uint32_t>* addr, int op, uint32_t val, const timespec* ts, bool shared) {
@@ -223,7 +230,8 @@ static void barrier_wake_all(const BarrierWords& w) {
   if (w.sleepers->load(std::memory_order_seq_cst)) futex_op(w.gen, FUTEX_WAKE, INT_MAX, nullptr, w.shared);
 }
 
-// 0 released, -1 timed out (aborts the barrier for everyone), -2 aborted.
+// 0 released, -1 timed out (aborts the barrier for everyone), -2 aborted, -3 a peer process
+// exited (aborts the barrier for everyone).
 static int barrier_wait(const BarrierWords& w) {
   if (w.abort->load(std::memory_order_acquire)) return -2;
   const uint32_t g = w.gen->load(std::memory_order_acquire);
@@ -251,6 +259,12 @@ static int barrier_wait(const BarrierWords& w) {
     if (w.gen->load(std::memory_order_seq_cst) == g) futex_op(w.gen, FUTEX_WAIT, g, &nap, w.shared);
     w.sleepers->fetch_sub(1, std::memory_order_seq_cst);
     double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // every ~100 ms of sleeping: a dead peer never arrives, so fail now instead of at the timeout
+    if (w.peer_dead && (spins & 7) == 0 && w.gen->load(std::memory_order_acquire) == g && w.peer_dead(w.ctx)) {
+      w.abort->store(1, std::memory_order_release);
+      futex_op(w.gen, FUTEX_WAKE, INT_MAX, nullptr, w.shared);
+      return -3;
+    }
     if (el > w.timeout_s) {
       w.abort->store(1, std::memory_order_release);
       w.gen->fetch_add(0, std::memory_order_seq_cst);
@@ -262,6 +276,8 @@ static int barrier_wait(const BarrierWords& w) {
 }
 
 // ---------------------------------------------------------------- shared-memory engine
+constexpr int kShmMaxPids = 128;     // ranks beyond this are not liveness-checked
+
 struct alignas(64) ShmHeader {
   std::atomic<uint32_t> count;
   std::atomic<uint32_t> gen;
@@ -269,7 +285,43 @@ struct alignas(64) ShmHeader {
   std::atomic<uint32_t> sleepers;
   uint32_t p;
   int64_t slot_bytes;
+  int32_t pid[kShmMaxPids];          // each rank's pid + /proc start time, written at attach
+  uint64_t start[kShmMaxPids];
 };
+
+// state letter and start time (clock ticks since boot) of `pid` from /proc/<pid>/stat
+static bool proc_stat(int pid, char* state, uint64_t* start) {
+  char path[64];
+  snprintf(path, sizeof(path), "/proc/%d/stat", pid);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  char buf[1024];
+  size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  const char* q = strrchr(buf, ')');          // comm may contain spaces: parse after the last ')'
+  if (!q) return false;
+  // fields after comm: 3 state, 4 ppid, ... 22 starttime
+  char st = 0;
+  unsigned long long v = 0;
+  int field = 2;
+  const char* c = q + 1;
+  while (*c) {
+    while (*c == ' ') ++c;
+    if (!*c) break;
+    ++field;
+    if (field == 3) st = *c;
+    if (field == 22) {
+      v = strtoull(c, nullptr, 10);
+      break;
+    }
+    while (*c && *c != ' ') ++c;
+  }
+  if (field != 22) return false;
+  *state = st;
+  *start = v;
+  return true;
+}
 static_assert(sizeof(ShmHeader) <= 4096, "header");
 static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics need lock-free");
 
@@ -280,12 +332,31 @@ struct Shm {
   int64_t slot;
   int nt;
   double timeout_s;
+  bool watch = false;                // every peer's /proc entry was visible at attach time
   char* slot_ptr(int r) const { return base + 4096 + (int64_t)r * slot; }
 };
+
+// A peer whose /proc entry vanished, turned zombie / dead, or now belongs to a different
+// process (pid reused: start time differs) will never arrive at the barrier.
+static bool shm_peer_dead(const void* ctx) {
+  const Shm* s = static_cast<const Shm*>(ctx);
+  const int np = s->p < kShmMaxPids ? s->p : kShmMaxPids;
+  for (int r = 0; r < np; ++r) {
+    if (r == s->rank) continue;
+    char st;
+    uint64_t t;
+    if (!proc_stat(s->hdr->pid[r], &st, &t) || st == 'Z' || st == 'X' || t != s->hdr->start[r]) return true;
+  }
+  return false;
+}
 
 int shm_barrier(Shm* s) {
   ShmHeader* h = s->hdr;
   BarrierWords w{&h->count, &h->gen, &h->abort, &h->sleepers, (uint32_t)s->p, s->timeout_s, true};
+  if (s->watch) {
+    w.peer_dead = shm_peer_dead;
+    w.ctx = s;
+  }
   return barrier_wait(w);
 }
 
@@ -315,7 +386,29 @@ void* mp4x_shm_attach(void* base, int rank, int p, int64_t slot_bytes, int nthre
     s->hdr->p = (uint32_t)p;
     s->hdr->slot_bytes = slot_bytes;
   }
+  if (rank < kShmMaxPids) {
+    char st;
+    uint64_t t = 0;
+    s->hdr->pid[rank] = (int32_t)getpid();
+    s->hdr->start[rank] = proc_stat((int)getpid(), &st, &t) ? t : 0;
+  }
   return s;
+}
+
+// After every rank attached: turn on peer-death detection in the barrier iff every peer is
+// visible in this process's /proc with the start time it published (same pid namespace).
+// Returns 1 when enabled, 0 when not (the barrier then relies on its timeout alone).
+int mp4x_shm_watch_peers(void* h) {
+  Shm* s = (Shm*)h;
+  s->watch = false;
+  if (s->p > kShmMaxPids) return 0;
+  for (int r = 0; r < s->p; ++r) {
+    char st;
+    uint64_t t;
+    if (!proc_stat(s->hdr->pid[r], &st, &t) || t != s->hdr->start[r] || t == 0) return 0;
+  }
+  s->watch = true;
+  return 1;
 }
 
 void mp4x_shm_detach(void* h) { delete (Shm*)h; }

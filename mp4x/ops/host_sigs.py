@@ -12,6 +12,7 @@ HOST_SIGS = {
     "mp4x_shm_attach": (c_void_p, [c_void_p, c_int, c_int, c_int64, c_int, c_double]),
     "mp4x_shm_detach": (None, [c_void_p]),
     "mp4x_shm_barrier": (c_int, [c_void_p]),
+    "mp4x_shm_watch_peers": (c_int, [c_void_p]),
     "mp4x_shm_allreduce": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int64]),
     "mp4x_shm_reduce_scatter": (c_int, [c_void_p, c_int, c_int, c_void_p, P64, P64]),
     "mp4x_shm_allgather": (c_int, [c_void_p, c_int, c_void_p, P64, P64]),

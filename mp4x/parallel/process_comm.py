@@ -48,7 +48,9 @@ HEARTBEAT_PERIOD = float(os.environ.get("MP4X_HEARTBEAT_PERIOD", 15.0))
 HEARTBEAT_MAX_FAIL = int(os.environ.get("MP4X_HEARTBEAT_MAX_FAIL", 4))
 BCAST_TREE_BYTES = int(os.environ.get("MP4X_BCAST_TREE_BYTES", 1 << 16))
 SHM_ON = os.environ.get("MP4X_SHM", "1") == "1"
-SHM_MIN_BYTES = 1 << 20     # below this the TCP mesh wins (shm barrier round trips dominate)
+# same-host ranks take /dev/shm at every size: 4 procs, 16 doubles 34 us vs 500 us over the TCP
+# mesh; 800 KB 0.36 vs 1.8 ms; 8 procs 0.14 vs 1.3 ms (profiles/r1/host_shm_vs_tcp.jsonl)
+SHM_MIN_BYTES = 0
 
 
 def _is_device_tensor(x) -> bool:

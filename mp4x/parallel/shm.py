@@ -8,8 +8,10 @@ reductions at memory bandwidth, OpenMP-parallel, a process-shared atomic barrier
 phases.  Rank 0 creates the segment and unlinks it as soon as everyone attached, so no
 /dev/shm file outlives the job.
 
-Used by ProcessComm's host path for primitive arrays >= ``MP4X_SHM_MIN_BYTES`` (default
-1 MiB) with built-in operators; ``MP4X_SHM=0`` disables it.
+Used by ProcessComm's host path for primitive arrays >= ``MP4X_SHM_MIN_BYTES`` (default 0:
+every size) with built-in operators; ``MP4X_SHM=0`` disables it.  A peer process that exits
+is noticed by the barrier within ~0.1 s (its /proc entry is polled while waiting), so a
+crashed rank fails the job fast, as a closed TCP connection does on the mesh.
 """
 from __future__ import annotations
 
@@ -20,8 +22,18 @@ from multiprocessing import shared_memory
 
 import numpy as np
 
+from ..exceptions import TransportError
 from ..ops import native
-from ..ops.native import check
+from ..ops.native import check as _native_check
+
+_BARRIER_ERRORS = {-1: "barrier timed out (MP4X_SHM_TIMEOUT)", -2: "barrier aborted by a peer",
+                   -3: "a peer process exited (connection closed)"}
+
+
+def _check(rc: int, where: str) -> None:
+    if rc in _BARRIER_ERRORS:
+        raise TransportError(f"{where}: shared-memory {_BARRIER_ERRORS[rc]}")
+    _native_check(rc, where)
 
 
 def _untrack(shm: shared_memory.SharedMemory) -> None:
@@ -57,26 +69,30 @@ class ShmEngine:
         nt = int(threads or int(os.environ.get("MP4X_HOST_THREADS", 0)) or max(1, (os.cpu_count() or 2) // self.p))
         timeout = float(os.environ.get("MP4X_SHM_TIMEOUT", 300.0))
         self.h = self.lib.mp4x_shm_attach(ctypes.addressof(self._base), self.rank, self.p, self.slot, nt, timeout)
+        # every rank published its pid: from now on a barrier wait notices a peer process that
+        # exited (fail fast, like a closed TCP connection) instead of sleeping until the timeout
+        _check(self.lib.mp4x_shm_barrier(self.h), "shm attach barrier")
+        self.watching = bool(self.lib.mp4x_shm_watch_peers(self.h))
 
     @staticmethod
     def _ptr(a: np.ndarray, off_elems: int = 0) -> int:
         return a.ctypes.data + off_elems * a.itemsize
 
     def allreduce(self, buf: np.ndarray, frm: int, to: int, dtype: int, op: int):
-        check(self.lib.mp4x_shm_allreduce(self.h, dtype, op, self._ptr(buf, frm), to - frm), "shm_allreduce")
+        _check(self.lib.mp4x_shm_allreduce(self.h, dtype, op, self._ptr(buf, frm), to - frm), "shm_allreduce")
 
     def reduce_scatter(self, buf: np.ndarray, froms, tos, dtype: int, op: int):
         f = (ctypes.c_int64 * self.p)(*froms)
         t = (ctypes.c_int64 * self.p)(*tos)
-        check(self.lib.mp4x_shm_reduce_scatter(self.h, dtype, op, self._ptr(buf), f, t), "shm_reduce_scatter")
+        _check(self.lib.mp4x_shm_reduce_scatter(self.h, dtype, op, self._ptr(buf), f, t), "shm_reduce_scatter")
 
     def allgather(self, buf: np.ndarray, froms, tos):
         f = (ctypes.c_int64 * self.p)(*froms)
         t = (ctypes.c_int64 * self.p)(*tos)
-        check(self.lib.mp4x_shm_allgather(self.h, buf.itemsize, self._ptr(buf), f, t), "shm_allgather")
+        _check(self.lib.mp4x_shm_allgather(self.h, buf.itemsize, self._ptr(buf), f, t), "shm_allgather")
 
     def broadcast(self, buf: np.ndarray, frm: int, to: int, root: int):
-        check(self.lib.mp4x_shm_broadcast(self.h, buf.itemsize, self._ptr(buf), frm, to, root), "shm_broadcast")
+        _check(self.lib.mp4x_shm_broadcast(self.h, buf.itemsize, self._ptr(buf), frm, to, root), "shm_broadcast")
 
     def close(self):
         if getattr(self, "h", None):

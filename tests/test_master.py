@@ -144,13 +144,22 @@ def _faulty(comm):
     return "survived"
 
 
-def test_fault_injection_peer_death_is_detected_not_hung():
-    # rank 1 dies at its 2nd collective; rank 0 must get a TransportError, not hang
-    res, code, errs = run_ranks(2, _faulty, expect_fail=True, timeout=60,
-                                env={"MP4X_FAULT_INJECT": "1:2:exit", "MP4X_RECV_TIMEOUT": "20"})
+@pytest.mark.parametrize("p,engine", [(2, "tcp"), (2, "shm"), (3, "shm")])
+def test_fault_injection_peer_death_is_detected_not_hung(p, engine):
+    # rank 1 dies at its 2nd collective; the others must get a TransportError, not hang.  On
+    # /dev/shm the barrier polls the peers' /proc entries, so it fails in well under a second
+    # rather than at MP4X_SHM_TIMEOUT (300 s).
+    env = {"MP4X_FAULT_INJECT": "1:2:exit", "MP4X_RECV_TIMEOUT": "20"}
+    if engine == "tcp":
+        env["MP4X_SHM"] = "0"
+    t0 = time.monotonic()
+    res, code, errs = run_ranks(p, _faulty, expect_fail=True, timeout=60, env=env)
     assert "survived" not in res.values()
     assert errs, "surviving rank should report the failure"
     assert any("closed" in e or "timed out" in e for e in errs)
+    if engine == "shm":
+        assert any("shared-memory" in e for e in errs)
+        assert time.monotonic() - t0 < 20
 
 
 def test_exchange_pairs_ranks():

@@ -132,7 +132,8 @@ def prim_matrix(comm, kind, compress, n):
 @pytest.mark.parametrize("p", [1, 2, 3, 4])
 @pytest.mark.parametrize("kind", list(PRIM))
 def test_primitive_matrix(p, kind):
-    res, code, _ = run_ranks(p, prim_matrix, (kind, False, 1001))
+    """The TCP mesh engine (ring / RHD / trees); same-host ranks would otherwise take /dev/shm."""
+    res, code, _ = run_ranks(p, prim_matrix, (kind, False, 1001), env={"MP4X_SHM": "0"})
     assert all(v == "ok" for v in res.values())
     assert code == 0
 
@@ -264,7 +265,7 @@ def big_ring(comm):
 
 
 def test_large_allreduce_4_ranks():
-    res, _, _ = run_ranks(4, big_ring, timeout=180)
+    res, _, _ = run_ranks(4, big_ring, timeout=180, env={"MP4X_SHM": "0"})     # the TCP ring
     assert all(v == 4 * 3_000_007 for v in res.values())
 
 
@@ -284,8 +285,8 @@ def test_trace_report_counts_calls():
 @pytest.mark.parametrize("p", [2, 3, 4])
 @pytest.mark.parametrize("kind", ["double", "int", "byte"])
 def test_primitive_matrix_shared_memory_engine(p, kind):
-    """Same matrix with the /dev/shm engine (C++ host runtime) forced on for every size."""
-    res, code, _ = run_ranks(p, prim_matrix, (kind, False, 1001), env={"MP4X_SHM_MIN_BYTES": "0"})
+    """Same matrix with the /dev/shm engine (C++ host runtime), the same-host default."""
+    res, code, _ = run_ranks(p, prim_matrix, (kind, False, 1001))
     assert code == 0
 
 

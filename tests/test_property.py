@@ -89,13 +89,13 @@ def random_cases(comm, seed, cases):
 
 @pytest.mark.parametrize("p,seed", [(2, 11), (3, 12), (5, 13), (8, 14)])
 def test_random_collectives_match_numpy(p, seed):
-    res, code, _ = run_ranks(p, random_cases, (seed, 60), timeout=240)
+    res, code, _ = run_ranks(p, random_cases, (seed, 60), timeout=240, env={"MP4X_SHM": "0"})   # TCP mesh
     assert code == 0 and all(v == 60 for v in res.values())
 
 
 @pytest.mark.parametrize("p,seed", [(3, 21), (8, 22)])
 def test_random_collectives_shared_memory(p, seed):
-    res, code, _ = run_ranks(p, random_cases, (seed, 40), timeout=240, env={"MP4X_SHM_MIN_BYTES": "0"})
+    res, code, _ = run_ranks(p, random_cases, (seed, 40), timeout=240)    # /dev/shm: the same-host default
     assert code == 0
 
 
@@ -103,7 +103,7 @@ def test_random_collectives_shared_memory(p, seed):
                                          ("ring", 7, 35)])
 def test_random_collectives_forced_host_allreduce_algo(algo, p, seed):
     """Both host allreduce schedules (ring / recursive halving-doubling with fold) vs NumPy."""
-    res, code, _ = run_ranks(p, random_cases, (seed, 30), timeout=240, env={"MP4X_HOST_ALGO": algo})
+    res, code, _ = run_ranks(p, random_cases, (seed, 30), timeout=240, env={"MP4X_HOST_ALGO": algo, "MP4X_SHM": "0"})
     assert code == 0 and all(v == 30 for v in res.values())
 
 
@@ -117,5 +117,5 @@ def _float_allreduce_digest(comm, n):
 
 @pytest.mark.parametrize("algo,p", [("rhd", 5), ("rhd", 8), ("ring", 5)])
 def test_host_allreduce_bit_identical_across_ranks(algo, p):
-    res, code, _ = run_ranks(p, _float_allreduce_digest, (10_001,), timeout=120, env={"MP4X_HOST_ALGO": algo})
+    res, code, _ = run_ranks(p, _float_allreduce_digest, (10_001,), timeout=120, env={"MP4X_HOST_ALGO": algo, "MP4X_SHM": "0"})
     assert code == 0 and len(set(res.values())) == 1
