@@ -153,8 +153,15 @@ class IpcAllreduce:
             raise Mp4jException("IPC allreduce needs contiguous tensors")
         es = view.element_size()
         total = view.numel() * es
-        if total % 16 or out.data_ptr() % 16:
+        if total % 16:
             raise Mp4jException("IPC allreduce needs 16-byte multiples")
+        if out.data_ptr() % 16:
+            # an oddly offset output on THIS rank must not change the protocol the peers run:
+            # reduce into an aligned temporary (allocator-aligned) and copy out
+            tmp = torch.empty(view.numel(), dtype=view.dtype, device=view.device)
+            self.allreduce(view, op, algo, out=tmp, blocks=blocks, overlap=overlap)
+            out.copy_(tmp)
+            return out
         dt = int(dtype_of_torch(view.dtype))
         if not blocks and self.max_blocks:
             vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
@@ -280,17 +287,27 @@ class IpcAllreduce:
         base, r = froms[0], self.rank
         st = stream_ptr()
         n = (tos[-1] - base) * es
-        if self._fuse_copy and flat[base:].data_ptr() % 16 == 0 and n:
-            # one launch: the kernel stages this rank's range and writes its segment in place
+        if self._fuse_copy and n:
+            # one launch: the kernel stages this rank's range and writes its segment in place.
+            # The path depends on rank-independent facts only (ranges, env); a range that is not
+            # 16-byte aligned on THIS rank goes through an aligned temporary instead.
+            rng = flat[base:tos[-1]]
+            tmp = None
+            if rng.data_ptr() % 16:
+                tmp = torch.empty(n, dtype=torch.uint8, device=view.device)
+                tmp.copy_(rng.view(torch.uint8))
+            b16 = tmp.data_ptr() if tmp is not None else rng.data_ptr()
+            mine_off = (froms[r] - base) * es
             edev = self._next_epoch(st)
             lo_a = (c_int64 * self.p)(*[(f - base) * es // 16 for f in froms])
             hi_a = (c_int64 * self.p)(*[(t - base) * es // 16 for t in tos])
             maxv = max(h - l_ for l_, h in zip(lo_a, hi_a))
             check(self.lib.mp4x_ipc_reduce_scatter_from(int(dtype_of_torch(view.dtype)), int(op.code),
                                                         self._pp_data[0], self._pp_sig[0], r, self.p, lo_a, hi_a,
-                                                        flat[base:].data_ptr(), flat[froms[r]:].data_ptr(),
-                                                        self.epoch, self._grid(maxv), edev, st),
+                                                        b16, b16 + mine_off, self.epoch, self._grid(maxv), edev, st),
                   "mp4x_ipc_reduce_scatter_from")
+            if tmp is not None and tos[r] > froms[r]:
+                flat[froms[r]:tos[r]].view(torch.uint8).copy_(tmp[mine_off:(tos[r] - base) * es])
             return True
         if n:
             check(self.lib.mp4x_memcpy_async(self._data.value, flat[base:].data_ptr(), n, st), "ipc RS staging")
@@ -312,18 +329,26 @@ class IpcAllreduce:
         es = view.element_size()
         flat = view.view(-1)
         base, r = froms[0], self.rank
-        if self._fuse_copy and flat[base:].data_ptr() % 16 == 0 and \
-                (not torch.cuda.is_current_stream_capturing() or self._epoch_dev is not None):
+        if self._fuse_copy and (not torch.cuda.is_current_stream_capturing() or self._epoch_dev is not None):
             # one copy-plan launch: stage the own segment in-kernel, pull every peer's segment
-            # straight into the output (no staging copy, no copy-out)
-            b16 = flat[base:].data_ptr()
+            # straight into the output (no staging copy, no copy-out).  A range that is not
+            # 16-byte aligned on THIS rank runs the same plan on an aligned temporary, so every
+            # rank takes the same protocol.
             lo = [(f - base) * es // 16 for f in froms]
             ln = [(t - f) * es // 16 for f, t in zip(froms, tos)]
             grid = max(ln)
             if grid == 0:
                 return True
+            rng = flat[base:tos[-1]]
+            tmp = None
+            if rng.data_ptr() % 16:
+                tmp = torch.empty(rng.numel() * es, dtype=torch.uint8, device=view.device)
+                tmp.copy_(rng.view(torch.uint8))
+            b16 = tmp.data_ptr() if tmp is not None else rng.data_ptr()
             pulls = [(lo[j], lo[j], ln[j], j) for j in range(self.p) if j != r and ln[j]]
             self._plan([(lo[r], lo[r], ln[r], 0)] if ln[r] else [], pulls, b16, b16, grid)
+            if tmp is not None:
+                rng.view(torch.uint8).copy_(tmp)
             return True
         st = stream_ptr()
         seg = (tos[r] - froms[r]) * es
@@ -357,17 +382,31 @@ class IpcAllreduce:
                                           self._grid(grid_len), edev, st), "mp4x_ipc_copy_plan")
 
     def _vec_ok(self, view: torch.Tensor, bounds) -> bool:
+        """Rank-independent qualification (shape, ranges, capture state).  The tensor's own
+        address is NOT part of it: an oddly offset tensor on one rank goes through
+        :meth:`_aligned` so every rank still runs the same plan."""
         es = view.element_size()
-        if not view.is_contiguous() or view.data_ptr() % 16:
+        if not view.is_contiguous():
             return False
         if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
             return False
         return all((b * es) % 16 == 0 for b in bounds)
 
+    @staticmethod
+    def _aligned(view: torch.Tensor, fn) -> bool:
+        """Run ``fn`` on an allocator-aligned copy of ``view`` and copy the result back."""
+        tmp = torch.empty_like(view, memory_format=torch.contiguous_format)
+        tmp.copy_(view)
+        ok = fn(tmp)
+        view.copy_(tmp)
+        return ok
+
     def broadcast(self, view: torch.Tensor, frm: int, to: int, root: int) -> bool:
         es = view.element_size()
         if to <= frm or (to - frm) * es > self.nbytes or not self._vec_ok(view, (frm, to)):
             return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.broadcast(t, frm, to, root))
         base = view.data_ptr()
         L = (to - frm) * es // 16
         off = frm * es // 16
@@ -384,6 +423,8 @@ class IpcAllreduce:
         if sum(ln for j, ln in enumerate(lens) if j != root) * 16 > self.nbytes or \
                 not self._vec_ok(view, list(froms) + list(tos)):
             return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.scatter(t, froms, tos, root))
         grid = max([ln for j, ln in enumerate(lens) if j != root] or [0])
         if grid == 0:
             return True
@@ -406,6 +447,8 @@ class IpcAllreduce:
         lens = [(t - f) * es // 16 for f, t in zip(froms, tos)]
         if max(lens) * 16 > self.nbytes or not self._vec_ok(view, list(froms) + list(tos)):
             return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.gather(t, froms, tos, root))
         grid = max([ln for j, ln in enumerate(lens) if j != root] or [0])
         if grid == 0:
             return True
@@ -496,7 +539,9 @@ class IpcAllreduce:
     FP8_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 
     def fp8_ok(self, view: torch.Tensor) -> bool:
-        return view.dtype in self.FP8_DTYPES and view.is_contiguous() and view.data_ptr() % 16 == 0 \
+        """Rank-independent qualification (dtype, shape); an oddly offset tensor on one rank is
+        handled inside :meth:`allreduce_fp8` so every rank runs the same kernels."""
+        return view.dtype in self.FP8_DTYPES and view.is_contiguous() \
             and view.numel() % 4 == 0 and view.numel() > 0
 
     def _fp8_piece_blocks(self) -> int:
@@ -516,7 +561,10 @@ class IpcAllreduce:
         as the RCCL fp8 schedule (two quantisations, f32 accumulation in rank order).  Needs
         :meth:`fp8_ok`."""
         if not self.fp8_ok(view):
-            raise Mp4jException("fp8 IPC allreduce needs a contiguous 16-byte aligned f32/bf16/f16 tensor, n % 4 == 0")
+            raise Mp4jException("fp8 IPC allreduce needs a contiguous f32/bf16/f16 tensor, n % 4 == 0")
+        if view.data_ptr() % 16:
+            self._aligned(view, self.allreduce_fp8)
+            return view
         Q = self.QBLOCK
         n = view.numel()
         es = view.element_size()

@@ -158,3 +158,86 @@ def test_engine_routes_small_bcast_scatter_gather_reduce_through_ipc():
         assert ok, r
         for k in ("broadcast.ipc", "scatter.ipc", "gather.ipc", "reduce.ipc1"):
             assert stats.get(k) == 1, (r, stats)
+
+
+def _misaligned_worker(port, q):
+    """Rank 0 passes tensors that start 4 bytes past a 16-byte boundary, rank 1 aligned ones:
+    every IPC collective must still run the SAME protocol on both ranks (aligned temporaries on
+    rank 0) — a rank-dependent decline would leave the peer spinning in a barrier."""
+    try:
+        import torch
+        from mp4x import CommUtils, Operators, ProcessCommSlave
+        from mp4x.parallel.ipc import IpcAllreduce, TWOSHOT
+        torch.cuda.set_device(0)
+        comm = ProcessCommSlave("t", "127.0.0.1", port, heartbeat=False)
+        r, p = comm.getRank(), comm.getSlaveNum()
+        ipc = IpcAllreduce(comm, nbytes=1 << 20)
+        n = 4096
+        shift = 1 if r == 0 else 0
+
+        def mk(fill):
+            big = torch.empty(n + 4, device="cuda")
+            v = big[shift:shift + n]
+            v.copy_(fill)
+            return v
+        res = []
+        base = torch.arange(n, device="cuda", dtype=torch.float32)
+        x = mk(base + r)
+        ipc.allreduce(x, Operators.Float.SUM, algo=TWOSHOT)
+        res.append(("allreduce", bool(torch.equal(x, base * p + sum(range(p))))))
+        froms, tos, _ = CommUtils.even_split(0, n, p)
+        x = mk(base + r)
+        ok = ipc.reduce_scatter(x, froms, tos, Operators.Float.SUM)
+        res.append(("rs", ok and bool(torch.equal(x[froms[r]:tos[r]], (base * p + sum(range(p)))[froms[r]:tos[r]]))))
+        x = mk(torch.full((n,), -1.0, device="cuda"))
+        x[froms[r]:tos[r]] = r
+        ok = ipc.allgather(x, froms, tos)
+        res.append(("ag", ok and all(bool(torch.all(x[froms[j]:tos[j]] == j)) for j in range(p))))
+        x = mk(base if r == 1 else torch.zeros(n, device="cuda"))
+        ok = ipc.broadcast(x, 0, n, 1)
+        res.append(("bcast", ok and bool(torch.equal(x, base))))
+        x = mk(torch.full((n,), float(r), device="cuda"))
+        ok = ipc.gather(x, froms, tos, 1)
+        res.append(("gather", ok and (r != 1 or all(bool(torch.all(x[froms[j]:tos[j]] == j)) for j in range(p)))))
+        x = mk(torch.full((n,), 0.0, device="cuda"))
+        if r == 0:
+            for j in range(p):
+                x[froms[j]:tos[j]] = j + 10
+        ok = ipc.scatter(x, froms, tos, 0)
+        res.append(("scatter", ok and bool(torch.all(x[froms[r]:tos[r]] == r + 10))))
+        x = mk(torch.ones(n, device="cuda"))
+        ipc.allreduce_fp8(x)
+        res.append(("fp8", bool(torch.allclose(x, torch.full_like(x, float(p)), rtol=2 ** -3))))
+        torch.cuda.synchronize()
+        res.append(("error_word", ipc.error_word() == 0))
+        comm.barrier()
+        ipc.close()
+        comm.close(0)
+        q.put((r, "ok", res))
+    except BaseException:
+        q.put((-1, "err", traceback.format_exc()))
+
+
+def test_misaligned_tensor_on_one_rank_keeps_protocols_in_step():
+    from mp4x import CommMaster
+    m = CommMaster(2, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_misaligned_worker, args=(m.port, q)) for _ in range(2)]
+    for pr in procs:
+        pr.start()
+    res = {}
+    try:
+        for _ in range(2):
+            r, st, val = q.get(timeout=240)
+            assert st == "ok", val
+            res[r] = val
+    finally:
+        for pr in procs:
+            pr.join(timeout=30)
+            if pr.is_alive():
+                pr.kill()
+        m.stop(timeout=5)
+    for r, rows in res.items():
+        for name, good in rows:
+            assert good, (r, name)
