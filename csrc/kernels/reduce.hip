@@ -97,8 +97,13 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tile(void* __restrict__ out_,
   using S = typename E::S;
   using A = typename E::A;
   constexpr int W = 16 / sizeof(S);
-  const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
   u32x4* out = reinterpret_cast<u32x4*>(out_);
+  // grid-stride over tiles when the launch caps the grid (MP4X_K1_GRID).  Default: no cap, one
+  // tile per block — a capped grid measured no better for NIN = 1-2 and 20% slower for NIN >= 4
+  // (profiles/r1/k1_grid_cap.txt), although a bare copy kernel gains 4% from it
+  // (tools/exp/copy_variants.hip, profiles/r1/copy_variants.txt)
+  const int64_t step = (int64_t)gridDim.x * kBlock * U;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x; base < nvec; base += step) {
   if (base + (int64_t)(U - 1) * kBlock < nvec) {
     u32x4 r[U][NIN];
 #pragma unroll
@@ -146,6 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tile(void* __restrict__ out_,
       out[v] = o;
     }
   }
+  }
   // scalar tail handled by block 0
   if (blockIdx.x == 0) {
     const int64_t tb = nvec * W;
@@ -156,6 +162,15 @@ __global__ __launch_bounds__(kBlock) void k_reduce_tile(void* __restrict__ out_,
       reinterpret_cast<S*>(out_)[i] = E::store(acc);
     }
   }
+}
+
+static int64_t g_k1_grid = -1;
+static int64_t k1_grid_cap() {
+  if (g_k1_grid < 0) {
+    const char* e = getenv("MP4X_K1_GRID");
+    g_k1_grid = e ? atoll(e) : 0;      // 0: one tile per block (no cap)
+  }
+  return g_k1_grid;
 }
 
 static int g_k1_variant = -1;
@@ -207,6 +222,8 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
       int64_t per_block = (int64_t)kBlock * u;
       int64_t g = (nvec + per_block - 1) / per_block;
       if (g < 1) g = 1;
+      const int64_t cap = k1_grid_cap();
+      if (cap > 0 && g > cap) g = cap;
       if (var == 1)
         hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, false>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
       else if (var == 3)
@@ -346,6 +363,7 @@ extern "C" int mp4x_scale(int dtype, void* out, const void* in, double scale, in
 
 // A/B hook for the kernel-variant sweep (tools/bench_kernels.py --variants).
 extern "C" void mp4x_set_k1_variant(int v) { g_k1_variant = v; }
+extern "C" void mp4x_set_k1_grid(int64_t cap) { g_k1_grid = cap; }
 
 extern "C" const char* mp4x_version(void) { return "mp4x-native 0.1 gfx950"; }
 

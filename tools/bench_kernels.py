@@ -53,16 +53,18 @@ def main():
         names = {0: "gridstride_u2", 1: "tile", 2: "tile_nt", 3: "tile_nt_u2x"}
         rounds = {}
         for rnd in range(3):
-            for v in (2, 3):
+            for v, cap in ((2, 0), (2, 4096), (2, 8192), (2, 16384), (3, 8192)):
                 lib.mp4x_set_k1_variant(v)
+                lib.mp4x_set_k1_grid(cap)
                 for nin in (1, 2, 4, 8):
                     ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
-                    rounds.setdefault(f"k1_{names[v]}_nin{nin}", []).append((nin + 1) * n * 4 / ms / 1e6)
+                    rounds.setdefault(f"k1_{names[v]}_grid{cap}_nin{nin}", []).append((nin + 1) * n * 4 / ms / 1e6)
                 ms = timeit(lambda: torch.add(xs[0], xs[1], out=out), a.iters)
                 rounds.setdefault("torch_add", []).append(3 * n * 4 / ms / 1e6)
         for k, v in rounds.items():
             print(f"{k:28s} GB/s median {sorted(v)[1]:.0f}  all {[round(x) for x in v]}")
         lib.mp4x_set_k1_variant(2)
+        lib.mp4x_set_k1_grid(0)
         return
     for nin in ([2, 8] if a.quick else [1, 2, 4, 8]):
         ms = timeit(lambda: K.reduce_(out, xs[:nin], int(OpCode.SUM)), a.iters)
