@@ -83,15 +83,30 @@ class IpcAllreduce:
         hs = self.lib.mp4x_ipc_handle_size()
         self._data = c_void_p()
         self._sig = c_void_p()
-        check(self.lib.mp4x_ipc_alloc(self.nbytes, ctypes.byref(self._data)), "ipc_alloc(data)")
-        check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)), "ipc_alloc(sig)")
-        hd = ctypes.create_string_buffer(hs)
-        hsg = ctypes.create_string_buffer(hs)
-        check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
-        check(self.lib.mp4x_ipc_get_handle(self._sig, hsg), "ipc_get_handle(sig)")
-        pci = ctypes.create_string_buffer(64)
-        check(self.lib.mp4x_device_pci_id(pci, 64), "device_pci_id")
-        allh = comm.server.call("allgather_obj", self.rank, hd.raw + hsg.raw + pci.value)
+        self._opened: List[c_void_p] = []
+        # a local failure here (out of memory, no IPC support) must still reach the allgather
+        # below: raising before it would leave the peers waiting there for this rank
+        local_err = None
+        try:
+            check(self.lib.mp4x_ipc_alloc(self.nbytes, ctypes.byref(self._data)), "ipc_alloc(data)")
+            check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)),
+                  "ipc_alloc(sig)")
+            hd = ctypes.create_string_buffer(hs)
+            hsg = ctypes.create_string_buffer(hs)
+            check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
+            check(self.lib.mp4x_ipc_get_handle(self._sig, hsg), "ipc_get_handle(sig)")
+            pci = ctypes.create_string_buffer(64)
+            check(self.lib.mp4x_device_pci_id(pci, 64), "device_pci_id")
+            blob = hd.raw + hsg.raw + pci.value
+        except Exception as e:
+            local_err = str(e)
+            blob = b"ERR:" + local_err.encode()
+        allh = comm.server.call("allgather_obj", self.rank, blob)
+        failed = [(i, bytes(b)[4:].decode(errors="replace")) for i, b in enumerate(allh)
+                  if bytes(b).startswith(b"ERR:")]
+        if failed:
+            self.close(sync=False)
+            raise Mp4jException(f"IPC buffer setup failed on ranks {failed}")
         ids = [bytes(b[2 * hs:]) for b in allh]
         share = max(ids.count(i) for i in ids)
         # ranks on one device (rehearsal): cap the grid so all ranks' blocks fit at once
@@ -99,7 +114,6 @@ class IpcAllreduce:
         self.shared_gpu = share > 1
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
-        self._opened: List[c_void_p] = []
         err = None
         try:
             for r, blob in enumerate(allh):
