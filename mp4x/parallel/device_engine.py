@@ -142,6 +142,7 @@ class DeviceEngine:
         self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
         self._ipc_obj = None
         self._ipc_large = None
+        self._ipc_large_failed = False   # set on every rank together (setup failure is collective)
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
@@ -274,13 +275,14 @@ class DeviceEngine:
         """Second IPC instance with a large buffer (``MP4X_IPC_LARGE_BYTES``, default 256 MiB)
         for messages above the two-shot tier, when autotuning (or ``MP4X_DEVICE_ALGO=ipc2``)
         routes them to IPC.  Collective, lazily created."""
-        if self._ipc_large is None and self.ipc() is not None:
+        if self._ipc_large is None and not self._ipc_large_failed and self.ipc() is not None:
             try:
                 from .ipc import IpcAllreduce
                 self._ipc_large = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
                                                tag="large")
             except Exception as e:
                 LOG.warning("large-message IPC allreduce disabled: %s", e)
+                self._ipc_large_failed = True
                 return self._ipc_obj
         return self._ipc_large or self._ipc_obj
 
