@@ -14,10 +14,18 @@ barrier + device sync, K timed calls with a hipEvent pair around each (p50 / p99
 barrier + sync; MAX over ranks.
 
 busbw follows the nccl-tests convention used in BASELINE.md: algbw = bytes / t,
-busbw = algbw * 2(p-1)/p.  ``value`` is the whole-job aggregate ``N * busbw``.
+busbw = algbw * 2(p-1)/p, and ``value`` IS that busbw (per rank, the BASELINE metric; the
+whole-job sum ``N * busbw`` is reported separately as ``aggregate_busbw_gbps``).
 With one rank nothing crosses a link (factor 2(p-1)/p = 0) and the in-place call is a
 no-op by the reference's contract, so N=1 times the OUT-OF-PLACE form of the same call
-(``out=``; a 1 GB device copy) and reports busbw := algbw for it.
+(``out=``; a 1 GB device copy through the K1 kernel) and reports algbw for it — HBM
+evidence, not an allreduce number.
+
+For N>1 the buffer is registered with the communicator (``registerBuffer``, collective), so
+the zero-copy two-shot can run straight on the peers' tensors; the autotune times it next to
+RCCL and the staged kernels (bounded per candidate, ``MP4X_AUTOTUNE_CAP_S``) and only ever
+pins a schedule that was exact on every rank; if every custom schedule fails, RCCL stays.
+Before any IPC tier is used, a collective self-test of the IPC mesh runs (``ipc_selftest``).
 """
 import argparse
 import json
@@ -57,6 +65,8 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="dry run of the launch/rendezvous path on CPU (gloo)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip the warm-up schedule autotune (RCCL vs IPC two-shot vs a2a) for N>1")
+    ap.add_argument("--no-register", action="store_true",
+                    help="do not register the buffer for the zero-copy IPC two-shot")
     args = ap.parse_args()
     if args.algo:
         os.environ["MP4X_DEVICE_ALGO"] = args.algo
@@ -103,8 +113,11 @@ def main():
             torch.cuda.synchronize()
 
     tuned = None
+    registered = False
     if p > 1 and not args.cpu:
         comm.device  # bring up the RCCL communicator before timing
+        if not args.no_register:
+            registered = comm.registerBuffer(buf)   # collective; False on every rank alike
         if not (args.no_autotune or args.algo or args.codec):
             # untimed: measure every applicable schedule on a scratch tensor of this shape and
             # pin the fastest (all ranks agree: MAX over ranks); the timed steps run it in full
@@ -144,10 +157,14 @@ def main():
     ref = REF_BUSBW_MBPS.get(p)
     algo = "k1_copy (out-of-place, 1 rank)" if p == 1 else ("host-tcp" if args.cpu else
                                   comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand))
+    if algo == "ipc2" and registered and not args.cpu and not comm.device._select_tuned:
+        algo = "ipc2z"
+    selftest = None if (p == 1 or args.cpu) else comm.device.ipc_selftest
+    stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items() if k.startswith("allreduce")}
     if rank == 0:
         rec = {
             "metric": METRIC,
-            "value": round(busbw * p, 3),
+            "value": round(busbw, 3),
             "unit": "GB/s",
             "n_gpus": p,
             "steps": args.steps,
@@ -158,11 +175,13 @@ def main():
             "vs_baseline": round(busbw / (ref / 1e3), 2) if ref else None,
             "dtype": "fp32",
             "data": "synthetic (torch.randn per rank)",
-            "config": {"model": f"allreduceArray float[{n}] ({nbytes:.0e} bytes), Operators.Float.SUM",
+            "config": {"model": f"allreduceArray float[{n}] ({nbytes / 1e9:g} GB), Operators.Float.SUM",
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
-                       "payload_bytes": nbytes, "algo": algo,
-                       "in_place": p > 1, "autotune_ms": tuned},
+                       "payload_bytes": nbytes, "algo": algo, "registered": registered,
+                       "in_place": p > 1, "autotune_ms": tuned, "ipc_selftest": selftest,
+                       "calls": stats},
             "busbw_gbps_per_rank": round(busbw, 3),
+            "aggregate_busbw_gbps": round(busbw * p, 3),
             "algbw_gbps": round(algbw, 3),
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
@@ -170,7 +189,8 @@ def main():
             "note": ("p=1: nothing crosses a link (nccl-tests busbw factor 2(p-1)/p = 0), so this is "
                      "busbw := algbw of the out-of-place single-rank allreduce, a 1 GB HBM copy through K1; "
                      "N>=2 values are xGMI-link-bound and not comparable to N=1 as a scaling base"
-                     if p == 1 else "busbw = algbw * 2(p-1)/p; value = p * busbw"),
+                     if p == 1 else "value = busbw = algbw * 2(p-1)/p (nccl-tests convention, per rank); "
+                                    "aggregate_busbw_gbps = p * busbw"),
         }
         print(json.dumps(rec), flush=True)
     comm.close(0)

@@ -34,13 +34,25 @@ namespace mp4x {
 constexpr int kIpcMaxRanks = 8;
 constexpr int kIpcMaxBlocks = 256;
 constexpr int kIpcThreads = 512;
+// Epoch tag of the zero-copy protocol (peers' registered tensors instead of the staging
+// buffers).  Host epochs live in the low 31 bits; a rank that runs the staged protocol while a
+// peer runs the zero-copy one sees the other tag in its flag slot and fails at once instead of
+// reading the wrong buffers (registration is collective, but the choice is made per rank).
+constexpr uint32_t kZcTag = 0x80000000u;
 
 struct alignas(128) Signal {
   uint32_t start[kIpcMaxBlocks][kIpcMaxRanks];
   uint32_t mid[kIpcMaxBlocks][kIpcMaxRanks];
   uint32_t end[kIpcMaxBlocks][kIpcMaxRanks];
   uint32_t error;
+  // host-visible copy of `error`: device address of a pinned, mapped host word (0 = none), set
+  // once at setup (mp4x_ipc_set_host_error); written on a barrier timeout so the host can fail
+  // the NEXT call without any device synchronisation.  Only the owning rank reads this field.
+  uint64_t host_err;
 };
+
+// Spin bound of every barrier wait, in s_memrealtime ticks (100 MHz); mp4x_ipc_set_spin.
+__device__ uint64_t g_ipc_spin_ticks = 1000000000ull;   // 10 s
 
 struct IpcPtrs {
   const void* data[kIpcMaxRanks];   // every rank's data buffer (own one included)
@@ -66,10 +78,17 @@ __device__ __forceinline__ bool block_barrier(uint32_t (*slots)[kIpcMaxRanks] /*
     uint32_t* mine = which == 0 ? &self->start[blockIdx.x][t]
                    : which == 1 ? &self->mid[blockIdx.x][t] : &self->end[blockIdx.x][t];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
+    const uint64_t spin = g_ipc_spin_ticks;
+    uint32_t seen;
+    while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
       __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 1000000000ull) {   // 10 s at 100 MHz
-        __hip_atomic_store(&self->error, 1u + (uint32_t)which, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const bool other_protocol = seen == (epoch ^ kZcTag);
+      if (other_protocol || __builtin_amdgcn_s_memrealtime() - t0 > spin) {
+        const uint32_t code = other_protocol ? 4u : 1u + (uint32_t)which;
+        __hip_atomic_store(&self->error, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        uint32_t* host = reinterpret_cast<uint32_t*>(
+            __hip_atomic_load(&self->host_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        if (host) __hip_atomic_store(host, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         s_fail = 1;
         break;
       }
@@ -115,11 +134,13 @@ __device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v) {
 __device__ __forceinline__ uint32_t resolve_epoch(uint32_t epoch, const uint32_t* epoch_dev) {
   // graph mode: the epoch lives in device memory and is bumped by k_ipc_bump_epoch, the
   // preceding node of the same graph, so every replay gets a fresh, rank-consistent epoch
-  return epoch_dev ? __hip_atomic_load(epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : epoch;
+  // (the protocol tag of a host-passed epoch is kept in graph mode too)
+  return epoch_dev ? (__hip_atomic_load(epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (epoch & kZcTag))
+                   : epoch;
 }
 
 __global__ void k_ipc_bump_epoch(uint32_t* epoch_dev) {
-  uint32_t e = *epoch_dev + 1;
+  uint32_t e = (*epoch_dev + 1) & ~kZcTag;
   *epoch_dev = e ? e : 1;
 }
 
@@ -169,10 +190,12 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
   {
     const int64_t b = (int64_t)rank * chunk;
     const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+    // zero-copy form: `out` IS this rank's registered buffer (== mine), one store per vector
+    const bool zc = out == mine;
     for (int64_t v = b + off0; v < e; v += stride) {
       u32x4 o = reduce_vec<DT, OP, NR>(P, v);
       mine[v] = o;
-      out[v] = o;
+      if (!zc) out[v] = o;
     }
   }
   if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
@@ -461,6 +484,32 @@ extern "C" int mp4x_ipc_alloc(size_t bytes, void** ptr) {
 
 extern "C" int mp4x_ipc_free(void* ptr) { return (int)hipFree(ptr); }
 
+// Pinned host word the kernels can write (mapped, coherent): *host_ptr for the CPU,
+// *dev_ptr for the kernels.  Zeroed.
+extern "C" int mp4x_host_word_alloc(void** host_ptr, void** dev_ptr) {
+  hipError_t e = hipHostMalloc(host_ptr, 64, hipHostMallocMapped | hipHostMallocCoherent);
+  if (e != hipSuccess) return (int)e;
+  __builtin_memset(*host_ptr, 0, 64);
+  return (int)hipHostGetDevicePointer(dev_ptr, *host_ptr, 0);
+}
+
+extern "C" int mp4x_host_word_free(void* host_ptr) { return (int)hipHostFree(host_ptr); }
+
+// Register the host-visible error word of a signal block (device address from
+// mp4x_host_word_alloc; nullptr to detach).
+extern "C" int mp4x_ipc_set_host_error(void* signal, void* dev_word) {
+  const uint64_t v = (uint64_t)(uintptr_t)dev_word;
+  hipError_t e = hipMemcpy((char*)signal + offsetof(Signal, host_err), &v, sizeof(v), hipMemcpyHostToDevice);
+  return (int)e;
+}
+
+// Barrier spin bound for every IPC kernel launched afterwards (process-wide), in seconds.
+extern "C" int mp4x_ipc_set_spin(double seconds) {
+  if (!(seconds > 0.0)) return MP4X_E_BADARG;
+  const uint64_t ticks = (uint64_t)(seconds * 1.0e8);
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_ipc_spin_ticks), &ticks, sizeof(ticks), 0, hipMemcpyHostToDevice);
+}
+
 // PCI bus id of the current device: ranks compare them to detect a GPU shared by several
 // ranks (single-GPU rehearsal), where the per-block barriers need every rank's blocks
 // co-resident and the block count must shrink accordingly.
@@ -472,6 +521,17 @@ extern "C" int mp4x_device_pci_id(char* buf, int len) {
 }
 
 extern "C" int mp4x_ipc_handle_size(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Base and size of the allocation that contains `ptr` (IPC handles name whole allocations:
+// a caller tensor inside a caching-allocator segment is exported as (segment handle, offset)).
+extern "C" int mp4x_mem_range(void* ptr, void** base, size_t* size) {
+  hipDeviceptr_t b = nullptr;
+  size_t sz = 0;
+  hipError_t e = hipMemGetAddressRange(&b, &sz, (hipDeviceptr_t)ptr);
+  *base = (void*)b;
+  *size = sz;
+  return (int)e;
+}
 
 extern "C" int mp4x_ipc_get_handle(void* ptr, void* handle_out) {
   return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle_out), ptr);

@@ -146,16 +146,43 @@ class DeviceEngine:
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
-        tune_file = os.environ.get("MP4X_TUNE_FILE")
-        if tune_file and os.path.exists(tune_file):
-            try:
-                n = self.load_tuning(tune_file)
-                LOG.info("rank %d: %d pinned schedules from %s", self.rank, n, tune_file)
-            except Exception as e:   # noqa: BLE001 — a stale or foreign table is ignored, not fatal
-                LOG.warning("ignoring tuning table %s: %s", tune_file, e)
+        self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
+        self._select_tuned = False
+        self._load_shared_tuning(shared=coll is None)
         # fail-stop detector for hung / failed collectives (parallel/watchdog.py)
         from . import watchdog
         self.watchdog = watchdog.CollectiveWatchdog(self) if coll is None and watchdog.enabled() else None
+
+    def _load_shared_tuning(self, shared: bool = True) -> None:
+        """``MP4X_TUNE_FILE``: rank 0 reads the table and every rank pins RANK 0's copy (shared
+        through the control plane).  A file present on one host only, or unreadable on one rank,
+        can then never make ranks pin different schedules for the same call (which would pair
+        mismatched collectives and hang).  Collective when more than one rank."""
+        table, err = None, None
+        path = os.environ.get("MP4X_TUNE_FILE")
+        if (self.rank == 0 or not shared) and path and os.path.exists(path):
+            try:
+                import json
+                with open(path) as f:
+                    table = json.load(f)
+            except Exception as e:   # noqa: BLE001 — a broken table is ignored, not fatal
+                err = str(e)
+        if self.p > 1 and shared:      # (injected loopback ranks share one process and file)
+            try:
+                table = self.all_gather_object(table)[0]
+            except Exception as e:   # noqa: BLE001
+                LOG.warning("tuning table not shared (%s): none pinned", e)
+                return
+        if err:
+            LOG.warning("ignoring tuning table %s: %s", path, err)
+        if table is None:
+            return
+        try:
+            n = self.load_tuning(table)
+            LOG.info("rank %d: %d pinned schedules from rank 0's %s", self.rank, n, path)
+        except Exception as e:   # noqa: BLE001 — a foreign table is refused identically on every rank
+            self._tuned.clear()
+            LOG.warning("ignoring tuning table %s: %s", path, e)
 
     # ------------------------------------------------------------------ bootstrap
     def _init_pg(self):
@@ -244,15 +271,145 @@ class DeviceEngine:
         return op.code in _RCCL_OPS and dtype in _RCCL_DTYPES
 
     def ipc(self):
-        """Lazily set up the IPC peer mappings (collective: every rank reaches this together)."""
+        """Lazily set up the IPC peer mappings (collective: every rank reaches this together).
+
+        A new mesh runs :meth:`_ipc_self_test` before any IPC tier is used: on first contact with
+        a topology whose peer mappings misbehave, every rank disables IPC together (logged) and
+        the job runs on RCCL instead of returning wrong sums."""
         if self._ipc_obj is None and self.ipc_enabled:
             try:
                 from .ipc import IpcAllreduce
-                self._ipc_obj = IpcAllreduce(self.comm)
+                inst = IpcAllreduce(self.comm)
             except Exception as e:
                 LOG.warning("IPC allreduce disabled: %s", e)
                 self.ipc_enabled = False
+                return None
+            bad = self._ipc_self_test(inst)
+            if bad:
+                LOG.warning("rank %d: IPC self-test failed (%s): IPC tiers disabled on every rank, RCCL used",
+                            self.rank, bad)
+                try:
+                    inst.close()
+                except Exception:   # noqa: BLE001
+                    pass
+                self.ipc_enabled = False
+                self.ipc_selftest = {"ok": False, "failures": bad}
+                return None
+            self._ipc_obj = inst
         return self._ipc_obj
+
+    ipc_selftest: Optional[dict] = None
+
+    def _ipc_self_test(self, inst) -> Optional[list]:
+        """Collective exact-pattern test of every IPC kernel family on the fresh mesh (f32 SUM):
+        one-shot 64 KiB, two-shot 64 KiB and 4 MiB, direct reduce-scatter / all-gather 4 MiB, a
+        copy-plan broadcast, and the zero-copy two-shot on a registered 4 MiB tensor.  Short
+        barrier spin bound (``MP4X_IPC_SELFTEST_SPIN_S``, 2 s) while it runs.  The verdict is the
+        union of every rank's failures (agreed through the control plane, not through the
+        transport under test).  Returns None when everything was exact on every rank."""
+        if os.environ.get("MP4X_IPC_SELFTEST", "1") == "0":
+            return None
+        from . import ipc as ipcm
+        from ..operators import Operators
+        t0 = time.perf_counter()
+        lib = inst.lib
+        fails = []
+        try:
+            ipcm.check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2"))), "set_spin")
+        except Exception as e:   # noqa: BLE001
+            fails.append(f"set_spin: {e}")
+        dev = self.device
+        p, r = self.p, self.rank
+        op = for_dtype(Operators.Float.SUM, DType.F32)
+        cap = inst.nbytes // 4
+
+        def pattern(n):
+            t = torch.empty(n, dtype=torch.float32, device=dev)
+            exp = self._fill_probe(t, op)
+            return t, exp
+
+        def step(name, fn):
+            try:
+                bad = fn()
+                torch.cuda.synchronize(dev)
+                code = inst.host_error()
+                inst.raise_if_failed()
+                nbad = 0 if code else bad()
+                if code:
+                    fails.append(f"{name}: barrier timeout {code}")
+                elif nbad:
+                    fails.append(f"{name}: {nbad} wrong elements")
+            except Exception as e:   # noqa: BLE001
+                fails.append(f"{name}: {type(e).__name__}: {e}")
+                try:
+                    torch.cuda.synchronize(dev)
+                    inst.raise_if_failed()
+                except Exception:   # noqa: BLE001
+                    pass
+
+        def allreduce_case(n, algo):
+            def fn():
+                t, exp = pattern(n)
+                inst.allreduce(t, op, algo=algo)
+                return lambda: int((t != exp).sum())
+            return fn
+
+        n64k, n4m = min(cap, 16 << 10), min(cap, 1 << 20)
+        step("oneshot_64KiB", allreduce_case(n64k, ipcm.ONESHOT))
+        step("twoshot_64KiB", allreduce_case(n64k, ipcm.TWOSHOT))
+        step("twoshot_4MiB", allreduce_case(n4m, ipcm.TWOSHOT))
+
+        froms, tos, _ = CommUtils.even_split(0, n4m, p)
+        a16 = all((f * 4) % 16 == 0 for f in froms + tos)
+
+        def rs():
+            t, exp = pattern(n4m)
+            if not inst.reduce_scatter(t, froms, tos, op):
+                return lambda: 0
+            return lambda: int((t[froms[r]:tos[r]] != exp[froms[r]:tos[r]]).sum())
+
+        def ag():
+            t = torch.full((n4m,), -1.0, device=dev)
+            exp = torch.arange(n4m, device=dev, dtype=torch.float32).remainder_(251)
+            t[froms[r]:tos[r]] = exp[froms[r]:tos[r]]
+            if not inst.allgather(t, froms, tos):
+                return lambda: 0
+            return lambda: int((t != exp).sum())
+
+        def bcast():
+            n = min(cap, 1 << 18)
+            exp = torch.arange(n, device=dev, dtype=torch.float32).remainder_(113)
+            t = exp.clone() if r == p - 1 else torch.zeros(n, device=dev)
+            if not inst.broadcast(t, 0, n, p - 1):
+                return lambda: 0
+            return lambda: int((t != exp).sum())
+
+        if a16:
+            step("reduce_scatter_4MiB", rs)
+            step("allgather_4MiB", ag)
+        step("broadcast_1MiB", bcast)
+        if self._zc:
+            t, exp = pattern(n4m)
+            if inst.register(t):
+                def zc():
+                    inst.allreduce_registered(t, op, inst.registered(t))
+                    return lambda: int((t != exp).sum())
+                step("zero_copy_twoshot_4MiB", zc)
+                inst.deregister(t)
+            else:
+                fails.append("register: refused")
+        try:
+            ipcm.check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SPIN_S", "10"))), "set_spin")
+        except Exception as e:   # noqa: BLE001
+            fails.append(f"set_spin: {e}")
+        if os.environ.get("MP4X_IPC_SELFTEST_INJECT", "").strip() == str(r):   # failure-path tests
+            fails.append("injected failure (MP4X_IPC_SELFTEST_INJECT)")
+        allf = self.comm.server.call("allgather_obj", self.rank, fails)
+        bad = [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
+        self.ipc_selftest = {"ok": not bad, "failures": bad, "seconds": round(time.perf_counter() - t0, 3)}
+        if not bad:
+            LOG.info("rank %d: IPC self-test passed in %.3f s", self.rank, self.ipc_selftest["seconds"])
+        return bad or None
 
     RCCL_CTA_VARIANTS = (64, 112)
 
@@ -280,6 +437,8 @@ class DeviceEngine:
                 from .ipc import IpcAllreduce
                 self._ipc_large = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
                                                tag="large")
+                if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
+                    self._ipc_large.prepare_graph()   # a capture is being prepared: same epoch mode
             except Exception as e:
                 LOG.warning("large-message IPC allreduce disabled: %s", e)
                 self._ipc_large_failed = True
@@ -308,13 +467,15 @@ class DeviceEngine:
         if kind == "allreduce" and op is not None and not getattr(op, "is_custom", False) and \
                 (codec == "zs" or (codec is None and getattr(operand, "compress", False))):
             return "zs"       # lossless wire compression (the reference's compress=true contract)
-        if forced in ("ipc1", "ipc2", "ipc2p") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
+        if forced in ("ipc1", "ipc2", "ipc2p", "ipc2z") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             return forced
         if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
             return forced     # (custom operators may be non-commutative: rank-ordered a2a only)
+        self._select_tuned = False
         if kind == "allreduce" and op is not None and forced in ("", "auto") and self._tuned:
             t = self._tuned.get(_tune_key(dtype, op, nbytes))
             if t is not None and self._algo_valid(t, op, dtype, nbytes):
+                self._select_tuned = True
                 return t
         if op is not None and not self.rccl_ok(op, dtype):
             return "a2a"
@@ -333,7 +494,7 @@ class DeviceEngine:
         return "rccl"
 
     # ------------------------------------------------------------------ hipGraph capture
-    _CAPTURABLE = ("rccl", "ipc1", "ipc2", "a2a", "rhd", "fp8", "bf16")
+    _CAPTURABLE = ("rccl", "ipc1", "ipc2", "ipc2z", "a2a", "rhd", "fp8", "bf16")
 
     def capture(self, fn, warmup: int = 2):
         """Capture ``fn()`` — a fixed sequence of device collectives on fixed tensors, e.g. a DDP
@@ -356,6 +517,10 @@ class DeviceEngine:
                 fn()
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._sync()
+        # the warm-up may have created the large-message instance: it needs device epochs too
+        for inst in (self._ipc_obj, self._ipc_large):
+            if inst is not None:
+                inst.prepare_graph()
         self.barrier()
         g = torch.cuda.CUDAGraph()
         wd = self.watchdog
@@ -377,9 +542,17 @@ class DeviceEngine:
         reduce_into(out, ins, op)
 
     # ================================================================== allreduce
-    def allreduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand=None, small: bool = False):
+    def allreduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand=None, small: bool = False,
+                  out: Optional[torch.Tensor] = None):
+        """In-place allreduce of ``arr[frm:to]``; with ``out`` the result goes to ``out[frm:to]``
+        and ``arr`` is left untouched (the staged IPC kernels write ``out`` directly; other
+        schedules copy into ``out`` first and run in place there)."""
         flat = self._flat(arr)
         view = flat[frm:to]
+        if out is not None:
+            oview = self._flat(out)[frm:to]
+            if view.numel() == 0:
+                return out
         if view.numel() == 0:
             return arr
         op = self._op(operator, view)
@@ -387,13 +560,56 @@ class DeviceEngine:
         if algo not in self._CAPTURABLE and view.is_cuda and torch.cuda.is_current_stream_capturing():
             # host-synchronising schedule inside a hipGraph capture: use a capturable twin
             algo = "ipc2" if algo == "ipc2p" else ("rccl" if self.rccl_ok(op, view.dtype) else "a2a")
+        if out is not None:
+            if algo in ("ipc1", "ipc2") and self.ipc() is not None and \
+                    view.numel() * view.element_size() <= self.ipc_twoshot_max and \
+                    (not torch.cuda.is_current_stream_capturing() or self._ipc_obj._epoch_dev is not None):
+                from .ipc import ONESHOT, TWOSHOT
+                self._count("allreduce." + algo + ".out")
+                self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT, out=oview)
+                return out
+            if view.is_cuda:   # the local copy runs through the K1 kernel (NIN = 1)
+                from ..ops.device_ops import reduce_
+                reduce_(oview, [view], int(OpCode.SUM))
+            else:
+                oview.copy_(view)
+            view, arr = oview, out
+        if algo == "ipc2" and not self._select_tuned and self._zc and self._ipc_obj is not None \
+                and self._ipc_obj.registered(view) is not None:
+            algo = "ipc2z"      # registered on this rank (registration is collective): zero-copy
         self._count("allreduce." + algo)
         self._run_allreduce(algo, view, op)
         return arr
 
+    # ------------------------------------------------------------------ registered buffers
+    def register_buffer(self, t: torch.Tensor) -> bool:
+        """Collective: map ``t`` into every peer for the zero-copy two-shot allreduce (no staging
+        copy, no pieces, any size).  Every rank registers its same-shaped tensor at the same
+        point and keeps it (and its allocation) alive until :meth:`deregister_buffer`.  Returns
+        True when the mesh accepted it on every rank; False (every rank) leaves the staged path."""
+        if not self._zc or self.p < 2 or self.ipc() is None:
+            return False
+        return self._ipc_obj.register(self._flat(t))
+
+    def deregister_buffer(self, t: torch.Tensor) -> None:
+        if self._ipc_obj is not None:
+            self._ipc_obj.deregister(self._flat(t))
+
     def _run_allreduce(self, algo: str, view: torch.Tensor, op) -> None:
-        if algo in ("ipc1", "ipc2", "ipc2p") and self.ipc() is None:
+        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
+        if algo == "ipc2z":
+            peers = self._ipc_obj.registered(view) if self._zc else None
+            if peers is not None and (not torch.cuda.is_current_stream_capturing()
+                                      or self._ipc_obj._epoch_dev is not None):
+                self._ipc_obj.allreduce_registered(view, op, peers)
+                return
+            algo = "ipc2"        # not registered (on this rank): the staged two-shot
+        if algo in ("ipc1", "ipc2", "ipc2p") and torch.cuda.is_current_stream_capturing():
+            nb = view.numel() * view.element_size()
+            inst = self.ipc_large() if nb > self.ipc_twoshot_max else self._ipc_obj
+            if inst is None or inst._epoch_dev is None:
+                algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
             self.coll.all_reduce(view, op.code)
         elif algo.startswith("rccl_c"):
@@ -432,11 +648,10 @@ class DeviceEngine:
             return None
         if self.ipc() is None or not self._ipc_obj.fp8_ok(view):
             return None
-        if torch.cuda.is_current_stream_capturing() and self._ipc_obj._epoch_dev is None:
+        inst = self._ipc_obj if view.numel() * 260 // 256 <= self._ipc_obj.nbytes else self.ipc_large()
+        if torch.cuda.is_current_stream_capturing() and (inst is None or inst._epoch_dev is None):
             return None
-        if view.numel() * 260 // 256 <= self._ipc_obj.nbytes:
-            return self._ipc_obj
-        return self.ipc_large()
+        return inst
 
     # ------------------------------------------------------------------ autotuning
     def _algo_valid(self, algo: str, op, dtype, nbytes: int) -> bool:
@@ -444,7 +659,7 @@ class DeviceEngine:
             return self.rccl_ok(op, dtype)
         if algo.startswith("rccl_c"):
             return self.backend == "nccl" and self.rccl_ok(op, dtype)
-        if algo in ("ipc1", "ipc2", "ipc2p"):
+        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z"):
             return self._ipc_ok(op, dtype, nbytes)
         if algo == "rhd":
             return not getattr(op, "is_custom", False)
@@ -462,6 +677,8 @@ class DeviceEngine:
             c.append("ipc2")
             if nbytes > self.ipc_twoshot_max:
                 c.append("ipc2p")     # pipelined pieces: input copies overlap the xGMI-bound kernel
+            if self._zc:
+                c.append("ipc2z")     # zero-copy two-shot on a registered tensor (one kernel)
         c.append("a2a")
         if nbytes <= (64 << 20):
             c.append("rhd")
@@ -484,10 +701,17 @@ class DeviceEngine:
         times = []
         if self.watchdog is not None:
             self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
+        registered = False
         try:
+            if "ipc2z" in cands:
+                registered = self.register_buffer(view)     # collective; False on every rank alike
+                if not registered:
+                    cands.remove("ipc2z")
             for c in cands:
                 times.append(self._time_candidate(c, view, op, iters))
         finally:
+            if registered:
+                self.deregister_buffer(view)
             if self.watchdog is not None:
                 self.watchdog.paused -= 1
         tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
@@ -574,37 +798,63 @@ class DeviceEngine:
         return res
 
     def _time_fn(self, run, uses_ipc: bool, iters: int, name: str, probe=None) -> float:
-        """Seconds per call of ``run`` (inf when it failed on this rank).  Collective.
+        """Seconds per call of ``run`` (inf when it failed or was wrong on ANY rank).  Collective.
 
         ``probe()`` (optional) fills the operand with an exact pattern and returns a function
-        that counts wrong elements after the warm-up call (see :meth:`_fill_probe`)."""
-        ok = True
-        dt = float("inf")
+        that counts wrong elements after the warm-up call (see :meth:`_fill_probe`).
+
+        Every rank joins the same agreement collectives whatever happened locally (a local
+        exception only sets a flag), so a schedule that fails on one rank cannot pair mismatched
+        collectives.  Bounded: when the agreed warm-up took longer than ``MP4X_AUTOTUNE_CAP_S``
+        (default 2 s) the warm-up time is the estimate and no timed calls run; otherwise the
+        timed calls are capped to about that wall time."""
+        cap = float(os.environ.get("MP4X_AUTOTUNE_CAP_S", "2"))
+        failed, wrong, warm = 0, 0, float("inf")
         try:
             check = probe() if probe is not None and self._verify_autotune else None
+            t0 = time.perf_counter()
             run()                                # warm-up (lazy IPC / RCCL setup)
             self._sync()
+            warm = time.perf_counter() - t0
             wrong = check() if check is not None else 0
-            timeout, nwrong = self._agree([self._ipc_error_local() if uses_ipc else 0, wrong])
-            if timeout:
-                raise Mp4jException("IPC barrier timeout during warm-up")
-            if nwrong:
-                raise Mp4jException(f"wrong result on the probe pattern (up to {nwrong} elements differ)")
+        except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
+            LOG.warning("autotune: %s failed on rank %d: %s", name, self.rank, e)
+            failed = 1
+        timeout = self._ipc_error_flag() if uses_ipc else 0
+        warm_us = int(min(warm, 1e9) * 1e6)
+        failed, timeout, nwrong, warm_us = self._agree([failed, timeout, wrong, warm_us])
+        if failed or timeout or nwrong:
+            if self.rank == 0:
+                LOG.warning("autotune: %s ruled out (%s)", name, "failed" if failed else
+                            "IPC barrier timeout" if timeout else f"up to {nwrong} wrong elements on the probe")
+            return float("inf")
+        warm = warm_us / 1e6
+        if warm > cap:
+            return warm                          # too slow to matter: not worth timed calls
+        n = max(1, min(max(1, iters), int(cap / max(warm, 1e-6))))
+        dt = float("inf")
+        failed = 0
+        try:
             self.barrier()
             t0 = time.perf_counter()
-            for _ in range(max(1, iters)):
+            for _ in range(n):
                 run()
             self._sync()
-            dt = (time.perf_counter() - t0) / max(1, iters)
-            if uses_ipc and self._ipc_error():
-                ok = False
-        except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
-            LOG.warning("autotune: %s failed: %s", name, e)
-            ok = False
-        return dt if ok else float("inf")
+            dt = (time.perf_counter() - t0) / n
+        except Exception as e:       # noqa: BLE001
+            LOG.warning("autotune: %s failed on rank %d: %s", name, self.rank, e)
+            failed = 1
+        failed, timeout = self._agree([failed, self._ipc_error_flag() if uses_ipc else 0])
+        return float("inf") if failed or timeout else dt
+
+    def _ipc_error_flag(self) -> int:
+        try:
+            return self._ipc_error_local()
+        except Exception:   # noqa: BLE001
+            return 1
 
     # ------------------------------------------------------------------ persisted tuning table
-    _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "a2a", "rhd"},
+    _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "a2a", "rhd"},
                     "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"}}
 
     def _topology(self) -> dict:
@@ -662,37 +912,21 @@ class DeviceEngine:
                 LOG.warning("could not save the tuning table to %s: %s", path, e)
 
     def _time_candidate(self, c: str, view: torch.Tensor, op, iters: int) -> float:
-        """Seconds per call of schedule ``c`` (inf when it failed on this rank).  Collective."""
-        ok = True
-        dt = float("inf")
-        try:
-            expect = self._fill_probe(view, op) if self._verify_autotune else None
-            self._run_allreduce(c, view, op)     # warm-up (lazy IPC / RCCL setup)
-            self._sync()
-            # the warm-up doubles as a correctness probe: a schedule whose result differs from
-            # the exact answer (e.g. a peer-visibility bug on some topology) is never pinned.
-            # Both verdicts are agreed (MAX over ranks) so every rank skips the timed calls together.
-            wrong = 0
-            if expect is not None:
-                wrong = int((view != expect).sum())
+        """Seconds per call of allreduce schedule ``c`` (inf when it failed or was wrong on any
+        rank; bounded, see :meth:`_time_fn`).  Collective.  The warm-up doubles as a correctness
+        probe: a schedule whose result differs from the exact answer (e.g. a peer-visibility bug
+        on some topology) is never pinned."""
+        def probe():
+            expect = self._fill_probe(view, op)
+            if expect is None:
+                return None
+
+            def check():
+                bad = int((view != expect).sum())
                 view.zero_()
-            timeout, nwrong = self._agree([self._ipc_error_local() if c.startswith("ipc") else 0, wrong])
-            if timeout:
-                raise Mp4jException("IPC barrier timeout during warm-up")
-            if nwrong:
-                raise Mp4jException(f"wrong result on the probe pattern (up to {nwrong} elements differ)")
-            self.barrier()
-            t0 = time.perf_counter()
-            for _ in range(max(1, iters)):
-                self._run_allreduce(c, view, op)
-            self._sync()
-            dt = (time.perf_counter() - t0) / max(1, iters)
-            if c.startswith("ipc") and self._ipc_error():
-                ok = False
-        except Exception as e:       # noqa: BLE001 — a failed candidate is just not chosen
-            LOG.warning("autotune: %s failed: %s", c, e)
-            ok = False
-        return dt if ok else float("inf")
+                return bad
+            return check
+        return self._time_fn(lambda: self._run_allreduce(c, view, op), c.startswith("ipc"), iters, c, probe)
 
     def _ipc_error_local(self) -> int:
         mine = 0

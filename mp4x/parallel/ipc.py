@@ -29,6 +29,11 @@ native.register_signatures({
     "mp4x_ipc_signal_bytes": (c_size_t, []),
     "mp4x_ipc_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
     "mp4x_ipc_free": (c_int, [c_void_p]),
+    "mp4x_host_word_alloc": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
+    "mp4x_host_word_free": (c_int, [c_void_p]),
+    "mp4x_ipc_set_host_error": (c_int, [c_void_p, c_void_p]),
+    "mp4x_ipc_set_spin": (c_int, [ctypes.c_double]),
+    "mp4x_mem_range": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
     "mp4x_ipc_handle_size": (c_int, []),
     "mp4x_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
     "mp4x_ipc_open_handle": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
@@ -61,7 +66,18 @@ native.register_signatures({
 _RESIDENT_BLOCKS = 1024
 
 ONESHOT, TWOSHOT = 0, 1
+ZC_TAG = 0x80000000      # epoch tag of the zero-copy protocol (csrc/runtime/ipc.hip kZcTag)
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64}
+
+
+_SPIN_SET = [False]
+
+
+def _set_spin(lib) -> None:
+    """Barrier spin bound (``MP4X_IPC_SPIN_S`` seconds, default 10), once per process."""
+    if not _SPIN_SET[0]:
+        check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SPIN_S", "10"))), "ipc_set_spin")
+        _SPIN_SET[0] = True
 
 
 class IpcAllreduce:
@@ -71,19 +87,33 @@ class IpcAllreduce:
         self.p = comm.slaveNum
         if not (2 <= self.p <= 8):
             raise Mp4jException("IPC allreduce supports 2..8 ranks")
-        self.lib = native.hip()
+        self.lib = None
+        self._data = c_void_p()
+        self._sig = c_void_p()
+        self._herr = c_void_p()          # pinned host error word (CPU address)
+        self._opened: List[c_void_p] = []
+        # Every local step that can fail runs before the first collective inside a try, and its
+        # error travels in that collective: a rank that fails alone must not leave its peers
+        # waiting in an allgather it never joins (every rank raises together instead).
+        local_err = None
+        try:
+            self.lib = native.hip()
+            self.device = torch.cuda.current_device()
+            hs = self.lib.mp4x_ipc_handle_size()
+            _set_spin(self.lib)
+        except Exception as e:   # noqa: BLE001
+            local_err = f"{type(e).__name__}: {e}"
         # IPC handles only open on the same node: a job spanning hosts keeps RCCL (decided from
         # the exchanged host names, identically on every rank, before anything is allocated)
-        hosts = comm.server.call("allgather_obj", self.rank, socket.gethostname())
+        infos = comm.server.call("allgather_obj", self.rank, (socket.gethostname(), local_err))
+        errs = [(i, e) for i, (_, e) in enumerate(infos) if e]
+        if errs:
+            raise Mp4jException(f"IPC setup failed on ranks {errs}")
+        hosts = [h for h, _ in infos]
         if len(set(hosts)) != 1:
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
-        self.device = torch.cuda.current_device()
-        hs = self.lib.mp4x_ipc_handle_size()
-        self._data = c_void_p()
-        self._sig = c_void_p()
-        self._opened: List[c_void_p] = []
         # a local failure here (out of memory, no IPC support) must still reach the allgather
         # below: raising before it would leave the peers waiting there for this rank
         local_err = None
@@ -91,6 +121,9 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_alloc(self.nbytes, ctypes.byref(self._data)), "ipc_alloc(data)")
             check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)),
                   "ipc_alloc(sig)")
+            herr_dev = c_void_p()
+            check(self.lib.mp4x_host_word_alloc(ctypes.byref(self._herr), ctypes.byref(herr_dev)), "host_word_alloc")
+            check(self.lib.mp4x_ipc_set_host_error(self._sig, herr_dev), "ipc_set_host_error")
             hd = ctypes.create_string_buffer(hs)
             hsg = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
@@ -143,8 +176,32 @@ class IpcAllreduce:
         self._sig_stream = None    # private stream for error-word reads (lazy)
         self._overlap_default = os.environ.get("MP4X_IPC_OVERLAP", "0") == "1"
         self._fuse_copy = os.environ.get("MP4X_IPC_FUSED_COPY", "1") == "1"
+        # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> peer pointers
+        self._regs = {}
+        self._peer_bases = {}       # (rank, handle bytes) -> mapped base (one open per allocation)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
+
+    # ---------------------------------------------------------------- fail-stop
+    def host_error(self) -> int:
+        """The host-visible barrier-timeout word (0 = fine; 1/2/3 = a start/mid/end barrier of an
+        earlier kernel timed out), read from pinned memory: no device synchronisation."""
+        if not self._herr:
+            return 0
+        return int(ctypes.c_uint32.from_address(self._herr.value).value)
+
+    def raise_if_failed(self) -> None:
+        """Fail the call instead of corrupting it: if an earlier IPC kernel of this instance gave
+        up waiting for a peer (a rank skipped or died in a collective), its result was left
+        incomplete — raise ``Mp4jException`` once (the word is cleared) before launching more.
+        Called at the start of every IPC collective (reference fail-stop contract,
+        ProcessCommSlave.java:360-373)."""
+        code = self.host_error()
+        if code:
+            ctypes.c_uint32.from_address(self._herr.value).value = 0
+            where = {1: "start", 2: "mid", 3: "end"}.get(code, str(code))
+            raise Mp4jException(f"rank {self.rank}: an earlier IPC collective timed out at its {where} barrier "
+                                f"(a peer skipped, failed or died in that call); its result is invalid")
 
     def supports(self, t: torch.Tensor, op) -> bool:
         if getattr(op, "is_custom", False) or t.dtype not in SUPPORTED_DTYPES:
@@ -161,6 +218,7 @@ class IpcAllreduce:
         input copies on a side stream; default from ``MP4X_IPC_OVERLAP`` (0).  It pays when the
         kernel is xGMI-bound; on a GPU shared by all ranks (single-GPU rehearsal) the copies
         compete for the same HBM and it measured 2x slower (profiles/r1/ipc_large_shared_gpu.jsonl)."""
+        self.raise_if_failed()
         if out is None:
             out = view
         if not view.is_contiguous() or not out.is_contiguous():
@@ -202,7 +260,7 @@ class IpcAllreduce:
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+                self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
             if fused:
                 check(self.lib.mp4x_ipc_allreduce_from(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
                                                        self.rank, self.p, m, src.data_ptr() + off, dst.data_ptr() + off,
@@ -247,7 +305,7 @@ class IpcAllreduce:
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, ms), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+                self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
             pp = self._pp_hi[0] if slot else self._pp_data[0]
             check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
                                               dst.data_ptr() + off, self.epoch, blocks, edev, ms),
@@ -258,6 +316,106 @@ class IpcAllreduce:
             off += m
             i += 1
         return out
+
+
+    # ---------------------------------------------------------------- registered buffers (zero-copy)
+    # A caller tensor registered on every rank (collectively, like ncclCommRegister) is mapped
+    # into every peer: the two-shot then reads and writes the peers' tensors directly — no
+    # staging copy, no piece loop, for any size.  Rank r's kernel writes only chunk r of its own
+    # tensor in the reduce-scatter half and only the foreign chunks in the all-gather half; the
+    # start / mid / end barriers order those against the peers' reads (csrc/runtime/ipc.hip).
+    # Contract: every rank registers the same-shaped tensor at the same point, keeps it alive
+    # (and its caching-allocator segment) until ``deregister``, and runs allreduces on it (or on
+    # the same [from, to) views of it) on every rank; a rank that runs the staged protocol
+    # against a zero-copy peer fails that call at once (epoch tag) instead of mixing buffers.
+    def register(self, t: torch.Tensor) -> bool:
+        """Collective.  Map ``t`` (contiguous, 16-byte aligned, 16-byte multiple) into every peer.
+        Returns True when every rank registered it (False on every rank otherwise)."""
+        key = (t.data_ptr(), t.numel() * t.element_size())
+        if key in self._regs:
+            ok_local = 1
+        else:
+            ok_local = 0
+        hs = self.lib.mp4x_ipc_handle_size()
+        blob = None
+        err = None
+        try:
+            if not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16 or key[1] % 16 or key[1] == 0:
+                raise Mp4jException("register needs a contiguous, 16-byte aligned device tensor of 16-byte multiple size")
+            base, size = c_void_p(), c_size_t()
+            check(self.lib.mp4x_mem_range(c_void_p(t.data_ptr()), ctypes.byref(base), ctypes.byref(size)), "mem_range")
+            h = ctypes.create_string_buffer(hs)
+            check(self.lib.mp4x_ipc_get_handle(base, h), "ipc_get_handle(registered)")
+            blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local)
+        except Exception as e:   # noqa: BLE001 — travels in the allgather: every rank decides together
+            err = str(e)
+        allb = self.comm.server.call("allgather_obj", self.rank, (blob, err))
+        errs = [(i, e) for i, (_, e) in enumerate(allb) if e]
+        if errs or len({b[2] for b, _ in allb}) != 1:
+            return False
+        if all(b[3] for b, _ in allb):
+            return True                               # already registered everywhere
+        ptrs, err = [], None
+        try:
+            for r, (b, _) in enumerate(allb):
+                if r == self.rank:
+                    ptrs.append(t.data_ptr())
+                    continue
+                hk = (r, bytes(b[0]))
+                if hk not in self._peer_bases:
+                    hb = ctypes.create_string_buffer(bytes(b[0]), hs)
+                    ptr = c_void_p()
+                    check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(registered, rank {r})")
+                    self._opened.append(ptr)
+                    self._peer_bases[hk] = ptr.value
+                ptrs.append(self._peer_bases[hk] + int(b[1]))
+        except Exception as e:   # noqa: BLE001
+            err = str(e)
+        oks = self.comm.server.call("allgather_obj", self.rank, err)
+        if any(oks):
+            return False
+        self._regs[key] = ptrs
+        return True
+
+    def deregister(self, t: torch.Tensor) -> None:
+        """Forget ``t`` (local; the peer mappings of its allocation stay open until close)."""
+        self._regs.pop((t.data_ptr(), t.numel() * t.element_size()), None)
+
+    def registered(self, view: torch.Tensor):
+        """Peer pointers of ``view`` when it lies inside a registered tensor, else None."""
+        if not self._regs:
+            return None
+        a = view.data_ptr()
+        n = view.numel() * view.element_size()
+        for (ptr, nb), peers in self._regs.items():
+            if ptr <= a and a + n <= ptr + nb:
+                d = a - ptr
+                return [q + d for q in peers]
+        return None
+
+    def allreduce_registered(self, view: torch.Tensor, op, peers) -> torch.Tensor:
+        """In-place two-shot straight on the registered tensors (see :meth:`register`): ONE
+        kernel, no staging and no pieces, whatever the size."""
+        self.raise_if_failed()
+        total = view.numel() * view.element_size()
+        if total % 16 or view.data_ptr() % 16:
+            raise Mp4jException("zero-copy IPC allreduce needs 16-byte aligned, 16-byte multiple views")
+        st = stream_ptr()
+        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+            raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
+        if edev is not None:
+            check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
+        else:
+            self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
+        blocks = 0
+        if self.max_blocks:
+            blocks = max(1, min(self.max_blocks, -(-total // 16 // 512)))
+        pp = ptr_array(peers)
+        check(self.lib.mp4x_ipc_allreduce(TWOSHOT, int(dtype_of_torch(view.dtype)), int(op.code), pp[0],
+                                          self._pp_sig[0], self.rank, self.p, total, view.data_ptr(),
+                                          self.epoch | ZC_TAG, blocks, edev, st), "mp4x_ipc_allreduce(zero-copy)")
+        return view
 
     # ---------------------------------------------------------------- RS / AG over ragged ranges
     # Results are produced inside the staging buffer (always 16-byte aligned) and copied out, so
@@ -276,7 +434,7 @@ class IpcAllreduce:
             return self._epoch_dev.data_ptr()
         if torch.cuda.is_current_stream_capturing():
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
-        self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+        self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
         return None
 
     def _blocks_for(self, nvec: int) -> int:
@@ -296,6 +454,7 @@ class IpcAllreduce:
         whose byte offsets are 16-byte multiples).  Returns False (nothing done) otherwise."""
         if not self._range_ok(view, froms, tos) or not self.supports(view, op):
             return False
+        self.raise_if_failed()
         es = view.element_size()
         flat = view.view(-1)
         base, r = froms[0], self.rank
@@ -340,6 +499,7 @@ class IpcAllreduce:
         """In place: every rank's ``view[froms[j]:tos[j]]`` lands everywhere (ragged, 16-byte offsets)."""
         if not self._range_ok(view, froms, tos):
             return False
+        self.raise_if_failed()
         es = view.element_size()
         flat = view.view(-1)
         base, r = froms[0], self.rank
@@ -387,6 +547,7 @@ class IpcAllreduce:
     # messages up to the buffer size; ranges must be whole 16-byte vectors from a 16-byte aligned
     # tensor (checked identically on every rank from the shared arguments).
     def _plan(self, stage, pull, src_ptr, out_ptr, grid_len) -> None:
+        self.raise_if_failed()
         st = stream_ptr()
         edev = self._next_epoch(st)
         sa = (c_int64 * (4 * max(1, len(stage))))(*[x for it in stage for x in it])
@@ -494,6 +655,7 @@ class IpcAllreduce:
         """In place ``view[froms[r]:tos[r]]`` <- op over all ranks, any message size, in pieces."""
         if not self.supports(view, op) or not self.large_ok(view, froms, tos):
             return False
+        self.raise_if_failed()
         es = view.element_size()
         flat = view.view(-1)
         p, r = self.p, self.rank
@@ -524,6 +686,7 @@ class IpcAllreduce:
         """In place: every rank's ``view[froms[j]:tos[j]]`` lands everywhere, any size, in pieces."""
         if not self.large_ok(view, froms, tos):
             return False
+        self.raise_if_failed()
         es = view.element_size()
         flat = view.view(-1)
         p, r = self.p, self.rank
@@ -576,6 +739,7 @@ class IpcAllreduce:
         :meth:`fp8_ok`."""
         if not self.fp8_ok(view):
             raise Mp4jException("fp8 IPC allreduce needs a contiguous f32/bf16/f16 tensor, n % 4 == 0")
+        self.raise_if_failed()
         if view.data_ptr() % 16:
             self._aligned(view, self.allreduce_fp8)
             return view
@@ -633,8 +797,12 @@ class IpcAllreduce:
         return int(v.value)
 
     def close(self, sync: bool = True):
+        if self.lib is None:
+            return
         if sync:
             torch.cuda.synchronize()
+        if self._sig and self._herr:
+            self.lib.mp4x_ipc_set_host_error(self._sig, None)
         for ptr in self._opened:
             self.lib.mp4x_ipc_close_handle(ptr)
         self._opened = []
@@ -644,3 +812,6 @@ class IpcAllreduce:
         if self._sig:
             self.lib.mp4x_ipc_free(self._sig)
             self._sig = c_void_p()
+        if self._herr:
+            self.lib.mp4x_host_word_free(self._herr)
+            self._herr = c_void_p()

@@ -251,6 +251,23 @@ class ProcessCommSlave:
             self._device_engine = DeviceEngine(self, self._device_index)
         return self._device_engine
 
+    def registerBuffer(self, tensor) -> bool:
+        """Collective (extension, like ``ncclCommRegister``): map a device tensor into every peer
+        so allreduces on it (or on [from, to) views of it) run the zero-copy xGMI two-shot — no
+        staging copy and no pieces at any size.  Every rank registers its same-shaped tensor at
+        the same point and keeps it alive until :meth:`deregisterBuffer`.  Returns False on every
+        rank when the mesh refused it (the staged kernels are used then)."""
+        if self.slaveNum == 1 or not _is_device_tensor(tensor):
+            return False
+        return self.device.register_buffer(tensor)
+
+    def deregisterBuffer(self, tensor) -> None:
+        if self._device_engine is not None:
+            self._device_engine.deregister_buffer(tensor)
+
+    register_buffer = registerBuffer
+    deregister_buffer = deregisterBuffer
+
     def _shm_engine(self, buf, operand: Operand, operator, nelems: int):
         """The shared-memory engine when this call qualifies (decision identical on every rank)."""
         if os.environ.get("MP4X_SHM", "1") != "1" or self.slaveNum == 1 or not operand.is_primitive \
@@ -649,6 +666,10 @@ class ProcessCommSlave:
         ``arrData`` is left untouched (with one rank this is a plain copy).
         """
         self._tick("allreduceArray")
+        if out is not None and self.slaveNum > 1 and _is_device_tensor(out) and _is_device_tensor(arrData):
+            # the device engine writes the result straight into ``out`` (no copy-then-in-place)
+            CommUtils.isFromToLegal(frm, to)
+            return self.device.allreduce(arrData, frm, to, operator, operand, out=out)
         if out is not None:
             CommUtils.isFromToLegal(frm, to)
             if _is_device_tensor(out):

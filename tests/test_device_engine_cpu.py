@@ -313,3 +313,77 @@ def test_rsag_autotune_probe_rejects_wrong_results():
     for a, b, tuned in res.values():
         assert all(v == float("inf") for v in a.values()) and all(v == float("inf") for v in b.values())
         assert not tuned
+
+
+def shared_table_job(comm, path):
+    """Only rank 0 can read the tuning file (rank 1's path is missing, as on a host without
+    the shared filesystem): every rank must pin rank 0's table, identically."""
+    import os
+    if comm.getRank() != 0:
+        os.environ["MP4X_TUNE_FILE"] = path + ".missing"
+    eng = comm.device
+    return dict(eng._tuned)
+
+
+def test_tuning_table_comes_from_rank0_only(tmp_path):
+    import json
+    path = str(tmp_path / "tune.json")
+    rows = [{"kind": "allreduce", "dtype": "float32", "op": 0, "size_class": 14, "algo": "a2a"}]
+    with open(path, "w") as f:
+        json.dump({"topology": {"p": 2, "device": "cpu", "backend": "gloo"}, "rows": rows}, f)
+    res, code, _ = run_ranks(2, shared_table_job, args=(path,), timeout=120, env={"MP4X_TUNE_FILE": path})
+    assert code == 0
+    assert res[0] == res[1] and len(res[0]) == 1, res
+
+
+def one_rank_raises_job(comm):
+    """A schedule whose local post-check raises on ONE rank during its warm-up (after its
+    transport calls completed): that rank only sets a flag, every rank still joins the same
+    agreement collectives, and the schedule is ruled out everywhere (no mispaired collectives,
+    no hang).  Before r2 the raising rank skipped the agreement all_reduce its peers entered."""
+    eng = comm.device
+    orig = eng._run_allreduce
+
+    def flaky(c, view, op):
+        orig(c, view, op)
+        if c == "rhd" and comm.getRank() == 1:
+            raise RuntimeError("local failure on rank 1")
+    eng._run_allreduce = flaky
+    res = eng.autotune_allreduce(torch.ones(4096), Operators.Float.SUM, iters=2)
+    eng._run_allreduce = orig
+    t = torch.ones(64)
+    eng.allreduce(t, 0, 64, Operators.Float.SUM)          # the job goes on
+    assert torch.all(t == comm.getSlaveNum())
+    return res
+
+
+def test_autotune_local_failure_is_agreed():
+    res, code, _ = run_ranks(3, one_rank_raises_job, timeout=120)
+    assert code == 0
+    for r in res.values():
+        assert r["rhd"] == float("inf") and all(v < float("inf") for c, v in r.items() if c != "rhd")
+
+
+def capped_job(comm):
+    """A schedule whose warm-up exceeds MP4X_AUTOTUNE_CAP_S gets no timed calls."""
+    import time as _t
+    eng = comm.device
+    orig = eng._run_allreduce
+    calls = {"rhd": 0}
+
+    def slow(c, view, op):
+        if c == "rhd":
+            calls["rhd"] += 1
+            _t.sleep(0.3)
+        orig(c, view, op)
+    eng._run_allreduce = slow
+    res = eng.autotune_allreduce(torch.ones(4096), Operators.Float.SUM, iters=5)
+    eng._run_allreduce = orig
+    return res, calls["rhd"]
+
+
+def test_autotune_wall_cap(monkeypatch):
+    res, code, _ = run_ranks(2, capped_job, timeout=120, env={"MP4X_AUTOTUNE_CAP_S": "0.1"})
+    assert code == 0
+    for r, n in res.values():
+        assert n == 1 and r["rhd"] >= 0.3, (r, n)

@@ -72,6 +72,18 @@ class _FakeLib:
         self.freed.append(ptr)
         return 0
 
+    def mp4x_ipc_set_spin(self, s):
+        return 0
+
+    def mp4x_host_word_alloc(self, hptr, dptr):
+        return 0
+
+    def mp4x_host_word_free(self, hptr):
+        return 0
+
+    def mp4x_ipc_set_host_error(self, sig, dev):
+        return 0
+
 
 def test_alloc_failure_on_one_rank_raises_on_every_rank(monkeypatch):
     p = 3
@@ -96,3 +108,35 @@ def test_alloc_failure_on_one_rank_raises_on_every_rank(monkeypatch):
         t.join(20)
     assert not any(t.is_alive() for t in threads), "a rank is stuck waiting for its peers"
     assert all(e is not None and "failed on ranks [(1," in e for e in errors), errors
+
+
+def test_native_load_failure_before_first_collective_raises_on_every_rank(monkeypatch):
+    """native.hip() / current_device() failing on ONE rank happen before any collective: the
+    error must travel in the first allgather so no peer is left waiting (ipc.py:74)."""
+    p = 3
+    tls = threading.local()
+    lib = _FakeLib(lambda: False)
+
+    def hip():
+        if tls.rank == 2:
+            raise OSError("libmp4x_hip.so: cannot open shared object file")
+        return lib
+    monkeypatch.setattr(ipc_mod.native, "hip", hip)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
+    server = _Server(p)
+    errors = [None] * p
+
+    def run(r):
+        tls.rank = r
+        try:
+            ipc_mod.IpcAllreduce(_Comm(server, r), nbytes=1 << 16)
+        except Mp4jException as e:
+            errors[r] = str(e)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(p)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(20)
+    assert not any(t.is_alive() for t in threads), "a rank is stuck waiting for its peers"
+    assert all(e is not None and "setup failed on ranks [(2," in e for e in errors), errors

@@ -30,3 +30,8 @@ def test_torchrun_bench_dry_run_all_ranks_exit_clean(tmp_path):
     assert len(lines) == 1
     rec = lines[0]
     assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["value"] > 0
+    # value is the per-rank nccl-tests busbw (BASELINE metric), not the whole-job sum
+    assert rec["value"] == rec["busbw_gbps_per_rank"]
+    assert abs(rec["aggregate_busbw_gbps"] - 4 * rec["busbw_gbps_per_rank"]) < 1e-2
+    assert abs(rec["busbw_gbps_per_rank"] - rec["algbw_gbps"] * 2 * 3 / 4) < 1e-2
+    assert "e+" not in rec["config"]["model"]
