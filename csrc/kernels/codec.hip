@@ -11,7 +11,8 @@
 //   dequant_reduce: one wave per block, NIN fp8 chunks dequantised and summed in f32
 //                   registers (the two-shot compressed allreduce's reduce step), optionally
 //                   re-quantised in the same pass for the all-gather leg.
-#include <hipcub/hipcub.hpp>
+#include <cstring>
+#include <rocprim/device/device_scan.hpp>   // 64-bit scan sizes (no (int) narrowing)
 #include <stdlib.h>
 
 #include "fp8.hpp"
@@ -540,7 +541,8 @@ static int zs_encode_twopass_t(const void* in, const int64_t* table, int nchunk,
   hipLaunchKernelGGL(k_zs_mask<W>, dim3(g), dim3(kBlock), 0, st, (const W*)in, table, nchunk, nblk, masks, counts);
   int e = (int)hipGetLastError();
   if (e) return e;
-  e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
+  e = (int)rocprim::exclusive_scan(temp, temp_bytes, counts, offs, (int64_t)0, (size_t)nblk, rocprim::plus<int64_t>(),
+                                   st);
   if (e) return e;
   hipLaunchKernelGGL(k_zs_total, dim3(1), dim3(1), 0, st, offs, counts, nblk, offs + nblk);
   const int g2 = grid_for((nblk + ZU2 - 1) / ZU2 * 64, 1);
@@ -553,7 +555,8 @@ template <typename W>
 static int zs_decode_t(const uint64_t* masks, const int32_t* counts, const void* vals, const int64_t* table,
                        int nchunk, int64_t nblk, void* out, int64_t* offs, void* temp, size_t temp_bytes,
                        hipStream_t st) {
-  int e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, offs, (int)nblk, st);
+  int e = (int)rocprim::exclusive_scan(temp, temp_bytes, counts, offs, (int64_t)0, (size_t)nblk,
+                                       rocprim::plus<int64_t>(), st);
   if (e) return e;
   // offs[nblk] (= total words) bounds the last wave's staged range: it must be written here too
   hipLaunchKernelGGL(k_zs_total, dim3(1), dim3(1), 0, st, offs, counts, nblk, offs + nblk);
@@ -602,8 +605,8 @@ extern "C" int mp4x_dequant_fp8(int dtype_out, void* out, const uint8_t* q, cons
 
 extern "C" size_t mp4x_zs_temp_bytes(int64_t nblk) {
   size_t bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const int32_t*)nullptr, (int64_t*)nullptr,
-                                         (int)(nblk < 1 ? 1 : nblk), (hipStream_t)0);
+  (void)rocprim::exclusive_scan(nullptr, bytes, (const int32_t*)nullptr, (int64_t*)nullptr, (int64_t)0,
+                                (size_t)(nblk < 1 ? 1 : nblk), rocprim::plus<int64_t>(), (hipStream_t)0);
   const size_t sb = zs_status_bytes(nblk < 1 ? 1 : nblk);      // single-pass encode: tile status words
   return bytes > sb ? bytes : sb;
 }

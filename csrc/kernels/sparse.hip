@@ -13,7 +13,12 @@
 //   K7  set union / intersection / concat reuse the same runs (count == p for intersection).
 //   K8  map merge (gather / allgather map): the same runs with OP = FIRST keep the first
 //       row of every key in rank order (dedupe-by-key).
-#include <hipcub/hipcub.hpp>
+// rocPRIM directly (64-bit sizes everywhere: no (int) narrowing of element counts)
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "common.hpp"
 
@@ -289,12 +294,13 @@ extern "C" int mp4x_key_owner(const int64_t* keys, int64_t n, int p, int32_t* de
 
 extern "C" size_t mp4x_sort_pairs_temp_bytes(int64_t n, int key_is_i32) {
   size_t bytes = 0;
+  const size_t sz = (size_t)(n < 1 ? 1 : n);
   if (key_is_i32)
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                       (const int64_t*)nullptr, (int64_t*)nullptr, (int)n, 0, 32, (hipStream_t)0);
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                    (const int64_t*)nullptr, (int64_t*)nullptr, sz, 0, 32, (hipStream_t)0);
   else
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr,
-                                       (const int64_t*)nullptr, (int64_t*)nullptr, (int)n, 0, 64, (hipStream_t)0);
+    (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                    (const int64_t*)nullptr, (int64_t*)nullptr, sz, 0, 64, (hipStream_t)0);
   return bytes;
 }
 
@@ -302,23 +308,23 @@ extern "C" int mp4x_sort_pairs_i64(const int64_t* keys_in, int64_t* keys_out, co
                                    int64_t n, int begin_bit, int end_bit, void* temp, size_t temp_bytes,
                                    void* stream) {
   if (n <= 0) return 0;
-  return (int)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (int)n,
-                                                 begin_bit, end_bit, (hipStream_t)stream);
+  return (int)rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (size_t)n,
+                                        (unsigned)begin_bit, (unsigned)end_bit, (hipStream_t)stream);
 }
 
 extern "C" int mp4x_sort_pairs_i32key(const int32_t* keys_in, int32_t* keys_out, const int64_t* idx_in,
                                       int64_t* idx_out, int64_t n, int begin_bit, int end_bit, void* temp,
                                       size_t temp_bytes, void* stream) {
   if (n <= 0) return 0;
-  return (int)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (int)n,
-                                                 begin_bit, end_bit, (hipStream_t)stream);
+  return (int)rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (size_t)n,
+                                        (unsigned)begin_bit, (unsigned)end_bit, (hipStream_t)stream);
 }
 
 extern "C" size_t mp4x_rle_temp_bytes(int64_t n) {
   size_t bytes = 0;
-  hipcub::CountingInputIterator<int64_t> it(0);
-  (void)hipcub::DeviceSelect::Flagged(nullptr, bytes, it, (const int32_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr,
-                                (int)n, (hipStream_t)0);
+  rocprim::counting_iterator<int64_t> it(0);
+  (void)rocprim::select(nullptr, bytes, it, (const int32_t*)nullptr, (int64_t*)nullptr, (int64_t*)nullptr,
+                        (size_t)(n < 1 ? 1 : n), (hipStream_t)0);
   return bytes;
 }
 
@@ -328,8 +334,8 @@ extern "C" int mp4x_run_starts(const int64_t* sorted_keys, int64_t n, int64_t* s
   if (n <= 0) return (int)hipMemsetAsync(nruns_dev, 0, sizeof(int64_t), st);
   int g = grid_for(n, 4);
   hipLaunchKernelGGL(k_head_flags, dim3(g), dim3(kBlock), 0, st, sorted_keys, n, flags);
-  hipcub::CountingInputIterator<int64_t> it(0);
-  return (int)hipcub::DeviceSelect::Flagged(temp, temp_bytes, it, flags, starts, nruns_dev, (int)n, st);
+  rocprim::counting_iterator<int64_t> it(0);
+  return (int)rocprim::select(temp, temp_bytes, it, flags, starts, nruns_dev, (size_t)n, st);
 }
 
 extern "C" int mp4x_segment_reduce_rows(int dtype, int op, const int64_t* sk, const int64_t* perm, const int64_t* starts,
@@ -358,8 +364,8 @@ extern "C" size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p) {
   const int64_t nblk = (n + kBlock - 1) / kBlock;
   const int64_t m = (int64_t)p * (nblk < 1 ? 1 : nblk);
   size_t cub_bytes = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, cub_bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int)m,
-                                         (hipStream_t)0);
+  (void)rocprim::exclusive_scan(nullptr, cub_bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int64_t)0, (size_t)m,
+                                rocprim::plus<int64_t>(), (hipStream_t)0);
   return 2 * pack_align(m * sizeof(int64_t)) + pack_align(cub_bytes);
 }
 
@@ -384,7 +390,7 @@ extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_
   hipLaunchKernelGGL(k_pack_hist, dim3(nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, nblk, hist);
   int e = (int)hipGetLastError();
   if (e) return e;
-  e = (int)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hist, off, (int)m, st);
+  e = (int)rocprim::exclusive_scan(temp, temp_bytes, hist, off, (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), st);
   if (e) return e;
   const int64_t V = vals ? row_bytes / 16 : 0;
   int G = 1;
