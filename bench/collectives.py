@@ -10,6 +10,10 @@
 1e5 ... 1e9 elements for gather / scatter / allgather / reduce-scatter / broadcast / reduce /
 allreduce, reporting algbw, busbw (nccl-tests factors) and p50/p99 per size,
 plus the reference's own time at that (p, size) for comparison.  One JSON line per row.
+``--check`` adds one exact-value verification call per (op, size) after the timed calls
+(small-integer patterns, exact in double; the row gets ``"exact": true/false``); the configs
+check their results too (exact for the bf16 ZeRO pair, error-bounded against the fp64 sum for
+the fp8-compressed allreduce).
 """
 import argparse
 import json
@@ -59,6 +63,50 @@ def timed(fn, iters, warmup, sync):
     return ts[len(ts) // 2], ts[min(len(ts) - 1, int(0.99 * len(ts)))]
 
 
+def check_op(op, buf, comm, D, froms, tos, counts, p, r, sync):
+    """One exact-value call of ``op`` on small-integer patterns (exact in double)."""
+    import torch
+    from mp4x import Operators
+    n = buf.numel()
+    i = torch.arange(n, device=buf.device, dtype=torch.float64)
+    base = torch.remainder(i, 97)
+    root = 0
+    if op in ("gather", "allgather"):
+        buf.fill_(-1)
+        buf[froms[r]:tos[r]] = r + 1
+        (comm.gatherArray(buf, D, froms, tos, root) if op == "gather" else comm.allgatherArray(buf, D, froms, tos))
+        sync()
+        if op == "gather" and r != root:
+            return True
+        return all(bool((buf[froms[j]:tos[j]] == j + 1).all()) for j in range(p))
+    if op == "scatter":
+        buf.fill_(-1)
+        if r == root:
+            for j in range(p):
+                buf[froms[j]:tos[j]] = j + 1
+        comm.scatterArray(buf, D, froms, tos, root)
+        sync()
+        return bool((buf[froms[r]:tos[r]] == r + 1).all())
+    if op == "broadcast":
+        buf.copy_(base if r == root else torch.full_like(base, -1))
+        comm.broadcastArray(buf, D, 0, n, root)
+        sync()
+        return bool(torch.equal(buf, base))
+    buf.copy_(base + r)
+    exp = base * p + p * (p - 1) // 2
+    if op == "reduce_scatter":
+        comm.reduceScatterArray(buf, D, Operators.Double.SUM, 0, counts)
+        sync()
+        return bool(torch.equal(buf[froms[r]:tos[r]], exp[froms[r]:tos[r]]))
+    if op == "reduce":
+        comm.reduceArray(buf, D, Operators.Double.SUM, 0, n, root)
+        sync()
+        return r != root or bool(torch.equal(buf, exp))
+    comm.allreduceArray(buf, D, Operators.Double.SUM, 0, n)
+    sync()
+    return bool(torch.equal(buf, exp))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sweep", choices=["ref", "none"], default="none")
@@ -67,12 +115,14 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--max-elems", type=float, default=1e9)
+    ap.add_argument("--check", action="store_true", help="exact-value check of every row / config")
+    ap.add_argument("--codecs", default="none,fp8", help="fp8_8gb config: wire codecs to run")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
     from mp4x import CommUtils, Operands, Operators
     from mp4x.launch import init_from_env
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("MP4X_DEVICE_INDEX", os.environ.get("LOCAL_RANK", "0")))
     torch.cuda.set_device(local)
     comm = init_from_env(heartbeat=False)
     p, r = comm.getSlaveNum(), comm.getRank()
@@ -107,14 +157,20 @@ def main():
                 "allreduce": lambda: comm.allreduceArray(buf, D, Operators.Double.SUM, 0, n),
             }
             for k, op in enumerate(OPS):
+                st0 = dict(eng.stats) if eng is not None else {}
                 p50, p99 = timed(fns[op], a.iters, a.warmup, sync)
                 nb = n * 8
                 algbw = nb / (p50 * 1e-3) / 1e9
                 ref = REF_MS.get(p, {}).get(n)
-                emit({"op": op, "p": p, "elements": n, "bytes": nb, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
-                      "algbw_GBps": round(algbw, 3), "busbw_GBps": round(algbw * busfactor(op, p), 3),
-                      "ref_ms_1GbE": ref[k] if ref else None,
-                      "speedup_vs_ref": round(ref[k] / p50, 1) if ref else None})
+                rec = {"op": op, "p": p, "elements": n, "bytes": nb, "p50_ms": round(p50, 4), "p99_ms": round(p99, 4),
+                       "algbw_GBps": round(algbw, 3), "busbw_GBps": round(algbw * busfactor(op, p), 3),
+                       "ref_ms_1GbE": ref[k] if ref else None,
+                       "speedup_vs_ref": round(ref[k] / p50, 1) if ref else None}
+                if eng is not None:
+                    rec["path"] = sorted(x for x, v in eng.stats.items() if v != st0.get(x, 0))
+                if a.check:
+                    rec["exact"] = check_op(op, buf, comm, D, froms, tos, counts, p, r, sync)
+                emit(rec)
             del buf
     if a.config == "zero_bf16":   # BASELINE config 3: RS + AG of a 4 GB bf16 tensor
         n = 2_000_000_000 // p * p
@@ -134,9 +190,22 @@ def main():
             tuned = {k: {c: round(t * 1e3, 3) for c, t in v.items()} for k, v in tuned.items()}
         p50, p99 = timed(step, a.iters, a.warmup, sync)
         nb = n * 2
-        emit({"config": "reduceScatter + allgather of 4 GB bf16 (ZeRO)", "p": p, "p50_ms": p50, "p99_ms": p99,
-              "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None,
-              "autotune_ms": tuned})
+        rec = {"config": "reduceScatter + allgather of 4 GB bf16 (ZeRO)", "p": p, "p50_ms": p50, "p99_ms": p99,
+               "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None,
+               "autotune_ms": tuned}
+        if a.check:     # (i % 13 + rank) per rank: the RS + AG result is exact in bf16
+            CH = 1 << 28
+            for s0 in range(0, n, CH):
+                i = torch.arange(s0, min(n, s0 + CH), device="cuda")
+                x[s0:s0 + CH] = (i % 13 + r).to(torch.bfloat16)
+            step()
+            sync()
+            ok = True
+            for s0 in range(0, n, CH):
+                i = torch.arange(s0, min(n, s0 + CH), device="cuda")
+                ok &= bool(torch.equal(x[s0:s0 + CH], (p * (i % 13) + p * (p - 1) // 2).to(torch.bfloat16)))
+            rec["exact"] = bool(ok)
+        emit(rec)
     if a.config == "sparse_map":  # BASELINE config 4: sparse Map<String, float[]> allreduce
         dim, nkeys = 64, 200_000
         shared = nkeys // 2
@@ -154,13 +223,42 @@ def main():
     if a.config in ("fp8_8gb", "allreduce_1gb"):   # BASELINE configs 5 / 2
         nbytes = 8_000_000_000 if a.config == "fp8_8gb" else 1_000_000_000
         n = nbytes // 4
-        x = torch.randn(n, device="cuda")
-        for codec in ([None, "fp8"] if a.config == "fp8_8gb" else [None]):
+        CH = 1 << 27
+
+        def fill(dst, rank):      # chunk c of rank j from seed (j, c): any rank can regenerate it
+            for c, s0 in enumerate(range(0, n, CH)):
+                g = torch.Generator(device="cuda").manual_seed(rank * 100003 + c)
+                dst[s0:s0 + CH] = torch.randn(min(CH, n - s0), device="cuda", generator=g)
+        x = torch.empty(n, device="cuda")
+        fill(x, r)
+        codecs = [None if c == "none" else c for c in a.codecs.split(",")] if a.config == "fp8_8gb" else [None]
+        for codec in codecs:
             F = Operands.FLOAT_OPERAND(codec=codec)
             p50, p99 = timed(lambda: comm.allreduceArray(x, F, Operators.Float.SUM, 0, n), a.iters, a.warmup, sync)
-            emit({"config": f"allreduce {nbytes/1e9:.0f} GB f32", "codec": codec or "none", "p": p,
-                  "p50_ms": p50, "p99_ms": p99,
-                  "busbw_GBps": round(nbytes / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None})
+            rec = {"config": f"allreduce {nbytes/1e9:.0f} GB f32", "codec": codec or "none", "p": p,
+                   "p50_ms": p50, "p99_ms": p99,
+                   "busbw_GBps": round(nbytes / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None}
+            if a.check:       # one call on fresh data against the fp64 sum of every rank's input
+                fill(x, r)
+                comm.allreduceArray(x, F, Operators.Float.SUM, 0, n)
+                sync()
+                num = den = 0.0
+                worst = 0.0
+                for c, s0 in enumerate(range(0, n, CH)):
+                    m = min(CH, n - s0)
+                    ref = torch.zeros(m, dtype=torch.float64, device="cuda")
+                    for j in range(p):
+                        g = torch.Generator(device="cuda").manual_seed(j * 100003 + c)
+                        ref += torch.randn(m, device="cuda", generator=g).double()
+                    d = x[s0:s0 + m].double() - ref
+                    num += float((d * d).sum())
+                    den += float((ref * ref).sum())
+                    worst = max(worst, float(d.abs().max()))
+                rel = (num / max(den, 1e-300)) ** 0.5
+                rec["rel_l2_error_vs_fp64"] = rel
+                rec["max_abs_error"] = worst
+                rec["exact"] = rel < (0.1 if codec == "fp8" else 1e-6)
+            emit(rec)
     comm.close(0)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -24,6 +24,22 @@ _RCCL_OPS = {OpCode.SUM: dist.ReduceOp.SUM, OpCode.MAX: dist.ReduceOp.MAX,
              OpCode.MIN: dist.ReduceOp.MIN, OpCode.PROD: dist.ReduceOp.PRODUCT}
 
 
+# dtypes the transports move natively; anything else (int16, ...) moves as its bytes in the
+# data-movement collectives (RCCL and gloo have no int16 type; a copy is a copy)
+_MOVE_DTYPES = {torch.float64, torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32,
+                torch.int8, torch.uint8}
+
+
+def _mv(t: torch.Tensor) -> torch.Tensor:
+    return t if t.dtype in _MOVE_DTYPES else t.view(torch.uint8)
+
+
+def _scale(splits, t: torch.Tensor):
+    if splits is None or t.dtype in _MOVE_DTYPES:
+        return splits
+    return [x * t.element_size() for x in splits]
+
+
 class TorchColl:
     def __init__(self, pg, backend: str):
         self.pg = pg
@@ -38,23 +54,23 @@ class TorchColl:
         dist.reduce(t, dst=dst, op=_RCCL_OPS[code], group=self.pg)
 
     def broadcast(self, t, src):
-        dist.broadcast(t, src=src, group=self.pg)
+        dist.broadcast(_mv(t), src=src, group=self.pg)
 
     def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.pg)
+        dist.all_to_all_single(_mv(out), _mv(inp), _scale(out_splits, out), _scale(in_splits, inp), group=self.pg)
 
     def all_gather_into_tensor(self, out, inp):
-        dist.all_gather_into_tensor(out, inp, group=self.pg)
+        dist.all_gather_into_tensor(_mv(out), _mv(inp), group=self.pg)
 
     def all_gather(self, outs, t):
-        dist.all_gather(outs, t, group=self.pg)
+        dist.all_gather([_mv(o) for o in outs], _mv(t), group=self.pg)
 
     def reduce_scatter_tensor(self, out, inp, code):
         dist.reduce_scatter_tensor(out, inp, op=_RCCL_OPS[code], group=self.pg)
 
     def p2p(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
-        ops = [dist.P2POp(dist.isend, t, j, group=self.pg) for t, j in sends]
-        ops += [dist.P2POp(dist.irecv, t, j, group=self.pg) for t, j in recvs]
+        ops = [dist.P2POp(dist.isend, _mv(t), j, group=self.pg) for t, j in sends]
+        ops += [dist.P2POp(dist.irecv, _mv(t), j, group=self.pg) for t, j in recvs]
         # gloo's send/recv of a DEVICE tensor is not ordered after the kernels queued on the
         # current stream (one-GPU rehearsals stand gloo in for RCCL): drain the stream first.
         # RCCL orders its own stream after the current one, so the production path never waits.

@@ -31,6 +31,22 @@ def engine_matrix(comm, algo):
     s = torch.full((n,), r + 1, dtype=torch.int16)
     eng.allreduce(s, 0, n, Operators.Short.SUM)
     assert torch.all(s == p * (p + 1) // 2)
+    # int16 through the data-movement collectives (RCCL / gloo have no int16: moved as bytes)
+    fr, to = CommUtils.createProcessArrayFroms(n, p), CommUtils.createProcessArrayTos(n, p)
+    s = torch.full((n,), -1, dtype=torch.int16)
+    s[fr[r]:to[r]] = r
+    eng.allgather(s, fr, to)
+    assert all(torch.all(s[fr[i]:to[i]] == i) for i in range(p))
+    s = torch.full((n,), -1, dtype=torch.int16)
+    s[fr[r]:to[r]] = r
+    eng.gather(s, fr, to, p - 1)
+    assert r != p - 1 or all(torch.all(s[fr[i]:to[i]] == i) for i in range(p))
+    s = torch.arange(n, dtype=torch.int16) if r == 0 else torch.zeros(n, dtype=torch.int16)
+    eng.scatter(s, fr, to, 0)
+    assert torch.all(s[fr[r]:to[r]] == torch.arange(fr[r], to[r], dtype=torch.int16))
+    s = torch.full((n,), 3 if r == 0 else 0, dtype=torch.int16)
+    eng.broadcast(s, 0, n, 0)
+    assert torch.all(s == 3)
     # reduce-scatter ragged
     counts = [100 + 7 * i for i in range(p)]
     froms = CommUtils.getFromsFromCount(5, counts, p)

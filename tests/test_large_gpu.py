@@ -1,0 +1,141 @@
+"""Reference-scale payloads (VERDICT r1 missing #2): >= 2^31 elements and 8 GB byte ranges through
+the hand-written kernels and the IPC allreduce, checked exactly against torch (fp32 reference of
+the same op).  The reference runs 1e9 doubles (8 GB) per collective (README.md:313, :352); every
+index, size and byte offset in the kernels is 64-bit (rocPRIM with size_t sizes for the library
+sort / scan / select).
+
+Sizes: N31 = 2^31 + 4096 elements (bf16 / int8, > INT32_MAX), and 2e9 f32 = 8 GB (byte offsets
+> 2^32).  Memory: at most ~26 GB of the 288 GB HBM.
+"""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+N31 = (1 << 31) + 4096
+CH = 1 << 28           # verification chunk (elements)
+
+
+def _pat(n, mod, dt, off=0, dev="cuda"):
+    """(off + i) % mod as dtype, built chunk by chunk (small integers: exact in bf16 / int8)."""
+    out = torch.empty(n, dtype=dt, device=dev)
+    for s in range(0, n, CH):
+        e = min(n, s + CH)
+        out[s:e] = (torch.arange(s + off, e + off, device=dev, dtype=torch.int64) % mod).to(dt)
+    return out
+
+
+def _all_equal_chunked(a, b):
+    for s in range(0, a.numel(), CH):
+        if not torch.equal(a[s:s + CH], b[s:s + CH]):
+            return False
+    return True
+
+
+def test_k1_reduce_bf16_beyond_int32():
+    from mp4x.ops.device_ops import reduce_
+    from mp4x.operators import OpCode
+    a = _pat(N31, 7, torch.bfloat16)
+    b = _pat(N31, 5, torch.bfloat16, off=3)
+    reduce_(a, [a, b], int(OpCode.SUM))
+    torch.cuda.synchronize()
+    ref = _pat(N31, 7, torch.bfloat16)
+    for s in range(0, N31, CH):
+        e = min(N31, s + CH)
+        ref[s:e] += b[s:e]                        # torch bf16 add: f32 compute, one rounding
+    assert _all_equal_chunked(a, ref)
+    del a, b, ref
+    torch.cuda.empty_cache()
+
+
+def test_k1_reduce_f32_8gb():
+    from mp4x.ops.device_ops import reduce_
+    from mp4x.operators import OpCode
+    n = 2_000_000_000                             # 8 GB per tensor
+    a = _pat(n, 1000, torch.float32)
+    b = _pat(n, 999, torch.float32, off=11)
+    out = torch.empty_like(a)
+    reduce_(out, [a, b], int(OpCode.MAX))
+    torch.cuda.synchronize()
+    ok = all(torch.equal(out[s:s + CH], torch.maximum(a[s:s + CH], b[s:s + CH])) for s in range(0, n, CH))
+    assert ok
+    del a, b, out
+    torch.cuda.empty_cache()
+
+
+def test_fp8_codec_beyond_int32():
+    """Quantise / dequantise 2^31 + 4096 bf16 values: the blocks past element 2^31 must equal the
+    same kernel run on that tail alone (the codec is block-local), and the round trip is within
+    the e4m3 step of every block."""
+    from mp4x.ops.device_ops import quant_fp8, dequant_fp8
+    x = _pat(N31, 251, torch.bfloat16)
+    x -= 125
+    q, s = quant_fp8(x)
+    tail0 = (1 << 31) - (1 << 20)                 # block-aligned (256 | 2^20), straddles 2^31
+    qt, st = quant_fp8(x[tail0:].clone())
+    torch.cuda.synchronize()
+    assert torch.equal(q[tail0:], qt)
+    assert torch.equal(s[tail0 // 256:], st)
+    y = torch.empty_like(x)
+    dequant_fp8(q, s, N31, y)
+    yt = torch.empty(N31 - tail0, dtype=torch.bfloat16, device="cuda")
+    dequant_fp8(qt, st, N31 - tail0, yt)
+    torch.cuda.synchronize()
+    assert torch.equal(y[tail0:], yt)
+    for s0 in range(0, N31, CH):                  # e4m3: 3 mantissa bits -> rel. step 2^-3
+        d = (y[s0:s0 + CH].float() - x[s0:s0 + CH].float()).abs()
+        assert float(d.max()) <= 125 * 2 ** -3 + 1e-3
+    del x, q, s, y, qt, st, yt
+    torch.cuda.empty_cache()
+
+
+def test_zs_codec_int8_beyond_int32():
+    """Lossless zero suppression of 2^31 + 4096 int8 words (mostly zero, a non-zero every 37th):
+    decode(encode(x)) == x exactly."""
+    from mp4x.parallel import zs
+    n = N31
+    x = _pat(n, 37, torch.int8)
+    x = torch.where(x == 1, x, torch.zeros((), dtype=torch.int8, device="cuda"))
+    masks, counts, vals, nnz, bs = zs.encode(x, [(0, n)])
+    assert nnz[0] == sum(int((x[s:s + CH] != 0).sum()) for s in range(0, n, CH))
+    y = torch.full((n,), 9, dtype=torch.int8, device="cuda")
+    zs.decode(masks, counts, vals, [(0, n)], y)
+    torch.cuda.synchronize()
+    assert _all_equal_chunked(x, y)
+    del x, y, masks, counts, vals
+    torch.cuda.empty_cache()
+
+
+def _ipc_large_fn(comm, n):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    res = {}
+    for mode in ("staged", "zero_copy"):
+        x = _pat(n, 13, torch.bfloat16, off=r)
+        if mode == "zero_copy":
+            assert comm.registerBuffer(x)
+        comm.allreduceArray(x, Operands.BF16_OPERAND(), Operators.BFloat16.SUM, 0, n)
+        torch.cuda.synchronize()
+        ok = True
+        for s in range(0, n, CH):
+            e = min(n, s + CH)
+            i = torch.arange(s, e, device="cuda", dtype=torch.int64)
+            exp = sum(((i + j) % 13) for j in range(p)).to(torch.bfloat16)
+            ok &= torch.equal(x[s:e], exp)
+        res[mode] = ok
+        if mode == "zero_copy":
+            comm.deregisterBuffer(x)
+        del x
+        torch.cuda.empty_cache()
+    return res, dict(comm.device.stats)
+
+
+def test_ipc_allreduce_bf16_beyond_int32():
+    """2 ranks, 2^31 + 4096 bf16 elements each (4.3 GB): the staged piecewise two-shot and the
+    zero-copy two-shot (one kernel over 2^28 16-byte vectors), exact on small-integer data."""
+    from spawn_ranks import run_spawn
+    out = run_spawn(2, _ipc_large_fn, args=(N31,), env={"MP4X_DEVICE_ALGO": "ipc2"}, timeout=300)
+    for r, (res, stats) in out.items():
+        assert res == {"staged": True, "zero_copy": True}, (r, res, stats)
+        assert stats.get("allreduce.ipc2") == 1 and stats.get("allreduce.ipc2z") == 1, stats

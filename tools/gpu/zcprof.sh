@@ -10,10 +10,10 @@ run() {  # run <name> <timeout> <rank0 profiler args...>
   local name=$1; local t=$2; shift 2
   PROF0="$*" timeout -k 10 -s KILL $t python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
     --master-addr 127.0.0.1 --master-port 29615 --no-python bash tools/gpu/rank_prof.sh \
-    --gpus 2 --steps ${STEPS:-10} --warmup 3 --no-autotune --bytes $B > gpurun_out/zcprof/$name.log 2>&1
+    --gpus 2 --steps ${STEPS:-10} --warmup 3 --no-autotune $EXTRA --bytes $B > gpurun_out/zcprof/$name.log 2>&1
   local rc=$?; echo "$name rc=$rc"; grep '^{"metric"' gpurun_out/zcprof/$name.log | cut -c1-400
   return $rc
 }
-run trace_$ALGO 300 --kernel-trace --stats -f csv -d gpurun_out/zcprof/trace_$ALGO -o rank_%pid% && \
-STEPS=3 run pmc_fetch_$ALGO 120 --pmc FETCH_SIZE -f csv -d gpurun_out/zcprof/pmc_fetch_$ALGO -o rank_%pid% && \
-STEPS=3 run pmc_write_$ALGO 120 --pmc WRITE_SIZE -f csv -d gpurun_out/zcprof/pmc_write_$ALGO -o rank_%pid%
+run trace_$ALGO$TAG 300 --kernel-trace --stats -f csv -d gpurun_out/zcprof/trace_$ALGO$TAG -o rank_%pid% && \
+STEPS=3 run pmc_fetch_$ALGO$TAG 120 --pmc FETCH_SIZE -f csv -d gpurun_out/zcprof/pmc_fetch_$ALGO$TAG -o rank_%pid% && \
+STEPS=3 run pmc_write_$ALGO$TAG 120 --pmc WRITE_SIZE -f csv -d gpurun_out/zcprof/pmc_write_$ALGO$TAG -o rank_%pid%
