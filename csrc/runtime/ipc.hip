@@ -102,8 +102,10 @@ __device__ __forceinline__ bool block_barrier(uint32_t (*slots)[kIpcMaxRanks] /*
 
 // NR (rank count) is a template parameter: the NR remote loads are issued unconditionally
 // and back to back (no per-load branch, cdna guide §5 trap (c)).
+// ``scale`` multiplies the reduced value before the store (the fused 1/p average of a DP
+// gradient allreduce); float dtypes only, 1.0 = plain reduction (a wave-uniform branch).
 template <int DT, int OP, int NR>
-__device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v) {
+__device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v, float scale = 1.0f) {
   using E = Elem<DT>;
   using S = typename E::S;
   using A = typename E::A;
@@ -122,6 +124,12 @@ __device__ __forceinline__ u32x4 reduce_vec(const IpcPtrs& P, int64_t v) {
     __builtin_memcpy(x, &r[k], 16);
 #pragma unroll
     for (int j = 0; j < W; ++j) acc[j] = combine<DT, OP>(acc[j], E::load(x[j]));
+  }
+  if constexpr (is_float_dt<DT>()) {
+    if (scale != 1.0f) {
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = acc[j] * (A)scale;
+    }
   }
 #pragma unroll
   for (int j = 0; j < W; ++j) s[j] = E::store(acc[j]);
@@ -151,7 +159,7 @@ template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
                                                               const uint32_t* epoch_dev,
-                                                              const u32x4* __restrict__ src) {
+                                                              const u32x4* __restrict__ src, float scale) {
   constexpr int p = NR;
   epoch = resolve_epoch(epoch, epoch_dev);
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
@@ -161,7 +169,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* 
   }
   if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
-    out[v] = reduce_vec<DT, OP, NR>(P, v);
+    out[v] = reduce_vec<DT, OP, NR>(P, v, scale);
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
 }
 
@@ -170,7 +178,7 @@ template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
                                                               const uint32_t* epoch_dev,
-                                                              const u32x4* __restrict__ src) {
+                                                              const u32x4* __restrict__ src, float scale) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
   epoch = resolve_epoch(epoch, epoch_dev);
@@ -193,7 +201,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
     // zero-copy form: `out` IS this rank's registered buffer (== mine), one store per vector
     const bool zc = out == mine;
     for (int64_t v = b + off0; v < e; v += stride) {
-      u32x4 o = reduce_vec<DT, OP, NR>(P, v);
+      u32x4 o = reduce_vec<DT, OP, NR>(P, v, scale);
       mine[v] = o;
       if (!zc) out[v] = o;
     }
@@ -338,7 +346,8 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_copy_plan(IpcPtrs P, Signal
 template <int DT, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Signal* self, int rank, int64_t cb,
                                                                   int64_t soff, void* __restrict__ out, int64_t n,
-                                                                  uint32_t epoch, const uint32_t* epoch_dev) {
+                                                                  uint32_t epoch, const uint32_t* epoch_dev,
+                                                                  float scale) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
   epoch = resolve_epoch(epoch, epoch_dev);
@@ -363,6 +372,10 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < NR; ++k) fp8_fma_acc(w[k], sc[k], acc);   // rank order: deterministic
+      if (scale != 1.0f) {                                // fused average, before the re-quantisation
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] *= scale;
+      }
       float m = fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3])));
       m = wave_max(m);
       const float scale = m > 0.0f ? m / kFp8Max : 1.0f;
@@ -401,11 +414,11 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
 
 template <int DT>
 static int fp8_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t cb, int64_t soff, void* out, int64_t n,
-                  uint32_t epoch, const uint32_t* edev, int blocks, hipStream_t st) {
+                  uint32_t epoch, const uint32_t* edev, float scale, int blocks, hipStream_t st) {
 #define MP4X_FP8_CASE(N)                                                                                     \
   case N:                                                                                                    \
     hipLaunchKernelGGL((k_ipc_fp8_twoshot<DT, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, cb, \
-                       soff, out, n, epoch, edev);                                                           \
+                       soff, out, n, epoch, edev, scale);                                                    \
     return (int)hipGetLastError();
   switch (p) {
     MP4X_FP8_CASE(2) MP4X_FP8_CASE(3) MP4X_FP8_CASE(4) MP4X_FP8_CASE(5) MP4X_FP8_CASE(6) MP4X_FP8_CASE(7)
@@ -415,35 +428,36 @@ static int fp8_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t cb, i
 #undef MP4X_FP8_CASE
 }
 
-// set per call by mp4x_ipc_allreduce (host-side, single-threaded use per communicator)
-static thread_local const uint32_t* g_epoch_dev = nullptr;
-static thread_local const void* g_src = nullptr;     // fused copy-in source (nullptr: pre-staged)
+// Per-call launch options of the one-/two-shot allreduce.
+struct LaunchOpts {
+  const uint32_t* edev;   // device epoch (graph mode) or nullptr
+  const u32x4* src;       // fused copy-in source or nullptr (pre-staged / zero-copy)
+  float scale;            // applied to the reduced value (1 = none)
+};
 
 template <int DT, int OP, int NR>
 static int launch_nr(int algo, const IpcPtrs& P, Signal* self, int rank, int64_t nvec, void* out, uint32_t epoch,
-                     int blocks, hipStream_t st) {
-  const uint32_t* edev = g_epoch_dev;
-  const u32x4* src = (const u32x4*)g_src;
+                     int blocks, hipStream_t st, const LaunchOpts& o) {
   if (algo == 0)
     hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch, edev, src);
+                       (u32x4*)out, epoch, o.edev, o.src, o.scale);
   else
     hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, nvec,
-                       (u32x4*)out, epoch, edev, src);
+                       (u32x4*)out, epoch, o.edev, o.src, o.scale);
   return (int)hipGetLastError();
 }
 
 template <int DT, int OP>
 static int launch_ipc(int algo, const IpcPtrs& P, Signal* self, int rank, int p, int64_t nvec, void* out,
-                      uint32_t epoch, int blocks, hipStream_t st) {
+                      uint32_t epoch, int blocks, hipStream_t st, const LaunchOpts& o) {
   switch (p) {
-    case 2: return launch_nr<DT, OP, 2>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 3: return launch_nr<DT, OP, 3>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 4: return launch_nr<DT, OP, 4>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 5: return launch_nr<DT, OP, 5>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 6: return launch_nr<DT, OP, 6>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 7: return launch_nr<DT, OP, 7>(algo, P, self, rank, nvec, out, epoch, blocks, st);
-    case 8: return launch_nr<DT, OP, 8>(algo, P, self, rank, nvec, out, epoch, blocks, st);
+    case 2: return launch_nr<DT, OP, 2>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 3: return launch_nr<DT, OP, 3>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 4: return launch_nr<DT, OP, 4>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 5: return launch_nr<DT, OP, 5>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 6: return launch_nr<DT, OP, 6>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 7: return launch_nr<DT, OP, 7>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
+    case 8: return launch_nr<DT, OP, 8>(algo, P, self, rank, nvec, out, epoch, blocks, st, o);
     default: return MP4X_E_BADARG;
   }
 }
@@ -452,16 +466,16 @@ static int launch_ipc(int algo, const IpcPtrs& P, Signal* self, int rank, int p,
 // the RCCL or a2a schedules.
 template <int DT>
 static int ipc_dt(int op, int algo, const IpcPtrs& P, Signal* self, int rank, int p, int64_t nvec, void* out,
-                  uint32_t epoch, int blocks, hipStream_t st) {
+                  uint32_t epoch, int blocks, hipStream_t st, const LaunchOpts& o) {
   switch (op) {
-    case MP4X_SUM: return launch_ipc<DT, MP4X_SUM>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_SUM: return launch_ipc<DT, MP4X_SUM>(algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
     case MP4X_MAX:
       if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
-        return launch_ipc<DT, MP4X_MAX>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+        return launch_ipc<DT, MP4X_MAX>(algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
       return MP4X_E_UNSUPPORTED;
     case MP4X_MIN:
       if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
-        return launch_ipc<DT, MP4X_MIN>(algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+        return launch_ipc<DT, MP4X_MIN>(algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
       return MP4X_E_UNSUPPORTED;
     default: return MP4X_E_UNSUPPORTED;
   }
@@ -483,6 +497,10 @@ extern "C" int mp4x_ipc_alloc(size_t bytes, void** ptr) {
 }
 
 extern "C" int mp4x_ipc_free(void* ptr) { return (int)hipFree(ptr); }
+
+// Plain (coarse-grained) device allocation, the kind the PyTorch caching allocator makes: the
+// self-test of the zero-copy protocol runs on memory like the caller tensors it will map.
+extern "C" int mp4x_dev_alloc(size_t bytes, void** ptr) { return (int)hipMalloc(ptr, bytes); }
 
 // Pinned host word the kernels can write (mapped, coherent): *host_ptr for the CPU,
 // *dev_ptr for the kernels.  Zeroed.
@@ -575,29 +593,17 @@ extern "C" int mp4x_ipc_bump_epoch(uint32_t* epoch_dev, void* stream) {
 
 // epoch_dev == NULL: `epoch` (host counter) is used.  epoch_dev != NULL: graph-capturable form,
 // the kernel reads the epoch from device memory (bump it with mp4x_ipc_bump_epoch first).
-extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
-                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
-                                  const uint32_t* epoch_dev, void* stream);
-
-// Same, with the copy of this rank's input (`src`, 16-byte aligned) into its own buffer fused
-// into the kernel: one launch per call instead of hipMemcpyAsync + kernel.
-extern "C" int mp4x_ipc_allreduce_from(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
-                                       int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
-                                       int blocks, const uint32_t* epoch_dev, void* stream) {
-  if (!src || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
-  g_src = src;
-  int e = mp4x_ipc_allreduce(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, out, epoch, blocks, epoch_dev,
-                             stream);
-  g_src = nullptr;
-  return e;
-}
-
-extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
-                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
-                                  const uint32_t* epoch_dev, void* stream) {
-  g_epoch_dev = epoch_dev;
+// src != NULL: this rank's input (16-byte aligned) is copied into its own buffer INSIDE the
+// kernel (fused copy-in: one launch per call); NULL: already staged, or zero-copy (the data
+// pointers are the registered caller tensors and out == data_ptrs[rank]).  scale != 1: the
+// reduced value is multiplied by it before it is stored (fused average; float dtypes only).
+extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                     int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
+                                     int blocks, const uint32_t* epoch_dev, float scale, void* stream) {
   if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
-  if (((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  if (((uintptr_t)out & 15) || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
+  if (scale != 1.0f && !(dtype == MP4X_F32 || dtype == MP4X_F64 || dtype == MP4X_BF16 || dtype == MP4X_F16))
+    return MP4X_E_BADARG;
   IpcPtrs P;
   for (int k = 0; k < kIpcMaxRanks; ++k) {
     P.data[k] = k < p ? data_ptrs[k] : nullptr;
@@ -615,16 +621,25 @@ extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data
   if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
   Signal* self = (Signal*)signal_ptrs[rank];
   hipStream_t st = (hipStream_t)stream;
+  const LaunchOpts o{epoch_dev, (const u32x4*)src, scale};
   // element count per 16-byte vector is encoded in the dtype; nvec is the vector count
   switch (dtype) {
-    case MP4X_F64: return ipc_dt<MP4X_F64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
-    case MP4X_F32: return ipc_dt<MP4X_F32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
-    case MP4X_I64: return ipc_dt<MP4X_I64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
-    case MP4X_I32: return ipc_dt<MP4X_I32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
-    case MP4X_BF16: return ipc_dt<MP4X_BF16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
-    case MP4X_F16: return ipc_dt<MP4X_F16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st);
+    case MP4X_F64: return ipc_dt<MP4X_F64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
+    case MP4X_F32: return ipc_dt<MP4X_F32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
+    case MP4X_I64: return ipc_dt<MP4X_I64>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
+    case MP4X_I32: return ipc_dt<MP4X_I32>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
+    case MP4X_BF16: return ipc_dt<MP4X_BF16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
+    case MP4X_F16: return ipc_dt<MP4X_F16>(op, algo, P, self, rank, p, nvec, out, epoch, blocks, st, o);
     default: return MP4X_E_UNSUPPORTED;
   }
+}
+
+// The pre-staged form (no fused copy-in, no scale).
+extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream) {
+  return mp4x_ipc_allreduce_ex(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, nullptr, out, epoch, blocks,
+                               epoch_dev, 1.0f, stream);
 }
 
 static int ipc_prepare(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p, IpcPtrs* P) {
@@ -764,7 +779,7 @@ extern "C" int mp4x_ipc_allgather(void* const* data_ptrs, void* const* signal_pt
 // zeroed); `out` (dtype = f32 / bf16 / f16, 16-B aligned) receives n elements.
 extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
                                       int64_t cb, int64_t soff, void* out, int64_t n, uint32_t epoch, int blocks,
-                                      const uint32_t* epoch_dev, void* stream) {
+                                      const uint32_t* epoch_dev, float scale, void* stream) {
   IpcPtrs P;
   if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
   if (cb <= 0 || n <= 0 || n > (int64_t)p * cb * kQBlock || (soff & 15) || ((uintptr_t)out & 15))
@@ -779,9 +794,9 @@ extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* c
   Signal* self = (Signal*)signal_ptrs[rank];
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
-    case MP4X_F32: return fp8_nr<MP4X_F32>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
-    case MP4X_BF16: return fp8_nr<MP4X_BF16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
-    case MP4X_F16: return fp8_nr<MP4X_F16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, blocks, st);
+    case MP4X_F32: return fp8_nr<MP4X_F32>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
+    case MP4X_BF16: return fp8_nr<MP4X_BF16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
+    case MP4X_F16: return fp8_nr<MP4X_F16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
     default: return MP4X_E_UNSUPPORTED;
   }
 }

@@ -5,8 +5,11 @@ d'être: ytk-learn syncs L-BFGS / GBDT statistics with ``allreduceArray``, READM
 into flat buffers, makes every ``param.grad`` a VIEW into its bucket (no flatten/unflatten
 copies), and launches each bucket's allreduce as soon as the last gradient of the bucket
 has been accumulated — on a dedicated HIP stream, so RCCL / the IPC kernels overlap the
-rest of the backward pass.  ``finish()`` joins the streams and applies the 1/p average with
-the K1 scale kernel.
+rest of the backward pass.  The 1/p average is fused into the allreduce itself (the IPC
+kernels scale the reduced value before their final store, RCCL uses ncclAvg, the fp8 path
+scales before re-quantising), so no separate pass over the buckets runs; ``finish()`` only
+joins the streams.  Bucket buffers are registered with the communicator, so the two-shot
+runs zero-copy on them.
 
 Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X) and RCCL splits a
 message over channels/links; buckets of 32-128 MiB keep every link busy while leaving
@@ -30,6 +33,7 @@ class _Bucket:
         self.buffer = torch.zeros(n, device=device, dtype=dtype)
         self.pending = len(params)
         self.event = None
+        self.averaged = False
         off = 0
         self.views = []
         for p in params:
@@ -68,6 +72,9 @@ class GradientSynchronizer:
                 p.register_post_accumulate_grad_hook(self._hook)
         self.cuda = self.buckets[0].buffer.is_cuda
         self.stream = torch.cuda.Stream() if self.cuda else None
+        if self.cuda and self.p > 1 and hasattr(self.comm, "registerBuffer"):
+            for b in self.buckets:        # collective; False on every rank alike (then staged)
+                self.comm.registerBuffer(b.buffer)
         self._launched: List[_Bucket] = []
         self.tuned = {}
         if autotune:
@@ -105,7 +112,12 @@ class GradientSynchronizer:
             ev.record()                          # gradients of this bucket are complete on the compute stream
             with torch.cuda.stream(self.stream):
                 self.stream.wait_event(ev)
-                self.comm.allreduceArray(b.buffer, self.operand, op, 0, b.buffer.numel())
+                if self.average and b.buffer.is_floating_point() and hasattr(self.comm, "device"):
+                    # average fused into the collective's final write (no extra HBM pass)
+                    self.comm.device.allreduce(b.buffer, 0, b.buffer.numel(), op, self.operand, scale=1.0 / self.p)
+                    b.averaged = True
+                else:
+                    self.comm.allreduceArray(b.buffer, self.operand, op, 0, b.buffer.numel())
         else:
             self.comm.allreduceArray(b.buffer, self.operand, op, 0, b.buffer.numel())
         self._launched.append(b)
@@ -119,14 +131,11 @@ class GradientSynchronizer:
             torch.cuda.current_stream().wait_stream(self.stream)
         if self.average and self.p > 1:
             for b in self.buckets:
-                if b.buffer.is_cuda and b.buffer.dtype in (torch.float32, torch.bfloat16, torch.float16,
-                                                           torch.float64):
-                    from ..ops.device_ops import scale_
-                    scale_(b.buffer, b.buffer, 1.0 / self.p)
-                else:
-                    b.buffer.mul_(1.0 / self.p)
+                if not b.averaged:
+                    b.buffer.mul_(1.0 / self.p)     # host buffers / integer buckets only
         for b in self.buckets:
             b.pending = len(b.params)
+            b.averaged = False
         self._launched = []
 
     def zero_grad(self):

@@ -47,8 +47,9 @@ class TorchColl:
         self.gather_into_tensor_ok = backend != "gloo"
         self.reduce_scatter_ok = backend != "gloo"
 
-    def all_reduce(self, t, code):
-        dist.all_reduce(t, op=_RCCL_OPS[code], group=self.pg)
+    def all_reduce(self, t, code, avg: bool = False):
+        """``avg``: SUM then divide by the group size inside the collective (ncclAvg)."""
+        dist.all_reduce(t, op=dist.ReduceOp.AVG if avg else _RCCL_OPS[code], group=self.pg)
 
     def reduce(self, t, dst, code):
         dist.reduce(t, dst=dst, op=_RCCL_OPS[code], group=self.pg)
@@ -137,11 +138,13 @@ class LoopbackColl:
         self.hub.bar.wait()
         return out
 
-    def all_reduce(self, t, code):
+    def all_reduce(self, t, code, avg: bool = False):
         xs = self._exchange(t.clone())
         acc = xs[0].clone()
         for x in xs[1:]:
             acc = _combine(code, acc, x)
+        if avg:
+            acc = acc / self.p
         t.copy_(acc)
         self._sync()
 

@@ -389,15 +389,19 @@ class DeviceEngine:
             step("allgather_4MiB", ag)
         step("broadcast_1MiB", bcast)
         if self._zc:
-            t, exp = pattern(n4m)
-            if inst.register(t):
-                def zc():
-                    inst.allreduce_registered(t, op, inst.registered(t))
-                    return lambda: int((t != exp).sum())
-                step("zero_copy_twoshot_4MiB", zc)
-                inst.deregister(t)
-            else:
-                fails.append("register: refused")
+            # on a dedicated plain allocation (a tensor from the caching allocator may sit in a
+            # segment too large to map, see ipc.IPC_OPEN_MAX)
+            try:
+                nbad = inst.selftest_zero_copy(n4m)
+                if nbad:
+                    fails.append(f"zero_copy_twoshot_4MiB: {'setup failed' if nbad < 0 else f'{nbad} wrong elements'}")
+                torch.cuda.synchronize(dev)
+                code = inst.host_error()
+                inst.raise_if_failed()
+                if code:
+                    fails.append(f"zero_copy_twoshot_4MiB: barrier timeout {code}")
+            except Exception as e:   # noqa: BLE001
+                fails.append(f"zero_copy_twoshot_4MiB: {type(e).__name__}: {e}")
         try:
             ipcm.check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SPIN_S", "10"))), "set_spin")
         except Exception as e:   # noqa: BLE001
@@ -543,10 +547,14 @@ class DeviceEngine:
 
     # ================================================================== allreduce
     def allreduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand=None, small: bool = False,
-                  out: Optional[torch.Tensor] = None):
+                  out: Optional[torch.Tensor] = None, scale: float = 1.0):
         """In-place allreduce of ``arr[frm:to]``; with ``out`` the result goes to ``out[frm:to]``
         and ``arr`` is left untouched (the staged IPC kernels write ``out`` directly; other
-        schedules copy into ``out`` first and run in place there)."""
+        schedules copy into ``out`` first and run in place there).
+
+        ``scale`` (float dtypes): the result is multiplied by it — the 1/p average of a DP
+        gradient sync fused into the collective's own final write (IPC kernels, fp8 requantise)
+        or RCCL's ncclAvg, instead of a separate pass over the buffer."""
         flat = self._flat(arr)
         view = flat[frm:to]
         if out is not None:
@@ -566,7 +574,9 @@ class DeviceEngine:
                     (not torch.cuda.is_current_stream_capturing() or self._ipc_obj._epoch_dev is not None):
                 from .ipc import ONESHOT, TWOSHOT
                 self._count("allreduce." + algo + ".out")
-                self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT, out=oview)
+                self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT, out=oview,
+                                        scale=self._fused_scale(scale, view))
+                self._post_scale(oview, scale, fused=True)
                 return out
             if view.is_cuda:   # the local copy runs through the K1 kernel (NIN = 1)
                 from ..ops.device_ops import reduce_
@@ -578,8 +588,23 @@ class DeviceEngine:
                 and self._ipc_obj.registered(view) is not None:
             algo = "ipc2z"      # registered on this rank (registration is collective): zero-copy
         self._count("allreduce." + algo)
-        self._run_allreduce(algo, view, op)
+        fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view))
+        self._post_scale(view, scale, fused)
         return arr
+
+    @staticmethod
+    def _fused_scale(scale: float, view: torch.Tensor) -> float:
+        return float(scale) if view.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.float16) else 1.0
+
+    def _post_scale(self, view: torch.Tensor, scale: float, fused: bool) -> None:
+        """The scale a schedule could not fuse: one K1 scale pass (device) / in-place multiply."""
+        if scale == 1.0 or (fused and self._fused_scale(scale, view) == scale):
+            return
+        if view.is_cuda and view.dtype in (torch.float32, torch.float64, torch.bfloat16, torch.float16):
+            from ..ops.device_ops import scale_
+            scale_(view, view, float(scale))
+        else:
+            view.mul_(scale)
 
     # ------------------------------------------------------------------ registered buffers
     def register_buffer(self, t: torch.Tensor) -> bool:
@@ -595,15 +620,16 @@ class DeviceEngine:
         if self._ipc_obj is not None:
             self._ipc_obj.deregister(self._flat(t))
 
-    def _run_allreduce(self, algo: str, view: torch.Tensor, op) -> None:
+    def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
+        """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
         if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "ipc2z":
             peers = self._ipc_obj.registered(view) if self._zc else None
             if peers is not None and (not torch.cuda.is_current_stream_capturing()
                                       or self._ipc_obj._epoch_dev is not None):
-                self._ipc_obj.allreduce_registered(view, op, peers)
-                return
+                self._ipc_obj.allreduce_registered(view, op, peers, scale=scale)
+                return True
             algo = "ipc2"        # not registered (on this rank): the staged two-shot
         if algo in ("ipc1", "ipc2", "ipc2p") and torch.cuda.is_current_stream_capturing():
             nb = view.numel() * view.element_size()
@@ -611,7 +637,10 @@ class DeviceEngine:
             if inst is None or inst._epoch_dev is None:
                 algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
-            self.coll.all_reduce(view, op.code)
+            avg = scale != 1.0 and abs(scale * self.p - 1.0) < 1e-9 and op.code == OpCode.SUM \
+                and self.backend == "nccl"
+            self.coll.all_reduce(view, op.code, avg=avg)          # ncclAvg: RCCL's fused average
+            return avg
         elif algo.startswith("rccl_c"):
             self.rccl_variant(int(algo[6:])).all_reduce(view, op.code)
         elif algo in ("ipc1", "ipc2", "ipc2p"):
@@ -619,7 +648,8 @@ class DeviceEngine:
             nbytes = view.numel() * view.element_size()
             inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
             inst.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT,
-                           overlap=True if algo == "ipc2p" else None)
+                           overlap=True if algo == "ipc2p" else None, scale=scale)
+            return True
         elif algo == "rhd":
             self._allreduce_rhd(view, op)
         elif algo == "zs":
@@ -628,9 +658,9 @@ class DeviceEngine:
             inst = self._ipc_fp8(view)
             if inst is not None:
                 self._count("allreduce.fp8.ipc")
-                inst.allreduce_fp8(view)          # fused quant-on-the-links two-shot over xGMI
-            else:
-                self._allreduce_fp8(view)
+                inst.allreduce_fp8(view, scale=scale)   # fused quant-on-the-links two-shot over xGMI
+                return True
+            self._allreduce_fp8(view)
         elif algo == "bf16":
             # 2x-compressed wire: bf16 all-to-all, f32 accumulation inside the K1 kernel
             # (bf16 inputs, one rounding), bf16 all-gather, widened back in place
@@ -639,6 +669,7 @@ class DeviceEngine:
             view.copy_(w)
         else:
             self._allreduce_a2a(view, op)
+        return False
 
     def _ipc_fp8(self, view: torch.Tensor):
         """The IPC instance that runs the fused fp8 two-shot for ``view``, or None (RCCL form).

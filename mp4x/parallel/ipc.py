@@ -34,6 +34,7 @@ native.register_signatures({
     "mp4x_ipc_set_host_error": (c_int, [c_void_p, c_void_p]),
     "mp4x_ipc_set_spin": (c_int, [ctypes.c_double]),
     "mp4x_mem_range": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
+    "mp4x_dev_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
     "mp4x_ipc_handle_size": (c_int, []),
     "mp4x_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
     "mp4x_ipc_open_handle": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
@@ -41,13 +42,13 @@ native.register_signatures({
     "mp4x_ipc_read_error": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32)]),
     "mp4x_ipc_error_word": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_uint32), c_int, c_void_p]),
     "mp4x_ipc_fp8_allreduce": (c_int, [c_int, PP, PP, c_int, c_int, c_int64, c_int64, c_void_p, c_int64,
-                                       ctypes.c_uint32, c_int, c_void_p, c_void_p]),
+                                       ctypes.c_uint32, c_int, c_void_p, ctypes.c_float, c_void_p]),
     "mp4x_memset_async": (c_int, [c_void_p, c_int, c_size_t, c_void_p]),
     "mp4x_memcpy_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_ipc_allreduce": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, ctypes.c_uint32,
                                    c_int, c_void_p, c_void_p]),
-    "mp4x_ipc_allreduce_from": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
-                                        ctypes.c_uint32, c_int, c_void_p, c_void_p]),
+    "mp4x_ipc_allreduce_ex": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
+                                      ctypes.c_uint32, c_int, c_void_p, ctypes.c_float, c_void_p]),
     "mp4x_ipc_reduce_scatter_from": (c_int, [c_int, c_int, PP, PP, c_int, c_int, ctypes.POINTER(c_int64),
                                              ctypes.POINTER(c_int64), c_void_p, c_void_p, ctypes.c_uint32, c_int,
                                              c_void_p, c_void_p]),
@@ -67,6 +68,10 @@ _RESIDENT_BLOCKS = 1024
 
 ONESHOT, TWOSHOT = 0, 1
 ZC_TAG = 0x80000000      # epoch tag of the zero-copy protocol (csrc/runtime/ipc.hip kZcTag)
+# hipIpcOpenMemHandle of an allocation of 2^31 bytes or more never returns on this ROCm
+# (measured: 2.0 GB opens in 0.1 ms, 2 GiB hangs — profiles/r2/ipc_open_probe.jsonl), so
+# registration refuses such allocations (every rank alike): the staged kernels run instead.
+IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64}
 
 
@@ -211,7 +216,7 @@ class IpcAllreduce:
         return op.code in (OpCode.MAX, OpCode.MIN) and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
 
     def allreduce(self, view: torch.Tensor, op, algo: int = ONESHOT, out: Optional[torch.Tensor] = None,
-                  blocks: int = 0, overlap: Optional[bool] = None) -> torch.Tensor:
+                  blocks: int = 0, overlap: Optional[bool] = None, scale: float = 1.0) -> torch.Tensor:
         """In place (or into ``out``) allreduce of a contiguous device tensor.
 
         ``overlap`` (messages larger than the buffer): pipeline half-buffer pieces with the
@@ -231,7 +236,7 @@ class IpcAllreduce:
             # an oddly offset output on THIS rank must not change the protocol the peers run:
             # reduce into an aligned temporary (allocator-aligned) and copy out
             tmp = torch.empty(view.numel(), dtype=view.dtype, device=view.device)
-            self.allreduce(view, op, algo, out=tmp, blocks=blocks, overlap=overlap)
+            self.allreduce(view, op, algo, out=tmp, blocks=blocks, overlap=overlap, scale=scale)
             out.copy_(tmp)
             return out
         dt = int(dtype_of_torch(view.dtype))
@@ -243,7 +248,7 @@ class IpcAllreduce:
         if overlap is None:
             overlap = self._overlap_default
         if total > self.nbytes and overlap and not torch.cuda.is_current_stream_capturing():
-            return self._allreduce_pipelined(src, dst, total, dt, op, algo, blocks, out)
+            return self._allreduce_pipelined(src, dst, total, dt, op, algo, blocks, out, scale)
         piece = self.nbytes - self.nbytes % 16
         off = 0
         st = stream_ptr()
@@ -261,18 +266,14 @@ class IpcAllreduce:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
-            if fused:
-                check(self.lib.mp4x_ipc_allreduce_from(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
-                                                       self.rank, self.p, m, src.data_ptr() + off, dst.data_ptr() + off,
-                                                       self.epoch, blocks, edev, st), "mp4x_ipc_allreduce_from")
-            else:
-                check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
-                                                  self.rank, self.p, m, dst.data_ptr() + off, self.epoch, blocks,
-                                                  edev, st), "mp4x_ipc_allreduce")
+            check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
+                                                 self.rank, self.p, m, src.data_ptr() + off if fused else None,
+                                                 dst.data_ptr() + off, self.epoch, blocks, edev, scale, st),
+                  "mp4x_ipc_allreduce")
             off += m
         return out
 
-    def _allreduce_pipelined(self, src, dst, total, dt, op, algo, blocks, out):
+    def _allreduce_pipelined(self, src, dst, total, dt, op, algo, blocks, out, scale=1.0):
         """Messages larger than the buffer: two half-buffers, the input copy of piece i+1 (side
         stream, HBM-bound) overlaps the xGMI-bound kernel of piece i.
 
@@ -307,8 +308,8 @@ class IpcAllreduce:
             else:
                 self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
             pp = self._pp_hi[0] if slot else self._pp_data[0]
-            check(self.lib.mp4x_ipc_allreduce(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
-                                              dst.data_ptr() + off, self.epoch, blocks, edev, ms),
+            check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
+                                                 None, dst.data_ptr() + off, self.epoch, blocks, edev, scale, ms),
                   "mp4x_ipc_allreduce")
             kd = torch.cuda.Event()
             kd.record(main)
@@ -344,6 +345,8 @@ class IpcAllreduce:
                 raise Mp4jException("register needs a contiguous, 16-byte aligned device tensor of 16-byte multiple size")
             base, size = c_void_p(), c_size_t()
             check(self.lib.mp4x_mem_range(c_void_p(t.data_ptr()), ctypes.byref(base), ctypes.byref(size)), "mem_range")
+            if size.value > IPC_OPEN_MAX:
+                raise Mp4jException(f"allocation of {size.value} bytes is above the IPC open limit ({IPC_OPEN_MAX})")
             h = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(base, h), "ipc_get_handle(registered)")
             blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local)
@@ -393,29 +396,88 @@ class IpcAllreduce:
                 return [q + d for q in peers]
         return None
 
-    def allreduce_registered(self, view: torch.Tensor, op, peers) -> torch.Tensor:
+    def allreduce_registered(self, view: torch.Tensor, op, peers, scale: float = 1.0) -> torch.Tensor:
         """In-place two-shot straight on the registered tensors (see :meth:`register`): ONE
         kernel, no staging and no pieces, whatever the size."""
-        self.raise_if_failed()
         total = view.numel() * view.element_size()
         if total % 16 or view.data_ptr() % 16:
             raise Mp4jException("zero-copy IPC allreduce needs 16-byte aligned, 16-byte multiple views")
-        st = stream_ptr()
         if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        self.allreduce_registered_ptrs(view.data_ptr(), total, op, peers, view.dtype, scale)
+        return view
+
+    def selftest_zero_copy(self, n: int) -> int:
+        """Collective exact-pattern run of the zero-copy two-shot (f32 SUM, ``n`` elements) on a
+        dedicated plain device allocation per rank, mapped into every peer like a registered
+        tensor.  Returns the number of wrong elements on this rank (-1: setup failed here)."""
+        nbytes = n * 4
+        ptr, opened, err = c_void_p(), [], None
+        hs = self.lib.mp4x_ipc_handle_size()
+        try:
+            check(self.lib.mp4x_dev_alloc(nbytes, ctypes.byref(ptr)), "dev_alloc")
+            h = ctypes.create_string_buffer(hs)
+            check(self.lib.mp4x_ipc_get_handle(ptr, h), "ipc_get_handle(selftest)")
+            blob = h.raw
+        except Exception as e:   # noqa: BLE001
+            err, blob = str(e), None
+        allh = self.comm.server.call("allgather_obj", self.rank, (blob, err))
+        bad = -1 if any(e for _, e in allh) else 0
+        peers = []
+        if bad == 0:
+            try:
+                for r, (b, _) in enumerate(allh):
+                    if r == self.rank:
+                        peers.append(ptr.value)
+                        continue
+                    q = c_void_p()
+                    check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(b), hs), ctypes.byref(q)),
+                          "ipc_open_handle(selftest)")
+                    opened.append(q)
+                    peers.append(q.value)
+            except Exception:   # noqa: BLE001
+                bad = -1
+        oks = self.comm.server.call("allgather_obj", self.rank, bad)
+        if all(o == 0 for o in oks):
+            from ..operators import Operators, for_dtype, DType
+            op = for_dtype(Operators.Float.SUM, DType.F32)
+            i = torch.arange(n, device="cuda", dtype=torch.int32) % 13
+            mine = (i + self.rank).float()
+            st = stream_ptr()
+            check(self.lib.mp4x_memcpy_async(ptr.value, mine.data_ptr(), nbytes, st), "selftest fill")
+            self.comm.server.call("barrier", self.rank)     # (the fill is stream-ordered before the kernel)
+            self.allreduce_registered_ptrs(ptr.value, nbytes, op, peers, torch.float32)
+            got = torch.empty(n, device="cuda")
+            check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr.value, nbytes, st), "selftest read")
+            torch.cuda.synchronize()
+            exp = (i * self.p + self.p * (self.p - 1) // 2).float()
+            bad = int((got != exp).sum())
+        elif bad == 0:
+            bad = -1
+        torch.cuda.synchronize()
+        self.comm.server.call("barrier", self.rank)         # every peer is done reading before unmapping
+        for q in opened:
+            self.lib.mp4x_ipc_close_handle(q)
+        if ptr:
+            self.lib.mp4x_ipc_free(ptr)
+        return bad
+
+    def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0) -> None:
+        """The zero-copy two-shot on raw pointers (``dst`` = this rank's buffer, ``peers`` = every
+        rank's mapped buffer)."""
+        self.raise_if_failed()
+        st = stream_ptr()
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
         if edev is not None:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
             self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
-        blocks = 0
-        if self.max_blocks:
-            blocks = max(1, min(self.max_blocks, -(-total // 16 // 512)))
+        blocks = max(1, min(self.max_blocks, -(-total // 16 // 512))) if self.max_blocks else 0
         pp = ptr_array(peers)
-        check(self.lib.mp4x_ipc_allreduce(TWOSHOT, int(dtype_of_torch(view.dtype)), int(op.code), pp[0],
-                                          self._pp_sig[0], self.rank, self.p, total, view.data_ptr(),
-                                          self.epoch | ZC_TAG, blocks, edev, st), "mp4x_ipc_allreduce(zero-copy)")
-        return view
+        check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
+                                             self._pp_sig[0], self.rank, self.p, total, None, dst,
+                                             self.epoch | ZC_TAG, blocks, edev, scale, st),
+              "mp4x_ipc_allreduce(zero-copy)")
 
     # ---------------------------------------------------------------- RS / AG over ragged ranges
     # Results are produced inside the staging buffer (always 16-byte aligned) and copied out, so
@@ -730,7 +792,7 @@ class IpcAllreduce:
             raise Mp4jException("IPC buffer too small for the fp8 two-shot")
         return int(cb)
 
-    def allreduce_fp8(self, view: torch.Tensor) -> torch.Tensor:
+    def allreduce_fp8(self, view: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
         """In-place SUM allreduce with the block-scaled e4m3 codec on the xGMI links, one fused
         kernel per piece (csrc/runtime/ipc.hip ``k_ipc_fp8_twoshot``): quantise this rank's
         piece into its own buffer (K6), then pull + dequantise + f32-sum + requantise the own
@@ -741,7 +803,7 @@ class IpcAllreduce:
             raise Mp4jException("fp8 IPC allreduce needs a contiguous f32/bf16/f16 tensor, n % 4 == 0")
         self.raise_if_failed()
         if view.data_ptr() % 16:
-            self._aligned(view, self.allreduce_fp8)
+            self._aligned(view, lambda t: self.allreduce_fp8(t, scale))
             return view
         Q = self.QBLOCK
         n = view.numel()
@@ -766,7 +828,7 @@ class IpcAllreduce:
             edev = self._next_epoch(st)
             check(self.lib.mp4x_ipc_fp8_allreduce(dt, self._pp_data[0], self._pp_sig[0], self.rank, self.p, cb, soff,
                                                   base + off * es, m, self.epoch, self._blocks_for_waves(cb), edev,
-                                                  st), "mp4x_ipc_fp8_allreduce")
+                                                  scale, st), "mp4x_ipc_fp8_allreduce")
             off += m
         return view
 

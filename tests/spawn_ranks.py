@@ -11,9 +11,16 @@ import tempfile
 import traceback
 
 
-def _worker(fn, port, args, env, threads, q):
+def _worker(fn, port, args, env, threads, q, dump_after):
     try:
+        import faulthandler
+        import sys
+        faulthandler.dump_traceback_later(dump_after, exit=False, file=sys.stderr)   # stacks if stuck
         os.environ.update(env)
+        if os.environ.get("MP4X_TEST_LOG"):
+            import logging
+            logging.basicConfig(level=logging.INFO, stream=sys.stderr,
+                                format="%(asctime)s %(name)s %(levelname)s %(message)s")
         import torch
         torch.cuda.set_device(0)
         from mp4x import ProcessCommSlave, ThreadCommSlave
@@ -37,7 +44,8 @@ def run_spawn(p, fn, args=(), env=None, timeout=240, threads=0):
     m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(fn, m.port, args, e, threads, q)) for _ in range(p)]
+    procs = [ctx.Process(target=_worker, args=(fn, m.port, args, e, threads, q, min(100, max(10, timeout - 60))))
+             for _ in range(p)]
     for pr in procs:
         pr.start()
     out = {}

@@ -210,3 +210,46 @@ def test_out_of_place_allreduce_writes_out_directly():
     for r, (untouched, ok, stats) in out.items():
         assert untouched and ok, (r, stats)
         assert any(k.endswith(".out") for k in stats), stats
+
+
+# ------------------------------------------------------------------ DDP: fused average, registered buckets
+def _ddp_fn(comm):
+    from mp4x.models.mlp import train_dp
+    losses = train_dp(comm, steps=6, global_batch=48, device="cuda", bucket_mb=0.01)
+    return losses, dict(comm.device.stats)
+
+
+def test_ddp_fused_average_on_registered_buckets():
+    """The DP MLP on GPU: the 1/p average is applied inside the IPC kernels (no separate scale
+    pass) on zero-copy registered buckets, and training matches single-process training."""
+    import numpy as np
+    from mp4x.models.mlp import train_single
+    ref = train_single(steps=6, global_batch=48, device="cuda")
+    out = run_spawn(2, _ddp_fn)
+    for r, (losses, stats) in out.items():
+        np.testing.assert_allclose(losses, ref, rtol=2e-4, atol=1e-5)
+        assert stats.get("allreduce.ipc2z", 0) >= 6 or stats.get("allreduce.ipc1", 0) >= 6, stats
+
+
+def _scale_fn(comm):
+    from mp4x import Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    res = {}
+    for algo, n in (("ipc1", 4096), ("ipc2", 1 << 18), ("ipc2z", 1 << 18), ("rccl", 4096), ("a2a", 4096)):
+        x = _pattern(n, r)
+        if algo == "ipc2z":
+            assert comm.registerBuffer(x)
+        exp = _expect(n, p) * 0.25
+        eng.algo = algo
+        eng.allreduce(x, 0, n, Operators.Float.SUM, scale=0.25)
+        eng.algo = "auto"
+        torch.cuda.synchronize()
+        res[algo] = float((x - exp).abs().max())
+    return res
+
+
+def test_allreduce_scale_every_schedule():
+    out = run_spawn(2, _scale_fn)
+    for r, res in out.items():
+        assert all(v == 0.0 for v in res.values()), (r, res)
