@@ -491,8 +491,9 @@ class DeviceEngine:
         if kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
             if nbytes <= self.ipc_oneshot_max:
                 return "ipc1"
-            if nbytes <= self.ipc_twoshot_max:
-                return "ipc2"
+            if nbytes <= self.ipc_twoshot_max or (self.backend != "nccl" and self.device.type == "cuda"
+                                                  and os.environ.get("MP4X_DM_LARGE", "auto") != "rccl"):
+                return "ipc2"     # (no RCCL underneath: the IPC two-shot takes every size)
         if self.a2a_bytes and nbytes >= self.a2a_bytes:
             return "a2a"
         return "rccl"
@@ -1291,9 +1292,12 @@ class DeviceEngine:
         :meth:`autotune_allgather` for this (dtype, op, size class); None = RCCL."""
         if self.algo in ("ipc2", "ipc"):
             return "ipc" if self.ipc_enabled and (op is None or self._ipc_ok(op, whole.dtype, 16)) else None
-        if self.algo not in ("", "auto") or not self._tuned:
+        if self.algo not in ("", "auto"):
             return None
-        return self._tuned.get(self._rsag_key(kind, whole, op))
+        t = self._tuned.get(self._rsag_key(kind, whole, op)) if self._tuned else None
+        if t is None and self._dm_large_ok(whole) and (op is None or self._ipc_ok(op, whole.dtype, 16)):
+            return "ipc"     # no RCCL underneath (see _dm_large_ok): the piecewise IPC kernels
+        return t
 
     @staticmethod
     def _rsag_key(kind: str, whole: torch.Tensor, op) -> tuple:
@@ -1329,9 +1333,27 @@ class DeviceEngine:
                     self._ipc_obj.broadcast(flat, frm, to, root):
                 self._count("broadcast.ipc")
                 return arr
+            if self._dm_large_ok(flat) and self.ipc_large().broadcast_large(flat, frm, to, root):
+                self._count("broadcast.ipc_large")
+                return arr
             self._count("broadcast")
             self.coll.broadcast(flat[frm:to], root)
         return arr
+
+    def _dm_large_ok(self, flat: torch.Tensor) -> bool:
+        """Piecewise IPC copy plans for broadcast / scatter / gather / all-gather above the
+        direct tier.  ``MP4X_DM_LARGE``: ``auto`` (default) = when the transport is not RCCL
+        (gloo standing in on GPU tensors moves device data through the host: 1-3 s per 80 MB in
+        the one-GPU rehearsals), or when ``MP4X_DEVICE_ALGO=ipc2``; ``ipc`` = always; ``rccl`` =
+        never.  Rank-independent (environment and backend only)."""
+        mode = os.environ.get("MP4X_DM_LARGE", "auto").lower()
+        if mode == "rccl" or not self.ipc_enabled or not flat.is_cuda:
+            return False
+        if flat.is_cuda and torch.cuda.is_current_stream_capturing():
+            return False
+        if mode != "ipc" and self.backend == "nccl" and self.algo not in ("ipc2", "ipc"):
+            return False
+        return self.ipc() is not None and self.ipc_large() is not None
 
     def _ipc_small_ok(self, flat: torch.Tensor, nbytes: int) -> bool:
         """The IPC copy-plan tier for broadcast / scatter / gather: up to the two-shot size, schedule
@@ -1358,6 +1380,11 @@ class DeviceEngine:
             self._count("reduce.ipc1" if one else "reduce.ipc2")
             self._ipc_obj.allreduce(view, op, algo=ONESHOT if one else TWOSHOT)
             return arr
+        if self.algo in ("", "auto") and self._ipc_ok(op, view.dtype, nbytes) and self._dm_large_ok(flat):
+            from .ipc import TWOSHOT          # no RCCL underneath: the piecewise IPC two-shot
+            self._count("reduce.ipc2")
+            self.ipc_large().allreduce(view, op, algo=TWOSHOT)
+            return arr
         if self.algo != "composite" and self.select("reduce", nbytes, op, view.dtype) == "rccl":
             self._count("reduce.rccl")
             self.coll.reduce(view, root, op.code)
@@ -1376,6 +1403,9 @@ class DeviceEngine:
                 self._ipc_obj.gather(flat, froms, tos, root):
             self._count("gather.ipc")
             return arr
+        if self._dm_large_ok(flat) and self.ipc_large().gather_large(flat, froms, tos, root):
+            self._count("gather.ipc_large")
+            return arr
         self._count("gather")
         if r == root:
             self.coll.p2p([], [(flat[froms[j]:tos[j]], j) for j in range(self.p) if j != r and tos[j] > froms[j]])
@@ -1389,6 +1419,9 @@ class DeviceEngine:
         if self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
                 self._ipc_obj.scatter(flat, froms, tos, root):
             self._count("scatter.ipc")
+            return arr
+        if self._dm_large_ok(flat) and self.ipc_large().scatter_large(flat, froms, tos, root):
+            self._count("scatter.ipc_large")
             return arr
         self._count("scatter")
         if r == root:

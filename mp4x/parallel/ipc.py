@@ -696,6 +696,74 @@ class IpcAllreduce:
             self._plan([(froms[r] * es // 16, 0, lens[r], 0)], [], base, None, grid)
         return True
 
+    # ---------------------------------------------------------------- piecewise large bcast / scatter / gather
+    # Any size through the buffer, one copy-plan launch per piece.  Piece i moves slab i of every
+    # segment (the same per-segment slab on every rank: grids and piece counts come from the
+    # shared ranges only).  The receivers pull every peer's slab at once (all links busy).
+    def broadcast_large(self, view: torch.Tensor, frm: int, to: int, root: int) -> bool:
+        es = view.element_size()
+        if to <= frm or not self._vec_ok(view, (frm, to)):
+            return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.broadcast_large(t, frm, to, root))
+        base = view.data_ptr()
+        L, off, s = (to - frm) * es // 16, frm * es // 16, self.nbytes // 16
+        for o in range(0, L, s):
+            m = min(s, L - o)
+            if self.rank == root:
+                self._plan([(off + o, 0, m, 0)], [], base, None, m)
+            else:
+                self._plan([], [(0, off + o, m, root)], None, base, m)
+        return True
+
+    def scatter_large(self, view: torch.Tensor, froms, tos, root: int) -> bool:
+        es = view.element_size()
+        p, r = self.p, self.rank
+        if not self._vec_ok(view, list(froms) + list(tos)):
+            return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.scatter_large(t, froms, tos, root))
+        lens = [(t - f) * es // 16 for f, t in zip(froms, tos)]
+        others = [j for j in range(p) if j != root]
+        s = (self.nbytes // 16) // max(1, len(others))          # slab per segment per piece
+        slot = {j: k * s for k, j in enumerate(others)}
+        base = view.data_ptr()
+        for i in range(-(-max([lens[j] for j in others] or [0]) // s)):
+            ln = {j: max(0, min(lens[j] - i * s, s)) for j in others}
+            grid = max(ln.values())
+            if grid == 0:
+                continue
+            if r == root:
+                self._plan([(froms[j] * es // 16 + i * s, slot[j], ln[j], 0) for j in others if ln[j]], [], base,
+                           None, grid)
+            else:
+                self._plan([], [(slot[r], froms[r] * es // 16 + i * s, ln[r], root)] if ln[r] else [], None, base,
+                           grid)
+        return True
+
+    def gather_large(self, view: torch.Tensor, froms, tos, root: int) -> bool:
+        es = view.element_size()
+        p, r = self.p, self.rank
+        if not self._vec_ok(view, list(froms) + list(tos)):
+            return False
+        if view.data_ptr() % 16:
+            return self._aligned(view, lambda t: self.gather_large(t, froms, tos, root))
+        lens = [(t - f) * es // 16 for f, t in zip(froms, tos)]
+        others = [j for j in range(p) if j != root]
+        s = self.nbytes // 16                                    # each rank stages one slab
+        base = view.data_ptr()
+        for i in range(-(-max([lens[j] for j in others] or [0]) // s)):
+            ln = {j: max(0, min(lens[j] - i * s, s)) for j in others}
+            grid = max(ln.values())
+            if grid == 0:
+                continue
+            if r == root:
+                self._plan([], [(0, froms[j] * es // 16 + i * s, ln[j], j) for j in others if ln[j]], None, base,
+                           grid)
+            else:
+                self._plan([(froms[r] * es // 16 + i * s, 0, ln[r], 0)] if ln[r] else [], [], base, None, grid)
+        return True
+
     # ---------------------------------------------------------------- piecewise large RS / AG
     # Messages beyond the staging buffer (e.g. the ZeRO reduce-scatter + all-gather of a 4 GB
     # bf16 tensor, BASELINE config 3): piece i covers slab i of EVERY rank's segment, staged at
