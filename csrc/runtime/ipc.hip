@@ -25,6 +25,7 @@
 //    error word and exits instead of hanging the GPU;
 //  * data buffers are uncached as well, so remote reads never see stale L2 lines.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "../kernels/common.hpp"
 #include "../kernels/fp8.hpp"
@@ -343,8 +344,117 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_copy_plan(IpcPtrs P, Signal
 // buffers: q bytes [0, M) then f32 scales at `soff` bytes, one per quant block; block j of chunk
 // k is global quant block k * cb + j.  Block b of every rank visits the same chunk-relative j
 // values in both phases, so the per-block barriers are the two-shot's.
+// Wide form: every lane moves 16 bytes (16 e4m3 values) per peer per step, so one wave covers
+// FOUR quant blocks (lanes 16g..16g+15 hold block g) and a block's amax is a 16-lane reduction;
+// the four scales a wave needs sit in one 16-byte span, so the scale load is one request per
+// wave.  Per element the arithmetic (rank-ordered FMAs, amax, e4m3 rounding) is the K6 codec's,
+// so the result stays bit-identical to quantise -> dequant-reduce-requant -> dequantise.
+__device__ __forceinline__ float group16_max(float v) {
+#pragma unroll
+  for (int o = 8; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));   // stays inside the 16-lane group
+  return v;
+}
+
 template <int DT, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Signal* self, int rank, int64_t cb,
+                                                                  int64_t soff, void* __restrict__ out, int64_t n,
+                                                                  uint32_t epoch, const uint32_t* epoch_dev,
+                                                                  float scale) {
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  const int lane = threadIdx.x & 63;
+  const int g = lane >> 4;                 // quant block of this lane within the wave's 4
+  const int sub = lane & 15;               // 16-byte slot inside the 256-byte block
+  constexpr int kWaves = kIpcThreads / 64;
+  const int64_t w0 = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  const int64_t nquad = (cb + 3) / 4;      // wave steps per chunk
+  {
+    u32x4* myq = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+    float* mys = reinterpret_cast<float*>(reinterpret_cast<char*>(myq) + soff);
+    for (int64_t t = w0; t < nquad; t += nw) {
+      const int64_t j = t * 4 + g;                       // chunk-relative quant block
+      const bool live = j < cb;
+      const int64_t b = (int64_t)rank * cb + (live ? j : 0);   // global quant block
+      u32x4 w[NR];
+      float sc[NR];
+#pragma unroll
+      for (int k = 0; k < NR; ++k) {                      // every peer's 16 bytes in flight at once
+        const u32x4* q = reinterpret_cast<const u32x4*>(P.data[k]);
+        w[k] = live ? q[b * 16 + sub] : u32x4{0u, 0u, 0u, 0u};
+        sc[k] = live ? reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b] : 0.0f;
+      }
+      float acc[4][4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0.0f;
+#pragma unroll
+        for (int k = 0; k < NR; ++k) fp8_fma_acc(w[k][d], sc[k], acc[d]);   // rank order: deterministic
+      }
+      if (scale != 1.0f) {                                // fused average, before the re-quantisation
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[d][e] *= scale;
+      }
+      float m = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 4; ++d)
+        m = fmaxf(m, fmaxf(fmaxf(fabsf(acc[d][0]), fabsf(acc[d][1])), fmaxf(fabsf(acc[d][2]), fabsf(acc[d][3]))));
+      m = group16_max(m);
+      const float bscale = m > 0.0f ? m / kFp8Max : 1.0f;
+      const float inv = 1.0f / bscale;
+      u32x4 qq;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) qq[d] = pack_fp8(acc[d], inv);
+      if (live) {
+        myq[b * 16 + sub] = qq;                           // read by the peers after the mid barrier
+        if (sub == 0) mys[b] = bscale;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          float y[4];
+          unpack_fp8(qq[d], bscale, y);
+          store4<DT>(out, b * kQBlock + sub * 16 + d * 4, n, y);
+        }
+      }
+    }
+  }
+  if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
+  for (int64_t t = w0; t < nquad; t += nw) {
+    const int64_t j = t * 4 + g;
+    if (j >= cb) continue;
+    u32x4 w[NR];
+    float sc[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      if (k == rank) continue;
+      const u32x4* q = reinterpret_cast<const u32x4*>(P.data[k]);
+      const int64_t b = (int64_t)k * cb + j;
+      w[k] = q[b * 16 + sub];
+      sc[k] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      if (k == rank) continue;
+      const int64_t b = (int64_t)k * cb + j;
+      if (b * kQBlock >= n) continue;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float y[4];
+        unpack_fp8(w[k][d], sc[k], y);
+        store4<DT>(out, b * kQBlock + sub * 16 + d * 4, n, y);
+      }
+    }
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+// The r1 form (4 bytes per lane per peer, one wave per quant block), kept for A/B measurement
+// (MP4X_FP8_NARROW=1); bit-identical results.
+template <int DT, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot_narrow(IpcPtrs P, Signal* self, int rank, int64_t cb,
                                                                   int64_t soff, void* __restrict__ out, int64_t n,
                                                                   uint32_t epoch, const uint32_t* epoch_dev,
                                                                   float scale) {
@@ -378,12 +488,12 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
       }
       float m = fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3])));
       m = wave_max(m);
-      const float scale = m > 0.0f ? m / kFp8Max : 1.0f;
-      const uint32_t qq = pack_fp8(acc, 1.0f / scale);
+      const float bscale = m > 0.0f ? m / kFp8Max : 1.0f;
+      const uint32_t qq = pack_fp8(acc, 1.0f / bscale);
       myq[b * 64 + lane] = qq;                            // read by the peers after the mid barrier
-      if (lane == 0) mys[b] = scale;
+      if (lane == 0) mys[b] = bscale;
       float y[4];
-      unpack_fp8(qq, scale, y);
+      unpack_fp8(qq, bscale, y);
       store4<DT>(out, b * kQBlock + lane * 4, n, y);
     }
   }
@@ -414,11 +524,15 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
 
 template <int DT>
 static int fp8_nr(const IpcPtrs& P, Signal* self, int rank, int p, int64_t cb, int64_t soff, void* out, int64_t n,
-                  uint32_t epoch, const uint32_t* edev, float scale, int blocks, hipStream_t st) {
+                  uint32_t epoch, const uint32_t* edev, float scale, int blocks, hipStream_t st, bool narrow) {
 #define MP4X_FP8_CASE(N)                                                                                     \
   case N:                                                                                                    \
-    hipLaunchKernelGGL((k_ipc_fp8_twoshot<DT, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank, cb, \
-                       soff, out, n, epoch, edev, scale);                                                    \
+    if (narrow)                                                                                              \
+      hipLaunchKernelGGL((k_ipc_fp8_twoshot_narrow<DT, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self,   \
+                         rank, cb, soff, out, n, epoch, edev, scale);                                        \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_ipc_fp8_twoshot<DT, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,   \
+                         cb, soff, out, n, epoch, edev, scale);                                              \
     return (int)hipGetLastError();
   switch (p) {
     MP4X_FP8_CASE(2) MP4X_FP8_CASE(3) MP4X_FP8_CASE(4) MP4X_FP8_CASE(5) MP4X_FP8_CASE(6) MP4X_FP8_CASE(7)
@@ -785,8 +899,9 @@ extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* c
   if (cb <= 0 || n <= 0 || n > (int64_t)p * cb * kQBlock || (soff & 15) || ((uintptr_t)out & 15))
     return MP4X_E_BADARG;
   if (soff < (int64_t)p * cb * kQBlock) return MP4X_E_BADARG;     // scales after the q bytes
+  static const bool narrow = getenv("MP4X_FP8_NARROW") && getenv("MP4X_FP8_NARROW")[0] == '1';
   if (blocks <= 0) {
-    const int64_t waves = cb;                                       // one wave per quant block
+    const int64_t waves = narrow ? cb : (cb + 3) / 4;               // one wave per 4 quant blocks
     int64_t b = (waves + kIpcThreads / 64 - 1) / (kIpcThreads / 64);
     blocks = (int)(b < 1 ? 1 : (b > kIpcMaxBlocks ? kIpcMaxBlocks : b));
   }
@@ -794,9 +909,9 @@ extern "C" int mp4x_ipc_fp8_allreduce(int dtype, void* const* data_ptrs, void* c
   Signal* self = (Signal*)signal_ptrs[rank];
   hipStream_t st = (hipStream_t)stream;
   switch (dtype) {
-    case MP4X_F32: return fp8_nr<MP4X_F32>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
-    case MP4X_BF16: return fp8_nr<MP4X_BF16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
-    case MP4X_F16: return fp8_nr<MP4X_F16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st);
+    case MP4X_F32: return fp8_nr<MP4X_F32>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st, narrow);
+    case MP4X_BF16: return fp8_nr<MP4X_BF16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st, narrow);
+    case MP4X_F16: return fp8_nr<MP4X_F16>(P, self, rank, p, cb, soff, out, n, epoch, epoch_dev, scale, blocks, st, narrow);
     default: return MP4X_E_UNSUPPORTED;
   }
 }

@@ -76,6 +76,7 @@ SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16,
 
 
 _SPIN_SET = [False]
+_FP8_NARROW = os.environ.get("MP4X_FP8_NARROW") == "1"    # the r1 4-byte-lane fp8 kernel (A/B)
 
 
 def _set_spin(lib) -> None:
@@ -895,7 +896,7 @@ class IpcAllreduce:
             check(self.lib.mp4x_quant_fp8(dt, base + off * es, m, own, own + soff, st), "fp8 quant")
             edev = self._next_epoch(st)
             check(self.lib.mp4x_ipc_fp8_allreduce(dt, self._pp_data[0], self._pp_sig[0], self.rank, self.p, cb, soff,
-                                                  base + off * es, m, self.epoch, self._blocks_for_waves(cb), edev,
+                                                  base + off * es, m, self.epoch, self._blocks_for_waves(cb if _FP8_NARROW else -(-cb // 4)), edev,
                                                   scale, st), "mp4x_ipc_fp8_allreduce")
             off += m
         return view
