@@ -355,6 +355,34 @@ __device__ __forceinline__ float group16_max(float v) {
   return v;
 }
 
+// Output of one wave's 1024 dequantised values (4 consecutive quant blocks starting at
+// global block b0): lane l holds values [16 l, 16 l + 16) — a 64-byte stride between lanes, so
+// storing straight from registers would leave every store instruction 16 bytes per line.  The
+// values go through a wave-private LDS tile (20-float lane pitch: 16-byte aligned, spread over
+// the banks) and leave as 16-byte-per-lane CONTIGUOUS stores (1 KB of f32 per instruction).
+constexpr int kFp8LdsPitch = 20;
+template <int DT>
+__device__ __forceinline__ void fp8_wave_store(float* tile, const float (&y)[16], int lane, void* out,
+                                               int64_t b0, int64_t cb_end, int64_t n) {
+#pragma unroll
+  for (int d = 0; d < 4; ++d)
+    *reinterpret_cast<float4*>(tile + lane * kFp8LdsPitch + d * 4) = make_float4(y[4 * d], y[4 * d + 1],
+                                                                                  y[4 * d + 2], y[4 * d + 3]);
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's LDS writes are done
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const int e = (d * 64 + lane) * 4;                  // value index inside the wave's 1024
+    const float4 v = *reinterpret_cast<const float4*>(tile + (e >> 4) * kFp8LdsPitch + (e & 15));
+    const int64_t blk = b0 + (e >> 8);
+    if (blk < cb_end) {
+      float x[4] = {v.x, v.y, v.z, v.w};
+      store4<DT>(out, b0 * kQBlock + e, n, x);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();      // the tile is rewritten by this wave's next step
+}
+
 template <int DT, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Signal* self, int rank, int64_t cb,
                                                                   int64_t soff, void* __restrict__ out, int64_t n,
@@ -362,12 +390,14 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
                                                                   float scale) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
+  __shared__ __attribute__((aligned(16))) float s_tile[kIpcThreads * kFp8LdsPitch];
   epoch = resolve_epoch(epoch, epoch_dev);
   if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
   const int lane = threadIdx.x & 63;
   const int g = lane >> 4;                 // quant block of this lane within the wave's 4
   const int sub = lane & 15;               // 16-byte slot inside the 256-byte block
   constexpr int kWaves = kIpcThreads / 64;
+  float* tile = s_tile + (threadIdx.x >> 6) * 64 * kFp8LdsPitch;
   const int64_t w0 = (int64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * kWaves;
   const int64_t nquad = (cb + 3) / 4;      // wave steps per chunk
@@ -412,40 +442,42 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_fp8_twoshot(IpcPtrs P, Sign
       if (live) {
         myq[b * 16 + sub] = qq;                           // read by the peers after the mid barrier
         if (sub == 0) mys[b] = bscale;
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-          float y[4];
-          unpack_fp8(qq[d], bscale, y);
-          store4<DT>(out, b * kQBlock + sub * 16 + d * 4, n, y);
-        }
       }
+      float y[16];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        float yy[4];
+        unpack_fp8(qq[d], bscale, yy);
+        y[4 * d] = yy[0]; y[4 * d + 1] = yy[1]; y[4 * d + 2] = yy[2]; y[4 * d + 3] = yy[3];
+      }
+      fp8_wave_store<DT>(tile, y, lane, out, (int64_t)rank * cb + t * 4, (int64_t)rank * cb + cb, n);
     }
   }
   if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
   for (int64_t t = w0; t < nquad; t += nw) {
     const int64_t j = t * 4 + g;
-    if (j >= cb) continue;
+    const bool live = j < cb;
     u32x4 w[NR];
     float sc[NR];
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       if (k == rank) continue;
       const u32x4* q = reinterpret_cast<const u32x4*>(P.data[k]);
-      const int64_t b = (int64_t)k * cb + j;
-      w[k] = q[b * 16 + sub];
-      sc[k] = reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b];
+      const int64_t b = (int64_t)k * cb + (live ? j : 0);
+      w[k] = live ? q[b * 16 + sub] : u32x4{0u, 0u, 0u, 0u};
+      sc[k] = live ? reinterpret_cast<const float*>(reinterpret_cast<const char*>(q) + soff)[b] : 0.0f;
     }
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       if (k == rank) continue;
-      const int64_t b = (int64_t)k * cb + j;
-      if (b * kQBlock >= n) continue;
+      float y[16];
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        float y[4];
-        unpack_fp8(w[k][d], sc[k], y);
-        store4<DT>(out, b * kQBlock + sub * 16 + d * 4, n, y);
+        float yy[4];
+        unpack_fp8(w[k][d], sc[k], yy);
+        y[4 * d] = yy[0]; y[4 * d + 1] = yy[1]; y[4 * d + 2] = yy[2]; y[4 * d + 3] = yy[3];
       }
+      fp8_wave_store<DT>(tile, y, lane, out, (int64_t)k * cb + t * 4, (int64_t)k * cb + cb, n);
     }
   }
   block_barrier(nullptr, P, 2, rank, p, epoch, self);

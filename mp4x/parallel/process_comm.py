@@ -311,12 +311,24 @@ class ProcessCommSlave:
         self.engine.tree_gather(buf, sendfroms, sendtos, operand, rootRank)
         return arrData
 
-    def _map_on_device(self, mapData: Dict) -> bool:
+    def _map_on_device(self, mapData: Dict, all_keys=None) -> bool:
         """Do this map collective's values live on the GPU?  A rank with an empty map cannot
-        tell, so the ranks agree over the control plane (one small RPC)."""
+        tell, so the ranks agree over the control plane — in ONE round that also carries every
+        rank's not-yet-numbered keys (``all_keys``: every key the device op will number; default
+        the map's), so the device op skips its own key-dictionary round (``_keys_presynced``)."""
         mine = -1 if not mapData else int(_is_torch(next(iter(mapData.values()))))
-        flags = self.server.call("allgather_obj", self.rank, mine)
-        return any(f == 1 for f in flags)
+        new = []
+        if mine == 1:
+            from .sparse import _dictionary
+            new = _dictionary(self.device).unknown(list(mapData.keys()) if all_keys is None else list(all_keys))
+        res = self.server.call("allgather_obj", self.rank, (mine, new))
+        on_device = any(f == 1 for f, _ in res)
+        if on_device:
+            from .sparse import _dictionary
+            eng = self.device
+            _dictionary(eng).learn_round([ks for _, ks in res])
+            eng._keys_presynced = True
+        return on_device
 
     def gatherMap(self, mapData: Dict, operand: Operand, rootRank: int) -> Dict:
         self._tick("gatherMap")
@@ -432,7 +444,7 @@ class ProcessCommSlave:
             return mapDataList[0]
         self._check_root(rootRank)
         probe = next((d for d in mapDataList if d), {}) if self.rank == rootRank and mapDataList else {}
-        if self._map_on_device(probe):
+        if self._map_on_device(probe, all_keys=(k for m in mapDataList for k in m.keys()) if probe else None):
             return self.device.scatter_map(mapDataList if self.rank == rootRank else None, rootRank)
         blocks = [[d] for d in mapDataList] if self.rank == rootRank else None
         got = self.engine.tree_scatter_maps(blocks, operand, rootRank)
@@ -472,7 +484,8 @@ class ProcessCommSlave:
             return mapDataList[0]
         if len(mapDataList) != self.slaveNum:
             raise Mp4jException(f"mapDataList size={len(mapDataList)}, must be equal to slaveNum={self.slaveNum}")
-        if self._map_on_device(next((d for d in mapDataList if d), {})):
+        if self._map_on_device(next((d for d in mapDataList if d), {}),
+                               all_keys=(k for m in mapDataList for k in m.keys())):
             return self.device.reduce_scatter_map(mapDataList, operator)
         return self.engine.ring_reduce_scatter_maps([[d] for d in mapDataList], operand, operator)[0]
 

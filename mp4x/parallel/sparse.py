@@ -49,6 +49,9 @@ class KeyDictionary:
 
     def unknown(self, keys) -> List:
         """Keys this rank has never numbered (first-seen order, de-duplicated)."""
+        keys = keys if isinstance(keys, (list, tuple)) else list(keys)
+        if not (set(keys) - self.key2id.keys()):      # steady state: one C-level set difference
+            return []
         seen = set()
         out = []
         for k in keys:
@@ -68,6 +71,18 @@ class KeyDictionary:
     def ids(self, keys) -> List[int]:
         return [self.key2id[k] for k in keys]
 
+    def id_array(self, keys) -> np.ndarray:
+        """int64 ids of ``keys`` (one C-level pass)."""
+        keys = keys if isinstance(keys, (list, tuple)) else list(keys)
+        return np.fromiter(map(self.key2id.__getitem__, keys), dtype=np.int64, count=len(keys))
+
+    def keys_of(self, ids: np.ndarray) -> List:
+        """Keys of an int64 id array (vectorised through an object array cached per size)."""
+        if getattr(self, "_obj_n", -1) != len(self.id2key):
+            self._obj = np.asarray(self.id2key + [None], dtype=object)[:-1]   # (+None: 1-D even for tuples)
+            self._obj_n = len(self.id2key)
+        return self._obj[ids].tolist()
+
     @property
     def bits(self) -> int:
         return max(1, (len(self.id2key) - 1).bit_length())
@@ -82,7 +97,14 @@ def _dictionary(engine) -> KeyDictionary:
 
 def _sync_new_keys(engine, new: List) -> None:
     """One sync round: allgather (control plane) of every rank's unseen keys, numbered in rank
-    order on every rank.  Collective — ranks with nothing new still take part."""
+    order on every rank.  Collective — ranks with nothing new still take part.
+
+    When the caller's device/host agreement round already carried the new keys
+    (``ProcessCommSlave._map_on_device`` sets ``engine._keys_presynced`` on EVERY rank), this
+    round is skipped: one control-plane round trip per map collective instead of two."""
+    if getattr(engine, "_keys_presynced", False):
+        engine._keys_presynced = False
+        return
     _dictionary(engine).learn_round(engine.all_gather_object(list(new)))
 
 
@@ -315,26 +337,35 @@ def list_concat(engine, ids: torch.Tensor) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ Map API
+def _stack_rows(vals: List[torch.Tensor]) -> torch.Tensor:
+    """[n, numel] rows of n same-shaped tensors: ONE stack (no per-value reshape views)."""
+    v = torch.stack(vals)
+    return v.view(len(vals), -1)
+
+
 def _map_tensors(engine, mapData: Dict):
-    """Dict[str, Tensor] -> (ids int64[n], rows [n, numel], value shape); syncs new keys."""
+    """Dict[str, Tensor] -> (ids int64[n], rows [n, numel], value shape); syncs new keys.
+    Vectorised: ids through one ``np.fromiter`` + one host->device copy, values through one
+    ``torch.stack`` (r1 built a Python list of ids and a reshaped view per value)."""
     d = _dictionary(engine)
     keys = list(mapData.keys())
     _sync_new_keys(engine, d.unknown(keys))
-    ids = d.ids(keys)
     vals = list(mapData.values())
     dev = vals[0].device if vals else engine.device
     if vals:
-        v = torch.stack([x.reshape(-1) for x in vals])
+        v = _stack_rows(vals)
         shape = tuple(vals[0].shape)
     else:
         v = torch.empty((0, 1), device=dev)
         shape = (1,)
-    return torch.tensor(ids, dtype=torch.int64, device=dev), v, shape
+    ids = torch.from_numpy(d.id_array(keys)).to(dev, non_blocking=False)
+    return ids, v, shape
 
 
 def _tensors_map(engine, k: torch.Tensor, v: torch.Tensor, shape) -> Dict:
     d = _dictionary(engine)
-    return {d.id2key[kid]: v[i].view(shape) for i, kid in enumerate(k.tolist())}
+    keys = d.keys_of(k.cpu().numpy())
+    return dict(zip(keys, v.view((v.shape[0],) + tuple(shape)).unbind(0)))
 
 
 def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
@@ -374,17 +405,17 @@ def _maps_by_dest(engine, maps: List[Dict]):
     dictionary sync for all of them."""
     d = _dictionary(engine)
     _sync_new_keys(engine, d.unknown(k for m in maps for k in m.keys()))
-    id_lists = [d.ids(list(m.keys())) for m in maps]
+    id_lists = [d.id_array(list(m.keys())) for m in maps]
     ks, vs, counts, shape = [], [], [], None
     for m, ids in zip(maps, id_lists):
         vals = list(m.values())
         dev = vals[0].device if vals else engine.device
         if vals:
             shape = tuple(vals[0].shape)
-            v = torch.stack([x.reshape(-1) for x in vals])
+            v = _stack_rows(vals)
         else:
             v = torch.empty((0, 1), device=dev)
-        ks.append(torch.tensor(ids, dtype=torch.int64, device=dev))
+        ks.append(torch.from_numpy(ids).to(dev))
         vs.append(v)
         counts.append(len(ids))
     return ks, vs, counts, shape
