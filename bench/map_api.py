@@ -60,6 +60,9 @@ def main():
             c = time.perf_counter()
             out2 = sparse._tensors_map(eng, rk, rv, shape)
             d = time.perf_counter()
+            if r == 0:
+                print(f"iter {it}: total {t1 - t0:.3f}s to_tensors {b - a:.3f}s kernels {c - b:.3f}s "
+                      f"to_dict {d - c:.3f}s", file=sys.stderr, flush=True)
             if it:
                 ts["total"].append(t1 - t0)
                 ts["to_tensors"].append(b - a)

@@ -319,8 +319,10 @@ class ProcessCommSlave:
         mine = -1 if not mapData else int(_is_torch(next(iter(mapData.values()))))
         new = []
         if mine == 1:
-            from .sparse import _dictionary
-            new = _dictionary(self.device).unknown(list(mapData.keys()) if all_keys is None else list(all_keys))
+            from .sparse import TensorMap, _dictionary
+            d = _dictionary(self.device)
+            if not (all_keys is None and isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d):
+                new = d.unknown(list(mapData.keys()) if all_keys is None else list(all_keys))
         res = self.server.call("allgather_obj", self.rank, (mine, new))
         on_device = any(f == 1 for f, _ in res)
         if on_device:

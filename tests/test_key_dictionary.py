@@ -28,3 +28,34 @@ def test_bits_small_dictionaries():
     assert d.bits == 2                          # ids 0..2
     d.learn_round([list(range(100, 1100))])
     assert d.bits == (len(d.id2key) - 1).bit_length()
+
+
+def test_tensor_map_is_a_dict_view():
+    """The device map collectives return a lazy mapping over (ids, rows): dict semantics,
+    mutation through an overlay, and the unmodified map goes back in without per-key work."""
+    import numpy as np
+    import torch
+    from mp4x.parallel.sparse import KeyDictionary, TensorMap, _map_tensors
+
+    d = KeyDictionary()
+    d.learn_round([["a", "b", "c"]])
+    rows = torch.arange(12, dtype=torch.float32).view(3, 4)
+    m = TensorMap(d, np.array([2, 0, 1], dtype=np.int64), rows, (2, 2))
+    assert list(m) == ["c", "a", "b"] and len(m) == 3
+    assert torch.equal(m["a"], rows[1].view(2, 2)) and "b" in m and "z" not in m
+    assert dict(m.items()).keys() == {"a", "b", "c"}
+
+    class _Eng:
+        _keydict = d
+        device = torch.device("cpu")
+        _keys_presynced = True              # the collective key round is skipped in this unit test
+    ids, v, shape = _map_tensors(_Eng, m)
+    assert ids.tolist() == [2, 0, 1] and v.data_ptr() == rows.data_ptr() and shape == (2, 2)
+
+    m["z"] = torch.zeros(2, 2)
+    del m["a"]
+    assert list(m) == ["c", "b", "z"] and len(m) == 3 and "a" not in m
+    m["a"] = torch.ones(2, 2)
+    assert len(m) == 4 and torch.equal(m["a"], torch.ones(2, 2))
+    del m["z"]
+    assert len(m) == 3 and not m.pristine()
