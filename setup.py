@@ -21,7 +21,7 @@ setup(
     packages=find_packages(include=["mp4x", "mp4x.*"]),
     package_data={"mp4x": ["_native/*.so"]},
     python_requires=">=3.10",
-    install_requires=["numpy", "msgpack", "torch"],
+    install_requires=["numpy", "msgpack", "torch", "cloudpickle"],
     extras_require={"test": ["pytest", "pytest-timeout"]},
     entry_points={"console_scripts": ["mp4x-master = mp4x.control.master:main",
                                       "mp4x-check = mp4x.check:main"]},
