@@ -40,6 +40,10 @@ constexpr int kIpcThreads = 512;
 // peer runs the zero-copy one sees the other tag in its flag slot and fails at once instead of
 // reading the wrong buffers (registration is collective, but the choice is made per rank).
 constexpr uint32_t kZcTag = 0x80000000u;
+// The zero-copy PUSH two-shot (k_ipc_twoshot_push) carries a second tag bit; host epochs live in
+// the low 30 bits, and a flag whose low bits match but whose tag differs fails the call at once.
+constexpr uint32_t kPushTag = 0x40000000u;
+constexpr uint32_t kTagMask = kZcTag | kPushTag;
 
 struct alignas(128) Signal {
   uint32_t start[kIpcMaxBlocks][kIpcMaxRanks];
@@ -83,7 +87,7 @@ __device__ __forceinline__ bool block_barrier(uint32_t (*slots)[kIpcMaxRanks] /*
     uint32_t seen;
     while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
       __builtin_amdgcn_s_sleep(2);
-      const bool other_protocol = seen == (epoch ^ kZcTag);
+      const bool other_protocol = seen != epoch && ((seen ^ epoch) & ~kTagMask) == 0;
       if (other_protocol || __builtin_amdgcn_s_memrealtime() - t0 > spin) {
         const uint32_t code = other_protocol ? 4u : 1u + (uint32_t)which;
         __hip_atomic_store(&self->error, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -144,12 +148,12 @@ __device__ __forceinline__ uint32_t resolve_epoch(uint32_t epoch, const uint32_t
   // graph mode: the epoch lives in device memory and is bumped by k_ipc_bump_epoch, the
   // preceding node of the same graph, so every replay gets a fresh, rank-consistent epoch
   // (the protocol tag of a host-passed epoch is kept in graph mode too)
-  return epoch_dev ? (__hip_atomic_load(epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (epoch & kZcTag))
+  return epoch_dev ? (__hip_atomic_load(epoch_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (epoch & kTagMask))
                    : epoch;
 }
 
 __global__ void k_ipc_bump_epoch(uint32_t* epoch_dev) {
-  uint32_t e = (*epoch_dev + 1) & ~kZcTag;
+  uint32_t e = (*epoch_dev + 1) & ~kTagMask;
   *epoch_dev = e ? e : 1;
 }
 
@@ -225,6 +229,124 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
     }
   }
   block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+// ---------------------------------------------------------------- zero-copy PUSH two-shot
+// The two-shot with every xGMI transfer a WRITE (posted: no request/response round trip per
+// line, the protocol RCCL's ring primitives use) instead of a read.  Data pointers are the
+// registered caller tensors; scr[k] is rank k's receive scratch of p-1 chunk slots (slot of
+// sender q: q < k ? q : q - 1).
+//   phase 1: rank r writes its chunk k (k != r) into slot(r) of rank k's scratch;
+//   mid barrier (every write released at system scope before the flag);
+//   phase 2: rank r reduces chunk r in RANK ORDER from its own tensor and the p-1 LOCAL slots,
+//            stores the result into its tensor and writes it into chunk r of every peer's tensor;
+//   end barrier.
+// Block b of every rank touches the same chunk-relative offsets in every phase, so the per-block
+// barriers order every write against the reads and writes of the same offsets on the peers.
+struct ScrPtrs {
+  void* s[kIpcMaxRanks];
+};
+
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot_push(IpcPtrs P, ScrPtrs S, Signal* self, int rank,
+                                                                   int64_t nvec, uint32_t epoch,
+                                                                   const uint32_t* epoch_dev, float scale) {
+  using E = Elem<DT>;
+  using St = typename E::S;
+  using A = typename E::A;
+  constexpr int W = 16 / sizeof(St);
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  const int64_t chunk = (nvec + p - 1) / p;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
+  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  const u32x4* myscr = reinterpret_cast<const u32x4*>(S.s[rank]);
+  if (!block_barrier(nullptr, P, 0, rank, p, epoch, self)) return;
+  for (int64_t v = off0; v < chunk; v += stride) {
+    u32x4 x[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {                 // local reads of every outgoing chunk
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec) x[k] = mine[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {                 // p-1 posted remote writes, every link at once
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec)
+        reinterpret_cast<u32x4*>(S.s[k])[(int64_t)(rank < k ? rank : rank - 1) * chunk + v] = x[k];
+    }
+  }
+  if (!block_barrier(nullptr, P, 1, rank, p, epoch, self)) return;
+  const int64_t b = (int64_t)rank * chunk;
+  const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+  for (int64_t v = off0; b + v < e; v += stride) {
+    u32x4 r[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q)                   // all local: own chunk + p-1 scratch slots
+      r[q] = q == rank ? mine[b + v] : myscr[(int64_t)(q < rank ? q : q - 1) * chunk + v];
+    St s0[W];
+    __builtin_memcpy(s0, &r[0], 16);
+    A acc[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) acc[j] = E::load(s0[j]);
+#pragma unroll
+    for (int q = 1; q < NR; ++q) {                 // rank order: deterministic, = the pull form
+      St xq[W];
+      __builtin_memcpy(xq, &r[q], 16);
+#pragma unroll
+      for (int j = 0; j < W; ++j) acc[j] = combine<DT, OP>(acc[j], E::load(xq[j]));
+    }
+    if constexpr (is_float_dt<DT>()) {
+      if (scale != 1.0f) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) acc[j] = acc[j] * (A)scale;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) s0[j] = E::store(acc[j]);
+    u32x4 o;
+    __builtin_memcpy(&o, s0, 16);
+    mine[b + v] = o;
+#pragma unroll
+    for (int k = 0; k < NR; ++k)                   // the all-gather half, pushed to every peer
+      if (k != rank) reinterpret_cast<u32x4*>(const_cast<void*>(P.data[k]))[b + v] = o;
+  }
+  block_barrier(nullptr, P, 2, rank, p, epoch, self);
+}
+
+template <int DT, int OP>
+static int push_nr(const IpcPtrs& P, const ScrPtrs& S, Signal* self, int rank, int p, int64_t nvec, uint32_t epoch,
+                   int blocks, const uint32_t* edev, float scale, hipStream_t st) {
+#define MP4X_PUSH_CASE(N)                                                                                     \
+  case N:                                                                                                     \
+    hipLaunchKernelGGL((k_ipc_twoshot_push<DT, OP, N>), dim3(blocks), dim3(kIpcThreads), 0, st, P, S, self,    \
+                       rank, nvec, epoch, edev, scale);                                                       \
+    return (int)hipGetLastError();
+  switch (p) {
+    MP4X_PUSH_CASE(2) MP4X_PUSH_CASE(3) MP4X_PUSH_CASE(4) MP4X_PUSH_CASE(5) MP4X_PUSH_CASE(6) MP4X_PUSH_CASE(7)
+    MP4X_PUSH_CASE(8)
+    default: return MP4X_E_BADARG;
+  }
+#undef MP4X_PUSH_CASE
+}
+
+template <int DT>
+static int push_dt(int op, const IpcPtrs& P, const ScrPtrs& S, Signal* self, int rank, int p, int64_t nvec,
+                   uint32_t epoch, int blocks, const uint32_t* edev, float scale, hipStream_t st) {
+  switch (op) {
+    case MP4X_SUM: return push_nr<DT, MP4X_SUM>(P, S, self, rank, p, nvec, epoch, blocks, edev, scale, st);
+    case MP4X_MAX:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return push_nr<DT, MP4X_MAX>(P, S, self, rank, p, nvec, epoch, blocks, edev, scale, st);
+      return MP4X_E_UNSUPPORTED;
+    case MP4X_MIN:
+      if constexpr (is_float_dt<DT>() && DT != MP4X_F64)
+        return push_nr<DT, MP4X_MIN>(P, S, self, rank, p, nvec, epoch, blocks, edev, scale, st);
+      return MP4X_E_UNSUPPORTED;
+    default: return MP4X_E_UNSUPPORTED;
+  }
 }
 
 // ---------------------------------------------------------------- direct reduce-scatter / all-gather
@@ -786,6 +908,44 @@ extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data
                                   const uint32_t* epoch_dev, void* stream) {
   return mp4x_ipc_allreduce_ex(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, nullptr, out, epoch, blocks,
                                epoch_dev, 1.0f, stream);
+}
+
+// Zero-copy PUSH two-shot (see k_ipc_twoshot_push): data_ptrs = every rank's registered tensor
+// (this rank's own included; the result replaces it), scratch_ptrs = every rank's receive
+// scratch of at least (p - 1) * ceil(nbytes / 16 / p) 16-byte vectors.
+extern "C" int mp4x_ipc_allreduce_push(int dtype, int op, void* const* data_ptrs, void* const* scratch_ptrs,
+                                       void* const* signal_ptrs, int rank, int p, int64_t nbytes, uint32_t epoch,
+                                       int blocks, const uint32_t* epoch_dev, float scale, void* stream) {
+  if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
+  if (scale != 1.0f && !(dtype == MP4X_F32 || dtype == MP4X_F64 || dtype == MP4X_BF16 || dtype == MP4X_F16))
+    return MP4X_E_BADARG;
+  IpcPtrs P;
+  ScrPtrs S;
+  for (int k = 0; k < kIpcMaxRanks; ++k) {
+    P.data[k] = k < p ? data_ptrs[k] : nullptr;
+    P.sig[k] = k < p ? (Signal*)signal_ptrs[k] : nullptr;
+    S.s[k] = k < p ? scratch_ptrs[k] : nullptr;
+    if (k < p && (((uintptr_t)P.data[k] & 15) || ((uintptr_t)S.s[k] & 15) || !P.sig[k] || !S.s[k]))
+      return MP4X_E_BADARG;
+  }
+  const int64_t nvec = nbytes / 16;
+  if (blocks <= 0) {
+    const int64_t chunk = (nvec + p - 1) / p;
+    int64_t b = (chunk + kIpcThreads - 1) / kIpcThreads;
+    blocks = (int)(b < 1 ? 1 : (b > kIpcMaxBlocks ? kIpcMaxBlocks : b));
+  }
+  if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+  switch (dtype) {
+    case MP4X_F64: return push_dt<MP4X_F64>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    case MP4X_F32: return push_dt<MP4X_F32>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    case MP4X_I64: return push_dt<MP4X_I64>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    case MP4X_I32: return push_dt<MP4X_I32>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    case MP4X_BF16: return push_dt<MP4X_BF16>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    case MP4X_F16: return push_dt<MP4X_F16>(op, P, S, self, rank, p, nvec, epoch, blocks, epoch_dev, scale, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
 }
 
 static int ipc_prepare(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p, IpcPtrs* P) {

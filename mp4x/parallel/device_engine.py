@@ -471,7 +471,8 @@ class DeviceEngine:
         if kind == "allreduce" and op is not None and not getattr(op, "is_custom", False) and \
                 (codec == "zs" or (codec is None and getattr(operand, "compress", False))):
             return "zs"       # lossless wire compression (the reference's compress=true contract)
-        if forced in ("ipc1", "ipc2", "ipc2p", "ipc2z") and kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
+        if forced in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and kind == "allreduce" and \
+                self._ipc_ok(op, dtype, nbytes):
             return forced
         if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
             return forced     # (custom operators may be non-commutative: rank-ordered a2a only)
@@ -499,7 +500,7 @@ class DeviceEngine:
         return "rccl"
 
     # ------------------------------------------------------------------ hipGraph capture
-    _CAPTURABLE = ("rccl", "ipc1", "ipc2", "ipc2z", "a2a", "rhd", "fp8", "bf16")
+    _CAPTURABLE = ("rccl", "ipc1", "ipc2", "ipc2z", "ipc2w", "a2a", "rhd", "fp8", "bf16")
 
     def capture(self, fn, warmup: int = 2):
         """Capture ``fn()`` — a fixed sequence of device collectives on fixed tensors, e.g. a DDP
@@ -623,13 +624,17 @@ class DeviceEngine:
 
     def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
         """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
-        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z") and self.ipc() is None:
+        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
-        if algo == "ipc2z":
+        if algo in ("ipc2z", "ipc2w"):
             peers = self._ipc_obj.registered(view) if self._zc else None
             if peers is not None and (not torch.cuda.is_current_stream_capturing()
                                       or self._ipc_obj._epoch_dev is not None):
-                self._ipc_obj.allreduce_registered(view, op, peers, scale=scale)
+                scr = self._ipc_obj.scratch_of(view) if algo == "ipc2w" else None
+                if scr is not None:     # posted remote writes only (push form)
+                    self._ipc_obj.allreduce_push(view, op, peers, scr, scale=scale)
+                else:
+                    self._ipc_obj.allreduce_registered(view, op, peers, scale=scale)
                 return True
             algo = "ipc2"        # not registered (on this rank): the staged two-shot
         if algo in ("ipc1", "ipc2", "ipc2p") and torch.cuda.is_current_stream_capturing():
@@ -691,7 +696,7 @@ class DeviceEngine:
             return self.rccl_ok(op, dtype)
         if algo.startswith("rccl_c"):
             return self.backend == "nccl" and self.rccl_ok(op, dtype)
-        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z"):
+        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w"):
             return self._ipc_ok(op, dtype, nbytes)
         if algo == "rhd":
             return not getattr(op, "is_custom", False)
@@ -711,6 +716,7 @@ class DeviceEngine:
                 c.append("ipc2p")     # pipelined pieces: input copies overlap the xGMI-bound kernel
             if self._zc:
                 c.append("ipc2z")     # zero-copy two-shot on a registered tensor (one kernel)
+                c.append("ipc2w")     # ... its push form: every xGMI transfer a posted write
         c.append("a2a")
         if nbytes <= (64 << 20):
             c.append("rhd")
@@ -735,10 +741,14 @@ class DeviceEngine:
             self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
         registered = False
         try:
-            if "ipc2z" in cands:
+            if "ipc2z" in cands or "ipc2w" in cands:
                 registered = self.register_buffer(view)     # collective; False on every rank alike
+                if not registered or (self._ipc_obj.scratch_of(view) is None and "ipc2w" in cands):
+                    # (the push form needs every rank's scratch: agreed inside register)
+                    cands[:] = [c for c in cands if c != "ipc2w" or registered and
+                                self._ipc_obj.scratch_of(view) is not None]
                 if not registered:
-                    cands.remove("ipc2z")
+                    cands[:] = [c for c in cands if c not in ("ipc2z", "ipc2w")]
             for c in cands:
                 times.append(self._time_candidate(c, view, op, iters))
         finally:
@@ -886,7 +896,8 @@ class DeviceEngine:
             return 1
 
     # ------------------------------------------------------------------ persisted tuning table
-    _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "a2a", "rhd"},
+    _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w", "a2a",
+                                  "rhd"},
                     "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"}}
 
     def _topology(self) -> dict:

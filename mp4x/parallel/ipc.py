@@ -35,6 +35,8 @@ native.register_signatures({
     "mp4x_ipc_set_spin": (c_int, [ctypes.c_double]),
     "mp4x_mem_range": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
     "mp4x_dev_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
+    "mp4x_ipc_allreduce_push": (c_int, [c_int, c_int, PP, PP, PP, c_int, c_int, c_int64, ctypes.c_uint32, c_int,
+                                        c_void_p, ctypes.c_float, c_void_p]),
     "mp4x_ipc_handle_size": (c_int, []),
     "mp4x_ipc_get_handle": (c_int, [c_void_p, c_void_p]),
     "mp4x_ipc_open_handle": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
@@ -68,6 +70,8 @@ _RESIDENT_BLOCKS = 1024
 
 ONESHOT, TWOSHOT = 0, 1
 ZC_TAG = 0x80000000      # epoch tag of the zero-copy protocol (csrc/runtime/ipc.hip kZcTag)
+PUSH_TAG = 0x40000000    # ... and of its push form (kPushTag); host epochs use the low 30 bits
+PUSH_ON = os.environ.get("MP4X_IPC_PUSH", "1") == "1"
 # hipIpcOpenMemHandle of an allocation of 2^31 bytes or more never returns on this ROCm
 # (measured: 2.0 GB opens in 0.1 ms, 2 GiB hangs — profiles/r2/ipc_open_probe.jsonl), so
 # registration refuses such allocations (every rank alike): the staged kernels run instead.
@@ -182,8 +186,11 @@ class IpcAllreduce:
         self._sig_stream = None    # private stream for error-word reads (lazy)
         self._overlap_default = os.environ.get("MP4X_IPC_OVERLAP", "0") == "1"
         self._fuse_copy = os.environ.get("MP4X_IPC_FUSED_COPY", "1") == "1"
-        # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> peer pointers
+        # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> (peer pointers,
+        # every rank's push scratch or None)
         self._regs = {}
+        self._scratch_allocs: List[c_void_p] = []
+        self._scratch_ptr = 0
         self._peer_bases = {}       # (rank, handle bytes) -> mapped base (one open per allocation)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
@@ -266,7 +273,7 @@ class IpcAllreduce:
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
+                self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
             check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
                                                  self.rank, self.p, m, src.data_ptr() + off if fused else None,
                                                  dst.data_ptr() + off, self.epoch, blocks, edev, scale, st),
@@ -307,7 +314,7 @@ class IpcAllreduce:
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, ms), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
+                self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
             pp = self._pp_hi[0] if slot else self._pp_data[0]
             check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
                                                  None, dst.data_ptr() + off, self.epoch, blocks, edev, scale, ms),
@@ -350,7 +357,10 @@ class IpcAllreduce:
                 raise Mp4jException(f"allocation of {size.value} bytes is above the IPC open limit ({IPC_OPEN_MAX})")
             h = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(base, h), "ipc_get_handle(registered)")
-            blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local)
+            scr_h = None
+            if PUSH_ON and not ok_local:
+                scr_h = self._alloc_scratch(key[1], hs)
+            blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local, scr_h)
         except Exception as e:   # noqa: BLE001 — travels in the allgather: every rank decides together
             err = str(e)
         allb = self.comm.server.call("allgather_obj", self.rank, (blob, err))
@@ -360,10 +370,14 @@ class IpcAllreduce:
         if all(b[3] for b, _ in allb):
             return True                               # already registered everywhere
         ptrs, err = [], None
+        push = all(b[4] is not None for b, _ in allb)      # every rank has a receive scratch
+        scr = []
         try:
             for r, (b, _) in enumerate(allb):
                 if r == self.rank:
                     ptrs.append(t.data_ptr())
+                    if push:
+                        scr.append(self._scratch_ptr)
                     continue
                 hk = (r, bytes(b[0]))
                 if hk not in self._peer_bases:
@@ -373,13 +387,40 @@ class IpcAllreduce:
                     self._opened.append(ptr)
                     self._peer_bases[hk] = ptr.value
                 ptrs.append(self._peer_bases[hk] + int(b[1]))
+                if push:
+                    q = c_void_p()
+                    check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(b[4]), hs),
+                                                        ctypes.byref(q)), f"ipc_open_handle(scratch, rank {r})")
+                    self._opened.append(q)
+                    scr.append(q.value)
         except Exception as e:   # noqa: BLE001
             err = str(e)
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
             return False
-        self._regs[key] = ptrs
+        self._regs[key] = (ptrs, scr if push else None)
         return True
+
+    def _alloc_scratch(self, nbytes: int, hs: int):
+        """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
+        slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
+        its IPC handle, or None (then the registration simply has no push form)."""
+        chunk = -(-(nbytes // 16) // self.p)
+        size = max(16, (self.p - 1) * chunk * 16)
+        ptr = c_void_p()
+        try:
+            if size > IPC_OPEN_MAX:
+                return None
+            check(self.lib.mp4x_ipc_alloc(size, ctypes.byref(ptr)), "ipc_alloc(scratch)")
+            h = ctypes.create_string_buffer(hs)
+            check(self.lib.mp4x_ipc_get_handle(ptr, h), "ipc_get_handle(scratch)")
+        except Exception:   # noqa: BLE001
+            if ptr:
+                self.lib.mp4x_ipc_free(ptr)
+            return None
+        self._scratch_allocs.append(ptr)
+        self._scratch_ptr = ptr.value
+        return h.raw
 
     def deregister(self, t: torch.Tensor) -> None:
         """Forget ``t`` (local; the peer mappings of its allocation stay open until close)."""
@@ -391,11 +432,48 @@ class IpcAllreduce:
             return None
         a = view.data_ptr()
         n = view.numel() * view.element_size()
-        for (ptr, nb), peers in self._regs.items():
+        for (ptr, nb), (peers, _) in self._regs.items():
             if ptr <= a and a + n <= ptr + nb:
                 d = a - ptr
                 return [q + d for q in peers]
         return None
+
+    def scratch_of(self, view: torch.Tensor):
+        """Every rank's push scratch for ``view``'s registered tensor, or None (no push form)."""
+        a = view.data_ptr()
+        n = view.numel() * view.element_size()
+        for (ptr, nb), (_, scr) in self._regs.items():
+            if ptr <= a and a + n <= ptr + nb:
+                return scr
+        return None
+
+    def allreduce_push(self, view: torch.Tensor, op, peers, scratch, scale: float = 1.0) -> torch.Tensor:
+        """In place, on registered tensors, with every xGMI transfer a posted WRITE (see
+        ``k_ipc_twoshot_push``): one kernel, any size."""
+        self.raise_if_failed()
+        total = view.numel() * view.element_size()
+        if total % 16 or view.data_ptr() % 16:
+            raise Mp4jException("zero-copy IPC allreduce needs 16-byte aligned, 16-byte multiple views")
+        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+            raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        self._push_ptrs(total, op, peers, scratch, view.dtype, scale)
+        return view
+
+    def _push_ptrs(self, total: int, op, peers, scratch, dtype, scale: float = 1.0) -> None:
+        st = stream_ptr()
+        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
+        if edev is not None:
+            check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
+        else:
+            self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+        chunk = -(-(total // 16) // self.p)
+        blocks = max(1, min(self.max_blocks, -(-chunk // 512))) if self.max_blocks else 0
+        pp = ptr_array(peers)
+        sp = ptr_array(scratch)
+        check(self.lib.mp4x_ipc_allreduce_push(int(dtype_of_torch(dtype)), int(op.code), pp[0], sp[0],
+                                               self._pp_sig[0], self.rank, self.p, total,
+                                               self.epoch | ZC_TAG | PUSH_TAG, blocks, edev, scale, st),
+              "mp4x_ipc_allreduce_push")
 
     def allreduce_registered(self, view: torch.Tensor, op, peers, scale: float = 1.0) -> torch.Tensor:
         """In-place two-shot straight on the registered tensors (see :meth:`register`): ONE
@@ -409,33 +487,40 @@ class IpcAllreduce:
         return view
 
     def selftest_zero_copy(self, n: int) -> int:
-        """Collective exact-pattern run of the zero-copy two-shot (f32 SUM, ``n`` elements) on a
-        dedicated plain device allocation per rank, mapped into every peer like a registered
-        tensor.  Returns the number of wrong elements on this rank (-1: setup failed here)."""
+        """Collective exact-pattern run of the zero-copy two-shot, pull AND push forms (f32 SUM,
+        ``n`` elements) on a dedicated plain device allocation per rank, mapped into every peer
+        like a registered tensor (+ a push scratch).  Returns the number of wrong elements on
+        this rank over both runs (-1: setup failed here)."""
         nbytes = n * 4
-        ptr, opened, err = c_void_p(), [], None
+        ptr, scr, opened, err = c_void_p(), c_void_p(), [], None
         hs = self.lib.mp4x_ipc_handle_size()
+        chunk = -(-(nbytes // 16) // self.p)
         try:
             check(self.lib.mp4x_dev_alloc(nbytes, ctypes.byref(ptr)), "dev_alloc")
+            check(self.lib.mp4x_ipc_alloc((self.p - 1) * chunk * 16, ctypes.byref(scr)), "ipc_alloc(scratch)")
             h = ctypes.create_string_buffer(hs)
+            hsc = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(ptr, h), "ipc_get_handle(selftest)")
-            blob = h.raw
+            check(self.lib.mp4x_ipc_get_handle(scr, hsc), "ipc_get_handle(selftest scratch)")
+            blob = (h.raw, hsc.raw)
         except Exception as e:   # noqa: BLE001
             err, blob = str(e), None
         allh = self.comm.server.call("allgather_obj", self.rank, (blob, err))
         bad = -1 if any(e for _, e in allh) else 0
-        peers = []
+        peers, scrs = [], []
         if bad == 0:
             try:
                 for r, (b, _) in enumerate(allh):
                     if r == self.rank:
                         peers.append(ptr.value)
+                        scrs.append(scr.value)
                         continue
-                    q = c_void_p()
-                    check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(b), hs), ctypes.byref(q)),
-                          "ipc_open_handle(selftest)")
-                    opened.append(q)
-                    peers.append(q.value)
+                    for hb, lst in ((b[0], peers), (b[1], scrs)):
+                        q = c_void_p()
+                        check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(hb), hs),
+                                                            ctypes.byref(q)), "ipc_open_handle(selftest)")
+                        opened.append(q)
+                        lst.append(q.value)
             except Exception:   # noqa: BLE001
                 bad = -1
         oks = self.comm.server.call("allgather_obj", self.rank, bad)
@@ -444,23 +529,31 @@ class IpcAllreduce:
             op = for_dtype(Operators.Float.SUM, DType.F32)
             i = torch.arange(n, device="cuda", dtype=torch.int32) % 13
             mine = (i + self.rank).float()
-            st = stream_ptr()
-            check(self.lib.mp4x_memcpy_async(ptr.value, mine.data_ptr(), nbytes, st), "selftest fill")
-            self.comm.server.call("barrier", self.rank)     # (the fill is stream-ordered before the kernel)
-            self.allreduce_registered_ptrs(ptr.value, nbytes, op, peers, torch.float32)
-            got = torch.empty(n, device="cuda")
-            check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr.value, nbytes, st), "selftest read")
-            torch.cuda.synchronize()
             exp = (i * self.p + self.p * (self.p - 1) // 2).float()
-            bad = int((got != exp).sum())
+            got = torch.empty(n, device="cuda")
+            st = stream_ptr()
+            for push in (False, True):
+                check(self.lib.mp4x_memcpy_async(ptr.value, mine.data_ptr(), nbytes, st), "selftest fill")
+                torch.cuda.synchronize()
+                self.comm.server.call("barrier", self.rank)     # every rank's fill is done
+                if push:
+                    self._push_ptrs(nbytes, op, peers, scrs, torch.float32)
+                else:
+                    self.allreduce_registered_ptrs(ptr.value, nbytes, op, peers, torch.float32)
+                check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr.value, nbytes, st), "selftest read")
+                torch.cuda.synchronize()
+                bad += int((got != exp).sum())
+                self.comm.server.call("barrier", self.rank)     # peers are done before the refill
         elif bad == 0:
             bad = -1
         torch.cuda.synchronize()
-        self.comm.server.call("barrier", self.rank)         # every peer is done reading before unmapping
+        self.comm.server.call("barrier", self.rank)         # every peer is done before unmapping
         for q in opened:
             self.lib.mp4x_ipc_close_handle(q)
         if ptr:
             self.lib.mp4x_ipc_free(ptr)
+        if scr:
+            self.lib.mp4x_ipc_free(scr)
         return bad
 
     def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0) -> None:
@@ -472,7 +565,7 @@ class IpcAllreduce:
         if edev is not None:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
-            self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
+            self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
         blocks = max(1, min(self.max_blocks, -(-total // 16 // 512))) if self.max_blocks else 0
         pp = ptr_array(peers)
         check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
@@ -497,7 +590,7 @@ class IpcAllreduce:
             return self._epoch_dev.data_ptr()
         if torch.cuda.is_current_stream_capturing():
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
-        self.epoch = (self.epoch + 1) & 0x7FFFFFFF or 1
+        self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
         return None
 
     def _blocks_for(self, nvec: int) -> int:
@@ -946,3 +1039,6 @@ class IpcAllreduce:
         if self._herr:
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
+        for ptr in getattr(self, "_scratch_allocs", []):
+            self.lib.mp4x_ipc_free(ptr)
+        self._scratch_allocs = []

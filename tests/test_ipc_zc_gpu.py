@@ -128,16 +128,19 @@ def _zc_fn(comm, sizes):
     return res, err, eng._ipc_obj.error_word()
 
 
+@pytest.mark.parametrize("algo", ["ipc2z", "ipc2w"])
 @pytest.mark.parametrize("p", [2, 4])
-def test_zero_copy_registered_two_shot_exact(p):
-    # 1 MiB (default two-shot tier) and 96 MiB (above the 64 MiB staging buffer: no pieces)
-    out = run_spawn(p, _zc_fn, args=([1 << 18, 24 << 20],), env={"MP4X_DEVICE_ALGO": "ipc2z"})
+def test_zero_copy_registered_two_shot_exact(p, algo):
+    """Pull (ipc2z) and push (ipc2w: every peer transfer a posted write) forms of the zero-copy
+    two-shot: 1 MiB (default two-shot tier) and 96 MiB (above the 64 MiB staging buffer: no
+    pieces), full range and an offset [from, to) view, exact; random data vs fp64."""
+    out = run_spawn(p, _zc_fn, args=([1 << 18, 24 << 20],), env={"MP4X_DEVICE_ALGO": algo})
     for r, (res, err, ew) in out.items():
         assert ew == 0
         for n, frm, to, reg, bad, used in res:
             assert reg, (r, n)
             assert bad == 0, (r, n, frm, to, bad)
-            assert used.get("allreduce.ipc2z") == 1, (r, n, used)
+            assert used.get("allreduce." + algo) == 1, (r, n, used)
         assert err < 1e-4 * p, err
 
 
@@ -236,9 +239,10 @@ def _scale_fn(comm):
     r, p = comm.getRank(), comm.getSlaveNum()
     eng = comm.device
     res = {}
-    for algo, n in (("ipc1", 4096), ("ipc2", 1 << 18), ("ipc2z", 1 << 18), ("rccl", 4096), ("a2a", 4096)):
+    for algo, n in (("ipc1", 4096), ("ipc2", 1 << 18), ("ipc2z", 1 << 18), ("ipc2w", 1 << 18), ("rccl", 4096),
+                    ("a2a", 4096)):
         x = _pattern(n, r)
-        if algo == "ipc2z":
+        if algo in ("ipc2z", "ipc2w"):
             assert comm.registerBuffer(x)
         exp = _expect(n, p) * 0.25
         eng.algo = algo
