@@ -527,22 +527,27 @@ class IpcAllreduce:
         if all(o == 0 for o in oks):
             from ..operators import Operators, for_dtype, DType
             op = for_dtype(Operators.Float.SUM, DType.F32)
-            i = torch.arange(n, device="cuda", dtype=torch.int32) % 13
-            mine = (i + self.rank).float()
-            exp = (i * self.p + self.p * (self.p - 1) // 2).float()
             got = torch.empty(n, device="cuda")
             st = stream_ptr()
-            for push in (False, True):
+            # each form twice on new data: the second run would read any stale cache line the
+            # first one left behind on this topology
+            for push, salt in ((False, 0), (True, 1)):
+                i = (torch.arange(n, device="cuda", dtype=torch.int32) + salt) % 13
+                mine = (i + self.rank).float()
+                exp = (i * self.p + self.p * (self.p - 1) // 2).float()
                 check(self.lib.mp4x_memcpy_async(ptr.value, mine.data_ptr(), nbytes, st), "selftest fill")
                 torch.cuda.synchronize()
                 self.comm.server.call("barrier", self.rank)     # every rank's fill is done
-                if push:
-                    self._push_ptrs(nbytes, op, peers, scrs, torch.float32)
-                else:
-                    self.allreduce_registered_ptrs(ptr.value, nbytes, op, peers, torch.float32)
-                check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr.value, nbytes, st), "selftest read")
-                torch.cuda.synchronize()
-                bad += int((got != exp).sum())
+                # twice: the second call reduces the first call's RESULT in place (as a training
+                # loop does), so a stale cache line left by the first call would show
+                for rep in range(2):
+                    if push:
+                        self._push_ptrs(nbytes, op, peers, scrs, torch.float32)
+                    else:
+                        self.allreduce_registered_ptrs(ptr.value, nbytes, op, peers, torch.float32)
+                    check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr.value, nbytes, st), "selftest read")
+                    torch.cuda.synchronize()
+                    bad += int((got != exp * (self.p ** rep)).sum())
                 self.comm.server.call("barrier", self.rank)     # peers are done before the refill
         elif bad == 0:
             bad = -1
