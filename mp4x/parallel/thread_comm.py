@@ -200,6 +200,15 @@ class ThreadCommSlave:
     def process(self) -> ProcessCommSlave:
         return self.processCommSlave
 
+    def registerBuffer(self, tensor) -> bool:
+        """Pass-through to ``ProcessCommSlave.registerBuffer`` (one thread per process, collective
+        over the processes): the tensor the process phase allreduces (the root thread's) runs
+        zero-copy."""
+        return self.processCommSlave.registerBuffer(tensor)
+
+    def deregisterBuffer(self, tensor) -> None:
+        self.processCommSlave.deregisterBuffer(tensor)
+
     # ------------------------------------------------------------------ thread-phase primitives
     def _publish(self, obj) -> None:
         self._slots[self.getThreadId()] = obj

@@ -298,3 +298,37 @@ def test_piecewise_ipc_data_movement_above_the_direct_tier():
         assert all(ok.values()), (r, ok)
         for k in ("broadcast", "scatter", "gather", "allgather"):
             assert stats.get(f"{k}.ipc_large") == 1, (r, stats)
+
+
+# ------------------------------------------------------------------ capture above the two-shot tier
+def _capture_large_fn(comm):
+    """the large-message IPC instance is created during capture()'s warm-up; it must be
+    switched to device epochs before the graph is captured (it used to raise mid-capture)."""
+    from mp4x import Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    n = 5 << 20                                   # 20 MiB f32 > the 16 MiB two-shot tier
+    x = torch.zeros(n, device="cuda")
+    w = torch.zeros(n, device="cuda")
+    assert comm.registerBuffer(w)
+
+    def step():
+        eng.allreduce(x, 0, n, Operators.Float.SUM)                  # staged pieces (ipc_large)
+        eng.allreduce(w, 0, n, Operators.Float.SUM, scale=0.5)       # zero-copy, fused scale
+    g = eng.capture(step)
+    bad = 0
+    for i in range(4):
+        x.copy_(_pattern(n, r + i))
+        w.copy_(_pattern(n, r + i))
+        g.replay()
+        torch.cuda.synchronize()
+        exp = sum(_pattern(n, j + i) for j in range(p))
+        bad += int((x != exp).sum()) + int((w != exp * 0.5).sum())
+    return bad, dict(eng.stats)
+
+
+def test_capture_large_and_zero_copy_allreduce():
+    out = run_spawn(2, _capture_large_fn, env={"MP4X_DEVICE_ALGO": "ipc2"})
+    for r, (bad, stats) in out.items():
+        assert bad == 0, (r, bad, stats)
+        assert stats.get("allreduce.ipc2z", 0) >= 3 and stats.get("allreduce.ipc2", 0) >= 3, stats
