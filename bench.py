@@ -67,6 +67,8 @@ def main():
                     help="skip the warm-up schedule autotune (RCCL vs IPC two-shot vs a2a) for N>1")
     ap.add_argument("--no-register", action="store_true",
                     help="do not register the buffer for the zero-copy IPC two-shot")
+    ap.add_argument("--no-tier-sweep", action="store_true",
+                    help="N>1: skip the untimed per-size schedule sweep (4 KiB .. 64 MiB) run after the timed steps")
     args = ap.parse_args()
     if args.algo:
         os.environ["MP4X_DEVICE_ALGO"] = args.algo
@@ -149,6 +151,19 @@ def main():
             dist.all_reduce(vals, op=dist.ReduceOp.MAX)
     wall, p50, p99 = vals.tolist()
 
+    # after the timed steps (never inside them): measure every schedule at the size classes
+    # the IPC tiers are chosen for, so a multi-GPU run records the tier boundaries on real links
+    tiers = None
+    if p > 1 and not args.cpu and not args.no_tier_sweep and not (args.algo or args.codec):
+        tiers = {}
+        for nb in (4 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+            try:
+                res = comm.device.autotune_allreduce(torch.empty(nb // 4, device=dev), op, iters=3)
+                tiers[str(nb)] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in res.items()}
+            except Exception as e:   # noqa: BLE001 — evidence only; the headline is already measured
+                tiers[str(nb)] = {"error": str(e)[:200]}
+                break
+
     ms_per_step = wall * 1e3 / args.steps
     nbytes = n * 4
     algbw = nbytes / (ms_per_step * 1e-3) / 1e9
@@ -179,7 +194,7 @@ def main():
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
                        "payload_bytes": nbytes, "algo": algo, "registered": registered,
                        "in_place": p > 1, "autotune_ms": tuned, "ipc_selftest": selftest,
-                       "calls": stats},
+                       "calls": stats, "tier_sweep_ms": tiers},
             "busbw_gbps_per_rank": round(busbw, 3),
             "aggregate_busbw_gbps": round(busbw * p, 3),
             "algbw_gbps": round(algbw, 3),
