@@ -18,14 +18,15 @@ def _free_port():
     return port
 
 
-@pytest.mark.parametrize("mode,p,threads", [("process", 3, 1), ("thread", 2, 2)])
-def test_master_and_check_tool_cli(tmp_path, mode, p, threads):
+@pytest.mark.parametrize("mode,p,threads,compress", [("process", 3, 1, "false"), ("thread", 2, 2, "false"),
+                                                     ("process", 2, 1, "true"), ("thread", 2, 3, "true")])
+def test_master_and_check_tool_cli(tmp_path, mode, p, threads, compress):
     port = _free_port()
     env = dict(os.environ, PYTHONPATH=ROOT, MP4X_EXCEPTION_SLEEP="0.1", MP4X_MASTER_BIND="127.0.0.1")
     master = subprocess.Popen([sys.executable, "-m", "mp4x.control.master", str(p), str(port)], cwd=tmp_path,
                               env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
     slaves = [subprocess.Popen([sys.executable, "-m", "mp4x.check", "tester", "127.0.0.1", str(port), "5000", "50",
-                                "2", str(threads), mode, "false", "true"], cwd=tmp_path, env=env,
+                                "2", str(threads), mode, compress, "true"], cwd=tmp_path, env=env,
                                stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for _ in range(p)]
     try:
         outs = [s.communicate(timeout=240)[0] for s in slaves]
