@@ -1276,6 +1276,10 @@ class DeviceEngine:
         algo = self.select("reduce_scatter", whole.numel() * whole.element_size(), op, whole.dtype, operand)
         if algo == "fp8":
             algo = "a2a"    # exact path for ragged RS; fp8 RS is used inside the compressed allreduce
+        if algo in ("rccl", "a2a") and self._zc_ok(whole) and self._ipc_obj.reduce_scatter_registered(flat, froms,
+                                                                                                        tos, op):
+            self._count("reduce_scatter.ipc_zc")       # registered tensor: zero copy, any size
+            return arr
         if algo in ("rccl", "a2a") and self._ipc_direct_ok(op, whole):
             if self._ipc_obj.reduce_scatter(flat, froms, tos, op):
                 self._count("reduce_scatter.ipc")
@@ -1311,6 +1315,9 @@ class DeviceEngine:
     def allgather(self, arr: torch.Tensor, froms, tos):
         flat = self._flat(arr)
         whole = flat[froms[0]:tos[-1]]
+        if whole.numel() and self._zc_ok(whole) and self._ipc_obj.allgather_registered(flat, froms, tos):
+            self._count("allgather.ipc_zc")            # registered tensor: zero copy, any size
+            return arr
         if whole.numel() and self._ipc_direct_ok(None, whole) and self._ipc_obj.allgather(flat, froms, tos):
             self._count("allgather.ipc")
             return arr
@@ -1345,6 +1352,13 @@ class DeviceEngine:
     def _rsag_key(kind: str, whole: torch.Tensor, op) -> tuple:
         return (kind, whole.dtype, int(op.code) if op is not None else -1,
                 max(0, whole.numel() * whole.element_size() - 1).bit_length())
+
+    def _zc_ok(self, whole: torch.Tensor) -> bool:
+        """Zero-copy RS / AG on a registered tensor (no schedule forced otherwise).  Whether the
+        range is registered is decided per rank; registration is collective, and a rank running
+        the other protocol fails the call at once (epoch tag), it cannot mix buffers."""
+        return self._zc and whole.is_cuda and self._ipc_obj is not None and self.ipc_enabled and \
+            self.algo in ("", "auto", "ipc2", "ipc2z", "ipc") and bool(self._ipc_obj._regs)
 
     def _ipc_direct_ok(self, op, whole: torch.Tensor) -> bool:
         """Direct IPC reduce-scatter / all-gather tier: up to the two-shot size, unless a schedule

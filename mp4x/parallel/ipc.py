@@ -578,6 +578,64 @@ class IpcAllreduce:
                                              self.epoch | ZC_TAG, blocks, edev, scale, st),
               "mp4x_ipc_allreduce(zero-copy)")
 
+    # ---------------------------------------------------------------- zero-copy RS / AG
+    # On a registered tensor the direct reduce-scatter / all-gather kernels read the peers'
+    # tensors themselves: rank r reduces segment r from every peer straight into its own
+    # segment r (peers only read THEIR segment of it), or pulls every peer's segment into its
+    # own tensor (peers only read ITS segment).  One launch at any size, no staging or copy-out.
+    def _zc_segs(self, flat: torch.Tensor, froms, tos):
+        es = flat.element_size()
+        base = froms[0]
+        rng = flat[base:tos[-1]]
+        if not self._zc_regs_ok(rng):
+            return None
+        peers = self.registered(rng)
+        if peers is None or rng.data_ptr() % 16:
+            return None
+        if not all(((f - base) * es) % 16 == 0 and ((t - base) * es) % 16 == 0 for f, t in zip(froms, tos)):
+            return None
+        lo = [(f - base) * es // 16 for f in froms]
+        hi = [(t - base) * es // 16 for t in tos]
+        return rng, peers, lo, hi
+
+    def _zc_regs_ok(self, rng: torch.Tensor) -> bool:
+        return bool(self._regs) and rng.numel() > 0 and \
+            (not torch.cuda.is_current_stream_capturing() or self._epoch_dev is not None)
+
+    def reduce_scatter_registered(self, flat: torch.Tensor, froms, tos, op) -> bool:
+        z = self._zc_segs(flat, froms, tos) if self.supports(flat, op) else None
+        if z is None:
+            return False
+        self.raise_if_failed()
+        rng, peers, lo, hi = z
+        r = self.rank
+        st = stream_ptr()
+        edev = self._next_epoch(st)
+        pp = ptr_array(peers)
+        maxv = max(h - l_ for l_, h in zip(lo, hi))
+        check(self.lib.mp4x_ipc_reduce_scatter(int(dtype_of_torch(flat.dtype)), int(op.code), pp[0], self._pp_sig[0],
+                                               r, self.p, lo[r], hi[r], rng.data_ptr() + lo[r] * 16,
+                                               self.epoch | ZC_TAG, self._grid(maxv), edev, st),
+              "mp4x_ipc_reduce_scatter(zero-copy)")
+        return True
+
+    def allgather_registered(self, flat: torch.Tensor, froms, tos) -> bool:
+        z = self._zc_segs(flat, froms, tos)
+        if z is None:
+            return False
+        self.raise_if_failed()
+        rng, peers, lo, hi = z
+        st = stream_ptr()
+        edev = self._next_epoch(st)
+        pp = ptr_array(peers)
+        lo_a = (c_int64 * self.p)(*lo)
+        hi_a = (c_int64 * self.p)(*hi)
+        maxv = max(h - l_ for l_, h in zip(lo, hi))
+        check(self.lib.mp4x_ipc_allgather(pp[0], self._pp_sig[0], self.rank, self.p, lo_a, hi_a, rng.data_ptr(),
+                                          self.epoch | ZC_TAG, self._grid(maxv), edev, st),
+              "mp4x_ipc_allgather(zero-copy)")
+        return True
+
     # ---------------------------------------------------------------- RS / AG over ragged ranges
     # Results are produced inside the staging buffer (always 16-byte aligned) and copied out, so
     # whether a call qualifies depends only on the (rank-independent) ranges: every rank takes

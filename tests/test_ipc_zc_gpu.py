@@ -332,3 +332,38 @@ def test_capture_large_and_zero_copy_allreduce():
     for r, (bad, stats) in out.items():
         assert bad == 0, (r, bad, stats)
         assert stats.get("allreduce.ipc2z", 0) >= 3 and stats.get("allreduce.ipc2", 0) >= 3, stats
+
+
+# ------------------------------------------------------------------ zero-copy reduce-scatter / all-gather
+def _zc_rsag_fn(comm):
+    from mp4x import CommUtils, Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    B = Operands.BF16_OPERAND()
+    n = (20 << 20) // 2                            # 20 MiB of bf16: above the 16 MiB direct tier
+    counts = [(n // p) // 8 * 8 + (8 if j == 0 else 0) for j in range(p)]
+    counts[-1] = n - sum(counts[:-1]) - 64
+    froms = CommUtils.getFromsFromCount(32, counts, p)
+    tos = CommUtils.getTosFromCount(32, counts, p)
+    x = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    assert comm.registerBuffer(x)
+    i = torch.arange(n, device="cuda")
+    x.copy_((i % 11 + r).to(torch.bfloat16))
+    comm.reduceScatterArray(x, B, Operators.BFloat16.SUM, 32, counts)
+    exp = (p * (i % 11) + p * (p - 1) // 2).to(torch.bfloat16)
+    ok_rs = bool(torch.equal(x[froms[r]:tos[r]], exp[froms[r]:tos[r]]))
+    ok_out = bool(torch.equal(x[:froms[0]], (i[:froms[0]] % 11 + r).to(torch.bfloat16)))
+    y = torch.full((n,), -1, dtype=torch.bfloat16, device="cuda")
+    assert comm.registerBuffer(y)
+    y[froms[r]:tos[r]] = r
+    comm.allgatherArray(y, B, froms, tos)
+    ok_ag = all(bool((y[froms[j]:tos[j]] == j).all()) for j in range(p))
+    torch.cuda.synchronize()
+    return ok_rs, ok_out, ok_ag, dict(comm.device.stats)
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_zero_copy_reduce_scatter_allgather_registered(p):
+    out = run_spawn(p, _zc_rsag_fn)
+    for r, (ok_rs, ok_out, ok_ag, stats) in out.items():
+        assert ok_rs and ok_out and ok_ag, (r, ok_rs, ok_out, ok_ag)
+        assert stats.get("reduce_scatter.ipc_zc") == 1 and stats.get("allgather.ipc_zc") == 1, stats
