@@ -432,6 +432,9 @@ class IpcAllreduce:
             return None
         a = view.data_ptr()
         n = view.numel() * view.element_size()
+        hit = self._regs.get((a, n))            # the whole registered tensor: O(1)
+        if hit is not None:
+            return hit[0]
         for (ptr, nb), (peers, _) in self._regs.items():
             if ptr <= a and a + n <= ptr + nb:
                 d = a - ptr
@@ -442,6 +445,9 @@ class IpcAllreduce:
         """Every rank's push scratch for ``view``'s registered tensor, or None (no push form)."""
         a = view.data_ptr()
         n = view.numel() * view.element_size()
+        hit = self._regs.get((a, n))
+        if hit is not None:
+            return hit[1]
         for (ptr, nb), (_, scr) in self._regs.items():
             if ptr <= a and a + n <= ptr + nb:
                 return scr
