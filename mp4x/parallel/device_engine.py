@@ -559,6 +559,8 @@ class DeviceEngine:
         or RCCL's ncclAvg, instead of a separate pass over the buffer."""
         flat = self._flat(arr)
         view = flat[frm:to]
+        if scale != 1.0 and not view.is_floating_point():
+            raise Mp4jException("allreduce scale= needs a floating-point tensor")
         if out is not None:
             oview = self._flat(out)[frm:to]
             if view.numel() == 0:
