@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -565,9 +566,21 @@ extern "C" int mp4x_tbarrier_wait(void* h) {
 // in thread order — the reference's thread reduce, ThreadCommSlave.java:259-303) and the
 // copy-back all run in C++.  Python pays one GIL release/re-acquire per phase instead of one
 // per barrier.
+//
+// GIL hand-off.  When a collective returns, every thread wants the GIL at once: all but one
+// sleep on CPython's GIL condition variable and are woken by a futex when the holder next
+// releases it -- that wake-up, not the data movement, used to dominate a small call (~20 us of
+// BASELINE config 1's 2-thread float[1024] allreduce).  So the threads leave in a chain: thread
+// 0 returns at once; thread t keeps spinning HERE (GIL still released) until thread t-1 has
+// entered its next team call -- ctypes released the GIL before that entry -- and only then
+// returns, to find the GIL free.  The threads' Python then runs back to back with no sleeping
+// hand-off.  The spin is bounded (MP4X_TEAM_HANDOFF_US, default 30; 0 turns it off), so a peer
+// that does other work between calls costs at most that much spinning, never a hang.
 struct Team {
   TBarrier bar;
   std::vector<void*> slots;
+  std::unique_ptr<std::atomic<uint64_t>[]> entered;   // team calls entered, per thread
+  double handoff_s = 30e-6;
 };
 
 extern "C" void* mp4x_team_create(int n, double timeout_s) {
@@ -576,11 +589,39 @@ extern "C" void* mp4x_team_create(int n, double timeout_s) {
   t->bar.n = (uint32_t)n;
   t->bar.timeout_s = timeout_s > 0 ? timeout_s : 1e30;
   t->slots.assign(n, nullptr);
+  t->entered.reset(new std::atomic<uint64_t>[n]);
+  for (int i = 0; i < n; ++i) t->entered[i].store(0, std::memory_order_relaxed);
+  if (const char* e = std::getenv("MP4X_TEAM_HANDOFF_US")) t->handoff_s = std::atof(e) * 1e-6;
   return t;
 }
 
+// Every team call starts here: count the entry (what thread tid+1's team_leave waits for).
+static inline uint64_t team_enter(Team* tm, int tid) {
+  return tm->entered[tid].fetch_add(1, std::memory_order_acq_rel) + 1;
+}
+
+// Every team call ends here: `k` is this call's sequence number (team calls are collective, so
+// thread tid-1's k-th call is the same collective); wait, bounded, for its (k+1)-th.
+static inline int team_leave(Team* tm, int tid, uint64_t k, int rc) {
+  if (rc || tid == 0 || tm->handoff_s <= 0) return rc;
+  const std::atomic<uint64_t>& prev = tm->entered[tid - 1];
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1; prev.load(std::memory_order_acquire) <= k; ++i) {
+    if (tm->bar.abort.load(std::memory_order_relaxed)) break;
+    __builtin_ia32_pause();
+    if ((i & 31) == 0 &&
+        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tm->handoff_s)
+      break;
+  }
+  return rc;
+}
+
 extern "C" void mp4x_team_destroy(void* h) { delete (Team*)h; }
-extern "C" int mp4x_team_barrier(void* h) { return mp4x_tbarrier_wait(&((Team*)h)->bar); }
+extern "C" int mp4x_team_barrier(void* h, int tid) {
+  Team* tm = (Team*)h;
+  const uint64_t k = team_enter(tm, tid);
+  return team_leave(tm, tid, k, mp4x_tbarrier_wait(&tm->bar));
+}
 extern "C" int mp4x_team_aborted(void* h) { return mp4x_tbarrier_aborted(&((Team*)h)->bar); }
 extern "C" void mp4x_team_abort(void* h) { mp4x_tbarrier_abort(&((Team*)h)->bar); }
 
@@ -590,52 +631,72 @@ static inline void team_chunk(int64_t f, int64_t t, int T, int tid, int64_t* lo,
   *hi = f + n * (tid + 1) / T;
 }
 
-static int team_reduce_phase(Team* tm, int tid, void* buf, int64_t f, int64_t t, int dtype, int op, int root) {
+// Thread tid's chunk of [f, t): all T buffers reduced into the root's (root's value first, then
+// the others in thread order); with `spread`, the result also copied into every other buffer's
+// chunk (the chunks are disjoint, so that needs no extra barrier).
+static int team_reduce_chunk(Team* tm, int tid, int64_t f, int64_t t, int dtype, int op, int root, bool spread) {
   const int T = (int)tm->bar.n;
-  tm->slots[tid] = buf;
-  if (int rc = mp4x_tbarrier_wait(&tm->bar)) return rc;
   const int es = esize(dtype);
   int64_t lo, hi;
   team_chunk(f, t, T, tid, &lo, &hi);
-  if (hi > lo) {
-    std::vector<const void*> ins;
-    ins.reserve(T);
-    ins.push_back((const char*)tm->slots[root] + lo * es);
-    for (int j = 0; j < T; ++j)
-      if (j != root) ins.push_back((const char*)tm->slots[j] + lo * es);
-    if (int rc = host_reduce(dtype, op, (char*)tm->slots[root] + lo * es, ins.data(), T, hi - lo, 1)) {
-      mp4x_tbarrier_abort(&tm->bar);
-      return rc;
-    }
+  if (hi <= lo) return 0;
+  const void* ins[64];
+  std::vector<const void*> big;
+  const void** in = ins;
+  if (T > 64) {
+    big.resize(T);
+    in = big.data();
   }
-  return mp4x_tbarrier_wait(&tm->bar);
+  int m = 0;
+  in[m++] = (const char*)tm->slots[root] + lo * es;
+  for (int j = 0; j < T; ++j)
+    if (j != root) in[m++] = (const char*)tm->slots[j] + lo * es;
+  char* out = (char*)tm->slots[root] + lo * es;
+  if (int rc = host_reduce(dtype, op, out, in, T, hi - lo, 1)) return rc;
+  if (spread)
+    for (int j = 0; j < T; ++j)
+      if (j != root) std::memcpy((char*)tm->slots[j] + lo * es, out, (hi - lo) * es);
+  return 0;
 }
 
-static int team_bcast_phase(Team* tm, int tid, void* buf, int64_t f, int64_t t, int es, int root) {
-  if (tid != root && t > f) std::memcpy((char*)buf + f * es, (const char*)tm->slots[root] + f * es, (t - f) * es);
+static int team_reduce_phase(Team* tm, int tid, void* buf, int64_t f, int64_t t, int dtype, int op, int root,
+                             bool spread) {
+  tm->slots[tid] = buf;
+  if (int rc = mp4x_tbarrier_wait(&tm->bar)) return rc;
+  if (int rc = team_reduce_chunk(tm, tid, f, t, dtype, op, root, spread)) {
+    mp4x_tbarrier_abort(&tm->bar);
+    return rc;
+  }
   return mp4x_tbarrier_wait(&tm->bar);
 }
 
 // [f, t) of every thread's buffer reduced into the root thread's buffer (then a barrier).
 extern "C" int mp4x_team_reduce(void* h, int tid, void* buf, int64_t f, int64_t t, int dtype, int op, int root) {
   if (!esize(dtype)) return MP4X_E_UNSUPPORTED;
-  return team_reduce_phase((Team*)h, tid, buf, f, t, dtype, op, root);
+  Team* tm = (Team*)h;
+  const uint64_t k = team_enter(tm, tid);
+  return team_leave(tm, tid, k, team_reduce_phase(tm, tid, buf, f, t, dtype, op, root, false));
 }
 
 // Root's [f, t) copied into every other thread's buffer: publish, barrier, copy, barrier.
 extern "C" int mp4x_team_bcast(void* h, int tid, void* buf, int64_t f, int64_t t, int elem_bytes, int root) {
   Team* tm = (Team*)h;
+  const uint64_t k = team_enter(tm, tid);
   tm->slots[tid] = buf;
-  if (int rc = mp4x_tbarrier_wait(&tm->bar)) return rc;
-  return team_bcast_phase(tm, tid, buf, f, t, elem_bytes, root);
+  int rc = mp4x_tbarrier_wait(&tm->bar);
+  if (!rc) {
+    if (tid != root && t > f)
+      std::memcpy((char*)buf + f * elem_bytes, (const char*)tm->slots[root] + f * elem_bytes, (t - f) * elem_bytes);
+    rc = mp4x_tbarrier_wait(&tm->bar);
+  }
+  return team_leave(tm, tid, k, rc);
 }
 
-// Fused thread-level allreduce (slaveNum == 1): publish, barrier, chunked reduce into thread
-// 0's buffer, barrier, copy-back, barrier.
+// Fused thread-level allreduce (slaveNum == 1): publish, barrier, each thread reduces its chunk
+// of every buffer and writes the result into every buffer's chunk, barrier.  Two meetings.
 extern "C" int mp4x_team_allreduce(void* h, int tid, void* buf, int64_t f, int64_t t, int dtype, int op) {
+  if (!esize(dtype)) return MP4X_E_UNSUPPORTED;
   Team* tm = (Team*)h;
-  const int es = esize(dtype);
-  if (!es) return MP4X_E_UNSUPPORTED;
-  if (int rc = team_reduce_phase(tm, tid, buf, f, t, dtype, op, 0)) return rc;
-  return team_bcast_phase(tm, tid, buf, f, t, es, 0);
+  const uint64_t k = team_enter(tm, tid);
+  return team_leave(tm, tid, k, team_reduce_phase(tm, tid, buf, f, t, dtype, op, 0, true));
 }

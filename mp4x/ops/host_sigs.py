@@ -25,7 +25,7 @@ HOST_SIGS = {
     "mp4x_team_create": (c_void_p, [c_int, c_double]),
     "mp4x_team_destroy": (None, [c_void_p]),
     "mp4x_team_abort": (None, [c_void_p]),
-    "mp4x_team_barrier": (c_int, [c_void_p]),
+    "mp4x_team_barrier": (c_int, [c_void_p, c_int]),
     "mp4x_team_aborted": (c_int, [c_void_p]),
     "mp4x_team_reduce": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_int, c_int, c_int]),
     "mp4x_team_bcast": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_int, c_int]),

@@ -122,6 +122,39 @@ def host():
     return _host
 
 
+_team_ext = None
+
+
+def team_ext():
+    """The CPython binding of the host thread team (``_mp4x_team``, csrc/pyext/team_ext.cpp), or
+    None when it is not built (ThreadCommSlave then calls the team through ctypes)."""
+    global _team_ext
+    if _team_ext is None:
+        try:
+            host()              # the extension links libmp4x_host.so: load it first (own lock)
+        except Exception:
+            pass
+        with _lock:
+            if _team_ext is None:
+                mod = False
+                try:
+                    if os.environ.get("MP4X_TEAM_EXT", "1") == "0":
+                        raise NativeUnavailable("MP4X_TEAM_EXT=0")
+                    import importlib.machinery
+                    import importlib.util
+                    for suf in importlib.machinery.EXTENSION_SUFFIXES:
+                        path = os.path.join(NATIVE_DIR, "_mp4x_team" + suf)
+                        if os.path.exists(path):
+                            spec = importlib.util.spec_from_file_location("_mp4x_team", path)
+                            mod = importlib.util.module_from_spec(spec)
+                            spec.loader.exec_module(mod)
+                            break
+                except Exception:
+                    mod = False
+                _team_ext = mod
+    return _team_ext or None
+
+
 def available() -> bool:
     try:
         hip()

@@ -53,17 +53,20 @@ class _TeamBarrier:
         self._py = threading.Barrier(n)
         self.team = None
         self._lib = None
+        self.ext = None          # CPython binding of the team (csrc/pyext/team_ext.cpp), if built
         if n > 1:
             try:
                 from ..ops import native
                 self._lib = native.host()
                 self.team = self._lib.mp4x_team_create(n, 0.0)
+                self.ext = native.team_ext() if _TEAM_ON else None
             except Exception:
                 self.team = None
 
-    def wait(self):
+    def wait(self, tid: int = 0):
         if self.team:            # the same native barrier the team phases use (GIL released)
-            if self._lib.mp4x_team_barrier(self.team):
+            rc = self.ext.barrier(self.team, tid) if self.ext else self._lib.mp4x_team_barrier(self.team, tid)
+            if rc:
                 raise threading.BrokenBarrierError("thread barrier aborted")
             return 0
         return self._py.wait()
@@ -89,6 +92,7 @@ class _TeamBarrier:
 
 _TEAM_DTYPES = None
 _TEAM_ON = __import__("os").environ.get("MP4X_THREAD_TEAM", "1") == "1"
+_EXT_NOT_ELIGIBLE, _EXT_OUT_OF_RANGE = -100, -101      # csrc/pyext/team_ext.cpp
 
 
 def _team_dtype(buf, operator):
@@ -107,6 +111,23 @@ def _team_dtype(buf, operator):
     if dt is None or int(getattr(operator, "dtype", dt)) != dt:
         return None
     return dt
+
+
+_OPINFO: Dict[int, tuple] = {}
+
+
+def _op_team_info(operator):
+    """``(operator, op code, dtype code)`` of a built-in operator (cached by identity), or None
+    for a custom one: what the native team binding takes."""
+    e = _OPINFO.get(id(operator))
+    if e is not None and e[0] is operator:
+        return e
+    if getattr(operator, "is_custom", False) or getattr(operator, "code", None) is None:
+        return None
+    if len(_OPINFO) > 4096:
+        _OPINFO.clear()
+    e = _OPINFO[id(operator)] = (operator, int(operator.code), int(operator.dtype))
+    return e
 
 
 class ThreadCommSlave:
@@ -144,13 +165,20 @@ class ThreadCommSlave:
 
     def threadBarrier(self) -> None:
         try:
-            self._barrier.wait()
+            self._barrier.wait(self.getThreadId())
         except threading.BrokenBarrierError as e:
             raise Mp4jException("thread barrier broken") from e
 
     def abort(self) -> None:
         """Break the thread barriers (a failing thread releases its peers with an error)."""
         self._barrier.abort()
+
+    def _team_fail(self, rc: int, frm: int, to: int):
+        self._barrier.abort()
+        if rc == _EXT_OUT_OF_RANGE:
+            CommUtils.isFromToLegal(frm, to)
+            raise Mp4jException(f"[{frm}, {to}) is out of the array's bounds")
+        raise Mp4jException(f"thread team collective failed ({rc})")
 
     def _team_call(self, fn, *args) -> None:
         rc = fn(self._barrier.team, self.getThreadId(), *args)
@@ -217,6 +245,16 @@ class ThreadCommSlave:
     def _thread_reduce_array(self, arr, operand: Operand, operator, f: int, t: int, rt: int):
         """All T arrays' [f, t) reduced into thread rt's array (rt's value first, then threads in order)."""
         tid = self.getThreadId()
+        ext = self._barrier.ext
+        if ext is not None and type(arr) is np.ndarray:
+            oi = _op_team_info(operator)
+            if oi is not None:
+                self._slots[tid] = arr
+                rc = ext.reduce(self._barrier.team, tid, arr, f, t, oi[2], oi[1], rt)
+                if rc == 0:
+                    return self._slots[rt]
+                if rc != _EXT_NOT_ELIGIBLE:
+                    self._team_fail(rc, f, t)
         if self._barrier.team and _TEAM_ON and not _is_device_tensor(arr):
             buf = _host_view(arr, operand)
             dt = _team_dtype(buf, operator)
@@ -530,11 +568,39 @@ class ThreadCommSlave:
     def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int):
         if self.threadNum == 1:
             return self.processCommSlave.allreduceArray(arrData, operand, operator, frm, to)
+        ext = self._barrier.ext
+        if ext is not None and type(arrData) is np.ndarray:
+            # the hot path (BASELINE config 1): one FASTCALL into the team per phase; the binding
+            # checks the array (1-D, C-contiguous, the operator's dtype, [frm, to) in bounds)
+            oi = _op_team_info(operator)
+            if oi is not None:
+                team, tid = self._barrier.team, getattr(self._tls, "tid", 0)
+                if self.slaveNum == 1:
+                    rc = ext.allreduce(team, tid, arrData, frm, to, oi[2], oi[1])
+                    if rc == 0:
+                        return arrData
+                    if rc != _EXT_NOT_ELIGIBLE:
+                        self._team_fail(rc, frm, to)
+                else:
+                    rc = ext.reduce(team, tid, arrData, frm, to, oi[2], oi[1], 0)
+                    if rc == 0:
+                        if tid == 0:
+                            try:
+                                self.processCommSlave.allreduceArray(arrData, operand, operator, frm, to)
+                            except BaseException:
+                                self._barrier.abort()
+                                raise
+                        rc = ext.bcast(team, tid, arrData, frm, to, oi[2], 0)
+                        if rc:
+                            self._team_fail(rc, frm, to)
+                        return arrData
+                    if rc != _EXT_NOT_ELIGIBLE:
+                        self._team_fail(rc, frm, to)
         CommUtils.isFromToLegal(frm, to)
         if self._barrier.team and _TEAM_ON and not _is_device_tensor(arrData):
             buf = _host_view(arrData, operand)
             dt = _team_dtype(buf, operator)
-            if dt is not None:       # native thread team: one GIL round trip per phase
+            if dt is not None:       # native thread team through ctypes (binding not built)
                 lib = self._barrier._lib
                 if self.slaveNum == 1:
                     self._team_call(lib.mp4x_team_allreduce, buf.ctypes.data, frm, to, dt, int(operator.code))

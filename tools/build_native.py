@@ -7,6 +7,9 @@
   streams inside one HIP runtime instance.
 * ``mp4x/_native/libmp4x_host.so`` — host runtime (csrc/host/*.cpp): CPU reduction kernels,
   the TCP data-plane engine; plain g++, no GPU dependency.
+* ``mp4x/_native/_mp4x_team*.so`` — CPython extension (csrc/pyext/team_ext.cpp) binding the
+  host runtime's thread team for ThreadCommSlave (buffer protocol + one FASTCALL per phase),
+  linked against libmp4x_host.so next to it (rpath $ORIGIN).
 
 Incremental: objects are rebuilt only when a source or header is newer.
 ``--debug`` builds ``libmp4x_hip_debug.so`` instead: ``-O1 -g -DMP4X_DEBUG``, which turns on the
@@ -132,6 +135,19 @@ def build_host(jobs):
     return out
 
 
+def build_pyext(host_so):
+    import sysconfig
+    src = os.path.join(CSRC, "pyext", "team_ext.cpp")
+    if not host_so or not os.path.exists(src):
+        return None
+    out = os.path.join(OUT, "_mp4x_team" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if newer(src, out, headers()) or os.path.getmtime(host_so) > os.path.getmtime(out):
+        run(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-shared", "-I", sysconfig.get_paths()["include"],
+             src, "-o", out, "-L", OUT, "-l:libmp4x_host.so", "-Wl,-rpath,$ORIGIN"])
+        print("  g++  ", os.path.relpath(src, ROOT), "->", os.path.relpath(out, ROOT))
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
@@ -148,7 +164,7 @@ def main(argv=None):
         build_hip(a.j, debug=True)
         return 0
     build_hip(a.j)
-    build_host(a.j)
+    build_pyext(build_host(a.j))
     return 0
 
 
