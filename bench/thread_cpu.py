@@ -21,6 +21,7 @@ def worker(port, T, n, iters, out):
     from mp4x import Operands, Operators, ThreadCommSlave
     tc = ThreadCommSlave("bench", T, "127.0.0.1", port, heartbeat=False)
     lat = [[] for _ in range(T)]
+    wall = [0.0] * T
 
     def body(t):
         tc.setThreadId(t)
@@ -29,17 +30,22 @@ def worker(port, T, n, iters, out):
         for _ in range(50):
             tc.allreduceArray(a, opnd, op, 0, n)
         tc.threadBarrier()
+        w0 = time.perf_counter()
         for _ in range(iters):
             t0 = time.perf_counter()
             tc.allreduceArray(a, opnd, op, 0, n)
             lat[t].append(time.perf_counter() - t0)
+        wall[t] = time.perf_counter() - w0
+        a[:] = t + 1                                 # one checked call after the timed ones
+        tc.allreduceArray(a, opnd, op, 0, n)
+        assert (a == T * (T + 1) // 2).all()
 
     ths = [threading.Thread(target=body, args=(t,)) for t in range(T)]
     [x.start() for x in ths]
     [x.join() for x in ths]
     tc.close(0)
     per_call = sorted(max(lat[t][i] for t in range(T)) for i in range(iters))
-    out.append(per_call)
+    out.append((per_call, max(wall) / iters))
 
 
 def main():
@@ -53,11 +59,13 @@ def main():
     out = []
     worker(m.port, a.threads, a.n, a.iters, out)
     m.stop(timeout=5)
-    lat = out[0]
+    lat, period = out[0]
+    env = {k: os.environ[k] for k in ("MP4X_TEAM_EXT", "MP4X_TEAM_HANDOFF_US", "MP4X_THREAD_TEAM") if k in os.environ}
     print(json.dumps({"config": f"{a.threads}-thread in-process float[{a.n}] allreduceArray (CPU, ThreadCommSlave)",
                       "p50_us": round(lat[len(lat) // 2] * 1e6, 2),
                       "p99_us": round(lat[int(0.99 * len(lat))] * 1e6, 2),
-                      "calls_per_s": round(1 / (sum(lat) / len(lat)), 1)}))
+                      "period_us": round(period * 1e6, 2),          # wall time per call, back to back
+                      "calls_per_s": round(1 / period, 1), "env": env}))
 
 
 if __name__ == "__main__":

@@ -609,9 +609,11 @@ static inline int team_leave(Team* tm, int tid, uint64_t k, int rc) {
   for (uint32_t i = 1; prev.load(std::memory_order_acquire) <= k; ++i) {
     if (tm->bar.abort.load(std::memory_order_relaxed)) break;
     __builtin_ia32_pause();
-    if ((i & 31) == 0 &&
-        std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tm->handoff_s)
-      break;
+    if ((i & 31) == 0) {
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > tm->handoff_s) break;
+      // if the scheduler put the GIL holder on THIS cpu, spinning would only delay it
+      if ((i & 255) == 0) sched_yield();
+    }
   }
   return rc;
 }
