@@ -23,6 +23,7 @@ take int64 id tensors directly and are what a training loop should call.
 """
 from __future__ import annotations
 
+import itertools
 from collections.abc import MutableMapping
 from typing import Dict, List, Optional
 
@@ -51,7 +52,7 @@ class KeyDictionary:
     def unknown(self, keys) -> List:
         """Keys this rank has never numbered (first-seen order, de-duplicated)."""
         keys = keys if isinstance(keys, (list, tuple)) else list(keys)
-        if not (set(keys) - self.key2id.keys()):      # steady state: one C-level set difference
+        if all(map(self.key2id.__contains__, keys)):  # steady state: one C-level pass, no set built
             return []
         seen = set()
         out = []
@@ -71,6 +72,12 @@ class KeyDictionary:
 
     def ids(self, keys) -> List[int]:
         return [self.key2id[k] for k in keys]
+
+    def lookup(self, keys) -> np.ndarray:
+        """int64 ids of ``keys``, -1 where a key was never numbered (one C-level pass)."""
+        keys = keys if isinstance(keys, (list, tuple)) else list(keys)
+        return np.fromiter(map(self.key2id.get, keys, itertools.repeat(-1, len(keys))), dtype=np.int64,
+                           count=len(keys))
 
     def id_array(self, keys) -> np.ndarray:
         """int64 ids of ``keys`` (one C-level pass)."""
@@ -436,7 +443,16 @@ def _map_tensors(engine, mapData: Dict):
         rows = mapData._rows.view(len(mapData._ids), -1)
         return torch.from_numpy(mapData._ids).to(rows.device), rows, mapData._shape
     keys = list(mapData.keys())
-    _sync_new_keys(engine, d.unknown(keys))
+    if getattr(engine, "_keys_presynced", False):   # the agreement round numbered them already
+        _sync_new_keys(engine, [])
+        ids_np = d.id_array(keys)
+    else:                                           # ONE lookup pass finds the ids and the misses
+        ids_np = d.lookup(keys)
+        miss = np.flatnonzero(ids_np < 0)
+        mk = [keys[i] for i in miss]
+        _sync_new_keys(engine, list(dict.fromkeys(mk)))
+        if mk:
+            ids_np[miss] = d.id_array(mk)
     vals = list(mapData.values())
     dev = vals[0].device if vals else engine.device
     if vals:
@@ -445,7 +461,7 @@ def _map_tensors(engine, mapData: Dict):
     else:
         v = torch.empty((0, 1), device=dev)
         shape = (1,)
-    ids = torch.from_numpy(d.id_array(keys)).to(dev, non_blocking=False)
+    ids = torch.from_numpy(ids_np).to(dev, non_blocking=False)
     return ids, v, shape
 
 
