@@ -59,3 +59,35 @@ def test_tensor_map_is_a_dict_view():
     assert len(m) == 4 and torch.equal(m["a"], torch.ones(2, 2))
     del m["z"]
     assert len(m) == 3 and not m.pristine()
+
+
+def test_rows_of_one_base_detection():
+    """The dict->rows fast path (sparse._rows_of_one_base) accepts only whole rows of one
+    contiguous base; everything else goes through torch.stack."""
+    import random
+
+    import torch
+    from mp4x.parallel.sparse import _rows_of_one_base
+    base = torch.randn(3000, 16)
+    vals = list(base.unbind(0))
+    perm = list(range(3000))
+    random.Random(0).shuffle(perm)
+    sub = [vals[i] for i in perm[:2000]]
+    idx = _rows_of_one_base(sub)
+    assert idx is not None and torch.equal(base.index_select(0, idx), torch.stack(sub))
+    sq = torch.randn(64, 64)
+    assert _rows_of_one_base([sq[:, i] for i in range(64)]) is None          # columns
+    assert _rows_of_one_base([sq[i, :32] for i in range(64)]) is None        # half rows
+    assert _rows_of_one_base(vals[:10] + list(torch.randn(4, 16).unbind(0))) is None   # two bases
+    t = torch.randn(500, 8)
+    rows = list(t[100:400].unbind(0))                                         # rows of a slice
+    assert torch.equal(t.index_select(0, _rows_of_one_base(rows)), torch.stack(rows))
+    t3 = torch.randn(50, 4, 8)
+    idx3 = _rows_of_one_base(list(t3.unbind(0)))                              # [4, 8] slabs
+    assert torch.equal(idx3, torch.arange(50))
+
+
+def test_lookup_marks_unseen_keys():
+    d = KeyDictionary()
+    d.learn_round([["a", "b"]])
+    assert d.lookup(["b", "x", "a", "x"]).tolist() == [1, -1, 0, -1]
