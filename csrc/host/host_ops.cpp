@@ -19,6 +19,7 @@
 #include <cstdint>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <type_traits>
 #include <vector>
@@ -39,8 +40,65 @@
 
 namespace {
 
-// Fork-safe fan-out (no OpenMP runtime state survives a fork in the rank launchers, and
-// torch ships its own libgomp): split [0, nb) over nt threads, the caller runs chunk 0.
+long futex_word(std::atomic<uint32_t>* addr, int op, uint32_t val) {
+  return syscall(SYS_futex, reinterpret_cast<uint32_t*>(addr), op | FUTEX_PRIVATE_FLAG, val, nullptr, nullptr, 0);
+}
+
+// Persistent fan-out pool (no OpenMP: no runtime state must survive a fork in the rank launchers,
+// and torch ships its own libgomp).  A job splits [0, nb) over nt threads, the caller runs chunk
+// 0; the workers wait on a generation word (short spin, then a futex), so a job costs one wake,
+// not nt-1 thread creations (the shm engine runs 4 fan-outs per 16 MiB piece: spawning was ~1/3
+// of an 800 MB allreduce on the box).  Every worker acknowledges every job (those past nt just
+// count), so the caller's wait covers them all and no late count leaks into the next job; workers
+// are only added under the job lock, between jobs.  One job at a time: a concurrent caller, or a
+// forked child (whose copy of the pool has no threads), falls back to spawning.
+struct Pool {
+  std::mutex job;
+  std::atomic<uint32_t> gen{0};
+  std::atomic<uint32_t> done{0};
+  std::atomic<uint32_t> sleepers{0};
+  int nworkers = 0;                         // detached worker threads 1..nworkers (job lock)
+  int nt = 0;                               // threads in the current job (incl. the caller)
+  int64_t nb = 0;
+  void (*fn)(void*, int64_t) = nullptr;
+  void* ctx = nullptr;
+  pid_t pid = 0;
+
+  void run_range(int t) const {
+    const int64_t lo = nb * t / nt, hi = nb * (t + 1) / nt;
+    for (int64_t b = lo; b < hi; ++b) fn(ctx, b);
+  }
+
+  void worker(int t, uint32_t seen) {
+    for (;;) {
+      for (int i = 0; gen.load(std::memory_order_acquire) == seen; ++i) {
+        if (i < 4096) {
+          __builtin_ia32_pause();
+          continue;
+        }
+        sleepers.fetch_add(1, std::memory_order_seq_cst);
+        if (gen.load(std::memory_order_seq_cst) == seen) futex_word(&gen, FUTEX_WAIT, seen);
+        sleepers.fetch_sub(1, std::memory_order_seq_cst);
+      }
+      ++seen;                               // exactly one job per generation (the caller waits)
+      if (t < nt) run_range(t);
+      done.fetch_add(1, std::memory_order_acq_rel);
+    }
+  }
+};
+
+Pool* g_pool = nullptr;
+std::mutex g_pool_mu;
+
+Pool* the_pool() {
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  if (!g_pool || g_pool->pid != getpid()) {   // first use, or a forked child: a fresh pool (leak the old)
+    g_pool = new Pool();
+    g_pool->pid = getpid();
+  }
+  return g_pool;
+}
+
 template <typename F>
 void parallel_for(int64_t nb, int nt, F&& body) {
   if (nt <= 1 || nb <= 1) {
@@ -48,15 +106,39 @@ void parallel_for(int64_t nb, int nt, F&& body) {
     return;
   }
   if (nt > nb) nt = (int)nb;
-  std::vector<std::thread> th;
-  th.reserve(nt - 1);
-  auto run = [&](int t) {
-    const int64_t lo = nb * t / nt, hi = nb * (t + 1) / nt;
-    for (int64_t b = lo; b < hi; ++b) body(b);
-  };
-  for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
-  run(0);
-  for (auto& x : th) x.join();
+  Pool* p = the_pool();
+  std::unique_lock<std::mutex> job(p->job, std::try_to_lock);
+  if (!job.owns_lock()) {                      // pool busy: spawn for this job
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    auto run = [&](int t) {
+      const int64_t lo = nb * t / nt, hi = nb * (t + 1) / nt;
+      for (int64_t b = lo; b < hi; ++b) body(b);
+    };
+    for (int t = 1; t < nt; ++t) th.emplace_back(run, t);
+    run(0);
+    for (auto& x : th) x.join();
+    return;
+  }
+  const uint32_t g = p->gen.load(std::memory_order_relaxed);
+  while (p->nworkers < nt - 1) {               // grow between jobs: new workers wait for g + 1
+    const int t = ++p->nworkers;
+    std::thread([p, t, g] { p->worker(t, g); }).detach();
+  }
+  using B = typename std::remove_reference<F>::type;
+  p->fn = [](void* c, int64_t b) { (*static_cast<B*>(c))(b); };
+  p->ctx = const_cast<void*>(static_cast<const void*>(&body));
+  p->nb = nb;
+  p->nt = nt;
+  p->done.store(0, std::memory_order_relaxed);
+  p->gen.store(g + 1, std::memory_order_seq_cst);
+  if (p->sleepers.load(std::memory_order_seq_cst)) futex_word(&p->gen, FUTEX_WAKE, INT_MAX);
+  p->run_range(0);
+  const uint32_t all = (uint32_t)p->nworkers;
+  for (int i = 0; p->done.load(std::memory_order_acquire) != all; ++i) {
+    if (i < 65536) __builtin_ia32_pause();
+    else sched_yield();                        // a worker descheduled by the cpu quota
+  }
 }
 
 template <typename T> struct Uns { using U = T; };

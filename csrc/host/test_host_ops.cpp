@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "mp4x/ops.h"
@@ -78,6 +79,23 @@ static void run_rank(void* base, int rank, int p, int64_t slot, int64_t n) {
   mp4x_shm_detach(h);
 }
 
+// sum of two int64 inputs over n elements through mp4x_host_reduce with nt threads, `reps` times
+static void pool_check(int64_t n, int nt, int reps) {
+  const int rank = -1;                               // (CHECK's report)
+  std::vector<int64_t> x(n), y(n), z(n);
+  for (int64_t i = 0; i < n; ++i) {
+    x[i] = i;
+    y[i] = 3 * i + 1;
+  }
+  const void* ins[2] = {x.data(), y.data()};
+  for (int r = 0; r < reps; ++r) {
+    const int w = 1 + (nt + r) % (nt + 2);           // widths 1..nt+2
+    CHECK(mp4x_host_reduce(MP4X_I64, MP4X_SUM, z.data(), ins, 2, n, w) == 0, "pool reduce");
+    for (int64_t i = 0; i < n; i += 997) CHECK(z[i] == 4 * i + 1, "pool reduce value at %lld", (long long)i);
+    CHECK(z[n - 1] == 4 * (n - 1) + 1, "pool reduce tail");
+  }
+}
+
 int main(int argc, char** argv) {
   const int p = argc > 1 ? atoi(argv[1]) : 4;
   const int64_t n = argc > 2 ? atoll(argv[2]) : 100003;
@@ -96,6 +114,15 @@ int main(int argc, char** argv) {
       CHECK(mp4x_host_reduce(MP4X_I64, op, z.data(), ins, 2, 1000, 4) == 0, "reduce op %d", op);
     CHECK(mp4x_host_reduce(MP4X_F32, MP4X_BXOR, z.data(), ins, 2, 10, 1) == MP4X_E_UNSUPPORTED, "float xor");
   }
+  // the persistent fan-out pool: many jobs back to back, varying widths, two concurrent callers
+  // (one gets the pool, the other the spawn fallback); the forked ranks below then get a fresh
+  // pool of their own (the parent's workers do not exist in a child)
+  pool_check(1 << 20, 4, 50);
+  {
+    std::thread a([] { pool_check((1 << 20) + 7, 5, 40); });
+    pool_check((1 << 19) + 3, 3, 40);
+    a.join();
+  }
   size_t bytes = 4096 + (size_t)p * slot;
   void* base = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
   if (base == MAP_FAILED) return 2;
@@ -104,6 +131,7 @@ int main(int argc, char** argv) {
   for (int r = 0; r < p; ++r) {
     pid_t pid = fork();
     if (pid == 0) {
+      pool_check(1 << 18, 3, 5);                   // pool after fork: a fresh one in the child
       run_rank(base, r, p, slot, n);
       _exit(0);
     }

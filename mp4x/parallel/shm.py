@@ -25,6 +25,7 @@ import numpy as np
 from ..exceptions import TransportError
 from ..ops import native
 from ..ops.native import check as _native_check
+from ..utils.cpus import usable_cpus
 
 _BARRIER_ERRORS = {-1: "barrier timed out (MP4X_SHM_TIMEOUT)", -2: "barrier aborted by a peer",
                    -3: "a peer process exited (connection closed)"}
@@ -66,7 +67,7 @@ class ShmEngine:
         if self.rank == 0:
             self.shm.unlink()                      # mapping stays valid; no leak on crash
         self._base = ctypes.c_char.from_buffer(self.shm.buf)
-        nt = int(threads or int(os.environ.get("MP4X_HOST_THREADS", 0)) or max(1, (os.cpu_count() or 2) // self.p))
+        nt = int(threads or int(os.environ.get("MP4X_HOST_THREADS", 0)) or max(1, usable_cpus() // self.p))
         timeout = float(os.environ.get("MP4X_SHM_TIMEOUT", 300.0))
         self.h = self.lib.mp4x_shm_attach(ctypes.addressof(self._base), self.rank, self.p, self.slot, nt, timeout)
         # every rank published its pid: from now on a barrier wait notices a peer process that

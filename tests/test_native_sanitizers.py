@@ -26,7 +26,13 @@ def _build(name, flags):
            "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        pytest.skip("sanitizer toolchain unavailable: " + r.stderr[-500:])
+        # skip only when the toolchain cannot build ANY sanitized program; a compile error in
+        # the sources is a failure
+        probe = subprocess.run(["g++", "-x", "c++", "-", "-o", os.devnull] + flags, input="int main(){}",
+                               capture_output=True, text=True)
+        if probe.returncode != 0:
+            pytest.skip("sanitizer toolchain unavailable: " + probe.stderr[-500:])
+        pytest.fail("host runtime does not build with " + " ".join(flags) + ":\n" + r.stderr[-3000:])
     return out
 
 
