@@ -114,7 +114,7 @@ static int dr_dt(void* out, const uint8_t* const* qs, const float* const* ss, in
 // zero suppression, the case where it pays on accelerator data (sparse / masked gradients,
 // histograms).  Per 256-element block:
 //   masks  4 x uint64 (ballot of "word != 0", one per 64-lane slice)
-//   counts int32 non-zero words  ->  exclusive scan (hipCUB) -> offsets
+//   counts int32 non-zero words  ->  exclusive scan (rocPRIM) -> offsets
 //   vals   the non-zero words, compacted in order
 // "Zero" means all bits zero, so -0.0, NaN payloads and every integer pattern round-trip
 // exactly.  Blocks never straddle chunks: a chunk table (elem_start, elem_len, blk_start)
@@ -531,7 +531,7 @@ static int zs_encode_t(const void* in, const int64_t* table, int nchunk, int64_t
   return (int)hipGetLastError();
 }
 
-// The three-kernel form (mask pass, hipCUB scan, compaction): the default (see zs_twopass) and
+// The three-kernel form (mask pass, rocPRIM scan, compaction): the default (see zs_twopass) and
 // the reference the single-pass kernel is tested against.
 template <typename W>
 static int zs_encode_twopass_t(const void* in, const int64_t* table, int nchunk, int64_t nblk, uint64_t* masks,

@@ -6,7 +6,7 @@
 // keys travel as 64-bit ids (host dictionary) and a map is a (keys[n], vals[n, dim]) pair:
 //
 //   K4  owner + histogram:  dest = id % p, per-block LDS histogram, one atomic per bucket;
-//       the stable radix sort by dest (hipCUB) then gives the all-to-all send layout.
+//       the stable radix sort by dest (rocPRIM) then gives the all-to-all send layout.
 //   K5  reduce-by-key:      stable radix sort by id (rank order preserved inside a key),
 //       head flags + DeviceSelect give run starts, then one wave per run reduces its rows
 //       (lanes over `dim`) in run order => deterministic, no float atomics.

@@ -11,7 +11,7 @@ Device design (one process per GPU):
   / histogram sync moves no strings at all, and the id sort runs over ``bits`` bits only;
 * values live in one ``[n, dim]`` device tensor (``Map<String, float[]>`` rows);
 * owner of a key = ``(uint64)id % p``; kernel K4b partitions keys AND rows by owner in one
-  fused LDS-multisplit pass (stable, deterministic; the hipCUB radix-sort K4 path remains
+  fused LDS-multisplit pass (stable, deterministic; the rocPRIM radix-sort K4 path remains
   as the fallback) and they are exchanged with ONE ragged all-to-all over RCCL (every link
   busy at once, no ring);
 * each owner reduces its rows with the deterministic reduce-by-key kernel K5 (stable sort
