@@ -34,10 +34,49 @@ from ..utils.scatter_allocate import plan as scatter_plan
 from . import wire
 
 
+_NATIVE_REDUCE_MIN = 1 << 20
+_NATIVE_DT = {np.dtype(np.float64): 0, np.dtype(np.float32): 1, np.dtype(np.int64): 2, np.dtype(np.int32): 3,
+              np.dtype(np.int16): 4, np.dtype(np.int8): 5}   # enum mp4x_dtype
+_native_lib = None
+
+
+def _native_reduce(seg: np.ndarray, data, op) -> bool:
+    """seg op= data through the host runtime's multi-threaded reduce (csrc/host/host_ops.cpp,
+    the persistent fan-out pool): numpy's ufuncs run on one core, which made the reduce-on-
+    receive the slowest stage of a large TCP allreduce.  Same element order and IEEE results as
+    the numpy path; False when the operands do not qualify (custom operator, dtype, layout)."""
+    global _native_lib
+    if getattr(op, "is_custom", False) or getattr(op, "code", None) is None:
+        return False
+    dt = _NATIVE_DT.get(seg.dtype)
+    if dt is None or int(op.dtype) != dt or not isinstance(data, np.ndarray) or data.dtype != seg.dtype:
+        return False
+    if not (seg.flags.c_contiguous and data.flags.c_contiguous) or data.size != seg.size:
+        return False
+    a, b = seg.ctypes.data, data.ctypes.data
+    if a % seg.itemsize or b % seg.itemsize:          # frames land at any byte offset
+        return False
+    if _native_lib is None:
+        try:
+            from ..ops import native
+            _native_lib = native.host()
+        except Exception:      # noqa: BLE001 — not built: numpy path
+            _native_lib = False
+    if not _native_lib:
+        return False
+    from ..ops.native import ptr_array
+    from ..utils.cpus import usable_cpus
+    pp, keep = ptr_array([a, b])
+    return _native_lib.mp4x_host_reduce(dt, int(op.code), a, pp, 2, seg.size, min(8, usable_cpus())) == 0
+
+
 def _reduce_segment(arr, f: int, t: int, data, op) -> None:
     if isinstance(arr, np.ndarray):
+        seg = arr[f:t]
+        if seg.nbytes >= _NATIVE_REDUCE_MIN and _native_reduce(seg, data, op):
+            return
         with np.errstate(over="ignore", invalid="ignore"):
-            op.reduce_into(arr[f:t], data)
+            op.reduce_into(seg, data)
     else:
         for i in range(t - f):
             arr[f + i] = op.apply(arr[f + i], data[i])
