@@ -157,11 +157,18 @@ def main():
     if p > 1 and not args.cpu and not args.no_tier_sweep and not (args.algo or args.codec):
         tiers = {}
         for nb in (4 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+            failed = 0.0
             try:
                 res = comm.device.autotune_allreduce(torch.empty(nb // 4, device=dev), op, iters=3)
                 tiers[str(nb)] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in res.items()}
             except Exception as e:   # noqa: BLE001 — evidence only; the headline is already measured
                 tiers[str(nb)] = {"error": str(e)[:200]}
+                failed = 1.0
+            # every rank stops together (a rank-local failure must not leave the others waiting
+            # in the next size's collectives)
+            flag = torch.tensor([failed], dtype=torch.float64, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if flag.item() > 0:
                 break
 
     ms_per_step = wall * 1e3 / args.steps
