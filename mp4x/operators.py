@@ -95,13 +95,19 @@ def dtype_of_numpy(dt) -> DType:
     return _DTYPE_BY_NP[np.dtype(dt)]
 
 
+_TORCH_DT = None
+
+
 def dtype_of_torch(t) -> DType:
-    import torch
-    return {
-        torch.float64: DType.F64, torch.float32: DType.F32, torch.int64: DType.I64,
-        torch.int32: DType.I32, torch.int16: DType.I16, torch.int8: DType.I8,
-        torch.bfloat16: DType.BF16, torch.float16: DType.F16, torch.uint8: DType.U8,
-    }[t]
+    global _TORCH_DT
+    if _TORCH_DT is None:    # built once: this is on every device collective's path
+        import torch
+        _TORCH_DT = {
+            torch.float64: DType.F64, torch.float32: DType.F32, torch.int64: DType.I64,
+            torch.int32: DType.I32, torch.int16: DType.I16, torch.int8: DType.I8,
+            torch.bfloat16: DType.BF16, torch.float16: DType.F16, torch.uint8: DType.U8,
+        }
+    return _TORCH_DT[t]
 
 
 def torch_dtype_of(dt: DType):

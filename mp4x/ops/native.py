@@ -175,6 +175,18 @@ def ptr_array(ptrs: Sequence[int]):
 
 
 _current_raw_stream = None
+_capturing_fn = None
+
+
+def capturing_now() -> bool:
+    """``torch.cuda.is_current_stream_capturing()`` without its Python wrapper (on every device
+    collective's path)."""
+    global _capturing_fn
+    if _capturing_fn is None:
+        import torch
+        _capturing_fn = getattr(torch._C, "_cuda_isCurrentStreamCapturing", None) or \
+            torch.cuda.is_current_stream_capturing
+    return bool(_capturing_fn())
 
 
 def stream_ptr(stream=None) -> int:

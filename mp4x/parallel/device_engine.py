@@ -36,6 +36,7 @@ import torch.distributed as dist
 
 from ..exceptions import Mp4jException
 from ..operators import DType, OpCode, Operator, dtype_of_torch, for_dtype
+from ..ops.native import capturing_now
 from ..utils.commutils import CommUtils
 
 LOG = logging.getLogger("mp4x.device")
@@ -568,14 +569,15 @@ class DeviceEngine:
         if view.numel() == 0:
             return arr
         op = self._op(operator, view)
-        algo = self.select("allreduce", view.numel() * view.element_size(), op, view.dtype, operand)
-        if algo not in self._CAPTURABLE and view.is_cuda and torch.cuda.is_current_stream_capturing():
+        nbytes = view.numel() * view.element_size()
+        algo = self.select("allreduce", nbytes, op, view.dtype, operand)
+        capturing = view.is_cuda and capturing_now()
+        if algo not in self._CAPTURABLE and capturing:
             # host-synchronising schedule inside a hipGraph capture: use a capturable twin
             algo = "ipc2" if algo == "ipc2p" else ("rccl" if self.rccl_ok(op, view.dtype) else "a2a")
         if out is not None:
-            if algo in ("ipc1", "ipc2") and self.ipc() is not None and \
-                    view.numel() * view.element_size() <= self.ipc_twoshot_max and \
-                    (not torch.cuda.is_current_stream_capturing() or self._ipc_obj._epoch_dev is not None):
+            if algo in ("ipc1", "ipc2") and self.ipc() is not None and nbytes <= self.ipc_twoshot_max and \
+                    (not capturing or self._ipc_obj._epoch_dev is not None):
                 from .ipc import ONESHOT, TWOSHOT
                 self._count("allreduce." + algo + ".out")
                 self._ipc_obj.allreduce(view, op, algo=ONESHOT if algo == "ipc1" else TWOSHOT, out=oview,

@@ -23,7 +23,7 @@ import torch
 from ..exceptions import Mp4jException
 from ..operators import OpCode, dtype_of_torch
 from ..ops import native
-from ..ops.native import check, ptr_array, stream_ptr, c_int, c_int64, c_void_p, c_size_t, PP
+from ..ops.native import check, capturing_now, ptr_array, stream_ptr, c_int, c_int64, c_void_p, c_size_t, PP
 
 native.register_signatures({
     "mp4x_ipc_signal_bytes": (c_size_t, []),
@@ -101,6 +101,7 @@ class IpcAllreduce:
         self._data = c_void_p()
         self._sig = c_void_p()
         self._herr = c_void_p()          # pinned host error word (CPU address)
+        self._herr_word = None           # its ctypes view, made once (read on every call)
         self._opened: List[c_void_p] = []
         # Every local step that can fail runs before the first collective inside a try, and its
         # error travels in that collective: a rank that fails alone must not leave its peers
@@ -199,9 +200,12 @@ class IpcAllreduce:
     def host_error(self) -> int:
         """The host-visible barrier-timeout word (0 = fine; 1/2/3 = a start/mid/end barrier of an
         earlier kernel timed out), read from pinned memory: no device synchronisation."""
-        if not self._herr:
-            return 0
-        return int(ctypes.c_uint32.from_address(self._herr.value).value)
+        w = self._herr_word
+        if w is None:
+            if not self._herr:
+                return 0
+            w = self._herr_word = ctypes.c_uint32.from_address(self._herr.value)
+        return w.value
 
     def raise_if_failed(self) -> None:
         """Fail the call instead of corrupting it: if an earlier IPC kernel of this instance gave
@@ -251,32 +255,33 @@ class IpcAllreduce:
         if not blocks and self.max_blocks:
             vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
             blocks = max(1, min(self.max_blocks, -(-min(total, self.nbytes) // 16 // vec_per_block)))
-        src = view.view(torch.uint8)
-        dst = out.view(torch.uint8)
         if overlap is None:
             overlap = self._overlap_default
-        if total > self.nbytes and overlap and not torch.cuda.is_current_stream_capturing():
-            return self._allreduce_pipelined(src, dst, total, dt, op, algo, blocks, out, scale)
+        capturing = capturing_now()
+        if total > self.nbytes and overlap and not capturing:
+            return self._allreduce_pipelined(view.view(torch.uint8), out.view(torch.uint8), total, dt, op, algo,
+                                             blocks, out, scale)
         piece = self.nbytes - self.nbytes % 16
         off = 0
         st = stream_ptr()
         # once prepare_graph() ran, EVERY call (eager or captured) takes its epoch from the device
         # counter, so eager calls and graph replays can interleave without reusing an epoch
-        if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
+        if capturing and self._epoch_dev is None:
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
-        fused = src.data_ptr() % 16 == 0 and self._fuse_copy   # copy-in inside the kernel: one launch
+        sp, dp = view.data_ptr(), out.data_ptr()
+        fused = sp % 16 == 0 and self._fuse_copy   # copy-in inside the kernel: one launch
         while off < total:
             m = min(piece, total - off)
             if not fused:
-                check(self.lib.mp4x_memcpy_async(self._data.value, src.data_ptr() + off, m, st), "ipc input copy")
+                check(self.lib.mp4x_memcpy_async(self._data.value, sp + off, m, st), "ipc input copy")
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
             check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
-                                                 self.rank, self.p, m, src.data_ptr() + off if fused else None,
-                                                 dst.data_ptr() + off, self.epoch, blocks, edev, scale, st),
+                                                 self.rank, self.p, m, sp + off if fused else None,
+                                                 dp + off, self.epoch, blocks, edev, scale, st),
                   "mp4x_ipc_allreduce")
             off += m
         return out
@@ -1106,6 +1111,7 @@ class IpcAllreduce:
             self.lib.mp4x_ipc_free(self._sig)
             self._sig = c_void_p()
         if self._herr:
+            self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
         for ptr in getattr(self, "_scratch_allocs", []):
