@@ -155,6 +155,41 @@ def team_ext():
     return _team_ext or None
 
 
+def _load_ext(name: str):
+    import importlib.machinery
+    import importlib.util
+    for suf in importlib.machinery.EXTENSION_SUFFIXES:
+        path = os.path.join(NATIVE_DIR, name + suf)
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location(name, path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            return mod
+    raise NativeUnavailable(f"{name} is not built (python tools/build_native.py)")
+
+
+_map_ext = None
+
+
+def map_ext():
+    """The native Dict[key, Tensor] -> ids / rows pass (``_mp4x_map``, csrc/pyext/map_ext.cpp),
+    or None when it is not built or ``MP4X_MAP_EXT=0`` (the map collectives then take the
+    Python form of the same pass)."""
+    global _map_ext
+    if _map_ext is None:
+        with _lock:
+            if _map_ext is None:
+                mod = False
+                if os.environ.get("MP4X_MAP_EXT", "1") != "0":
+                    try:
+                        import torch  # noqa: F401 — libtorch_python must be loaded first
+                        mod = _load_ext("_mp4x_map")
+                    except Exception:   # noqa: BLE001
+                        mod = False
+                _map_ext = mod
+    return _map_ext or None
+
+
 def available() -> bool:
     try:
         hip()

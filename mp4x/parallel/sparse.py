@@ -460,6 +460,51 @@ def _stack_rows(vals: List[torch.Tensor]) -> torch.Tensor:
     return v.view(len(vals), -1)
 
 
+def _pack_native(d: "KeyDictionary", mapData):
+    """The native one-walk form of :func:`_map_tensors`'s lookup + row checks
+    (csrc/pyext/map_ext.cpp): ``(ids, n_missing, rows or None, base)``, or None when the
+    extension is not built or the map is not a plain non-empty dict of tensors."""
+    if type(mapData) is not dict or not mapData:
+        return None
+    from ..ops import native
+    ext = native.map_ext()
+    if ext is None:
+        return None
+    first = next(iter(mapData.values()))
+    if not isinstance(first, torch.Tensor):
+        return None
+    b = first._base
+    base = b if b is not None and b.is_contiguous() else None
+    n = len(mapData)
+    ids = np.empty(n, dtype=np.int64)
+    rows = np.empty(n, dtype=np.int64)
+    nmiss, rows_ok = ext.pack(mapData, d.key2id, base, ids, rows)
+    return ids, int(nmiss), rows if rows_ok else None, base
+
+
+def _map_tensors_packed(engine, d: "KeyDictionary", mapData: Dict, ids_np, nmiss, rows, base):
+    """:func:`_map_tensors` after the native walk: misses numbered in one sync round, values
+    gathered as rows of their base tensor with ONE index_select (CPU or GPU) when every value is
+    a whole row of it (``base`` viewed as [-1, value numel]), else one stack."""
+    if getattr(engine, "_keys_presynced", False) or not nmiss:
+        _sync_new_keys(engine, [])
+        if nmiss:                                   # presynced but a key has no id: a caller bug
+            raise KeyError(list(mapData.keys())[int(np.flatnonzero(ids_np < 0)[0])])
+    else:
+        keys = list(mapData.keys())
+        miss = np.flatnonzero(ids_np < 0)
+        mk = [keys[i] for i in miss]
+        _sync_new_keys(engine, list(dict.fromkeys(mk)))
+        ids_np[miss] = d.id_array(mk)
+    first = next(iter(mapData.values()))
+    shape = tuple(first.shape)
+    if rows is not None:
+        v = base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(base.device))
+    else:
+        v = _stack_rows(list(mapData.values()))
+    return torch.from_numpy(ids_np).to(v.device), v, shape
+
+
 def _map_tensors(engine, mapData: Dict):
     """Dict[str, Tensor] -> (ids int64[n], rows [n, numel], value shape); syncs new keys.
     Vectorised: ids through one ``np.fromiter`` + one host->device copy, values through one
@@ -469,6 +514,9 @@ def _map_tensors(engine, mapData: Dict):
         _sync_new_keys(engine, [])          # every key is numbered already (collective round)
         rows = mapData._rows.view(len(mapData._ids), -1)
         return torch.from_numpy(mapData._ids).to(rows.device), rows, mapData._shape
+    packed = _pack_native(d, mapData)
+    if packed is not None:
+        return _map_tensors_packed(engine, d, mapData, *packed)
     keys = list(mapData.keys())
     if getattr(engine, "_keys_presynced", False):   # the agreement round numbered them already
         _sync_new_keys(engine, [])
@@ -533,9 +581,21 @@ def _maps_by_dest(engine, maps: List[Dict]):
     dictionary sync for all of them."""
     d = _dictionary(engine)
     _sync_new_keys(engine, d.unknown(k for m in maps for k in m.keys()))
-    id_lists = [d.id_array(list(m.keys())) for m in maps]
     ks, vs, counts, shape = [], [], [], None
-    for m, ids in zip(maps, id_lists):
+    for m in maps:
+        packed = _pack_native(d, m)
+        if packed is not None:                      # native walk: ids + rows of one base
+            ids, _, rows, base = packed
+            first = next(iter(m.values()))
+            shape = tuple(first.shape)
+            dev = first.device
+            v = (base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(dev))
+                 if rows is not None else _stack_rows(list(m.values())))
+            ks.append(torch.from_numpy(ids).to(dev))
+            vs.append(v)
+            counts.append(len(ids))
+            continue
+        ids = d.id_array(list(m.keys()))
         vals = list(m.values())
         dev = vals[0].device if vals else engine.device
         if vals:

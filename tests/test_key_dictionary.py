@@ -91,3 +91,54 @@ def test_lookup_marks_unseen_keys():
     d = KeyDictionary()
     d.learn_round([["a", "b"]])
     assert d.lookup(["b", "x", "a", "x"]).tolist() == [1, -1, 0, -1]
+
+
+def _python_form(d, m):
+    """What the Python path computes: ids (-1 when unknown) and the stacked rows."""
+    import numpy as np
+    import torch
+    ids = d.lookup(list(m.keys()))
+    rows = torch.stack([v.reshape(-1) for v in m.values()])
+    return ids, rows
+
+
+def test_native_map_pack_matches_the_python_form():
+    """csrc/pyext/map_ext.cpp: one dict walk gives the same ids as ``KeyDictionary.lookup`` and
+    rows only when EVERY value is a whole contiguous row of the first value's base tensor of the
+    same dtype; anything else falls back to one stack with identical values."""
+    import numpy as np
+    import pytest
+    import torch
+    from mp4x.ops import native
+    from mp4x.parallel import sparse
+
+    if native.map_ext() is None:
+        pytest.skip("_mp4x_map not built")
+    base = torch.arange(40 * 6, dtype=torch.float32).view(40, 6)
+    d = KeyDictionary()
+    d.learn_round([[f"k{i}" for i in range(0, 40, 2)]])
+    cases = {
+        "rows in order": {f"k{i}": base[i] for i in range(40)},
+        "rows shuffled": {f"k{i}": base[i] for i in (5, 3, 39, 0, 17)},
+        "foreign value": {**{f"k{i}": base[i] for i in range(4)}, "x": torch.zeros(6)},
+        "other dtype view": {"k0": base[0], "k1": base[1].view(torch.int32)},
+        "partial rows": {"k0": base[0, :3], "k2": base[2, 3:]},     # rows of base as [80, 3]
+        "misaligned": {"k0": base[0, :3], "k2": base[2, 1:4]},
+        "strided row": {"k0": base[:, 0], "k2": base[:, 1]},
+        "2-D values": {f"k{i}": base.view(20, 2, 6)[i] for i in range(20)},
+    }
+    expect_rows = {"rows in order": True, "rows shuffled": True, "2-D values": True, "partial rows": True}
+    for name, m in cases.items():
+        ids, nmiss, rows, b = sparse._pack_native(d, m)
+        ref_ids, ref_rows = _python_form(d, m)
+        assert np.array_equal(ids, ref_ids), name
+        assert nmiss == int((ref_ids < 0).sum()), name
+        assert (rows is not None) == expect_rows.get(name, False), name
+        if rows is not None:
+            got = b.reshape(-1, ref_rows.shape[1]).index_select(0, torch.from_numpy(rows))
+            assert torch.equal(got, ref_rows), name
+    # non-dict mappings and empty maps take the Python path
+    from collections import OrderedDict
+    assert sparse._pack_native(d, OrderedDict(k0=base[0])) is None
+    assert sparse._pack_native(d, {}) is None
+    assert sparse._pack_native(d, {"k0": [1.0, 2.0]}) is None

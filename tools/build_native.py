@@ -148,6 +148,27 @@ def build_pyext(host_so):
     return out
 
 
+def build_mapext():
+    """``_mp4x_map``: CPython extension reading ``at::Tensor`` facts directly (libtorch headers,
+    linked against the torch libraries PyTorch itself loads; rpath to torch/lib)."""
+    import sysconfig
+    src = os.path.join(CSRC, "pyext", "map_ext.cpp")
+    tl = torch_lib_dir()
+    if not os.path.exists(src) or tl is None:
+        return None
+    import torch
+    tinc = os.path.join(os.path.dirname(tl), "include")
+    out = os.path.join(OUT, "_mp4x_map" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if newer(src, out, []):
+        abi = int(bool(torch._C._GLIBCXX_USE_CXX11_ABI))
+        run(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-shared", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+             "-I", sysconfig.get_paths()["include"], "-isystem", tinc,
+             "-isystem", os.path.join(tinc, "torch", "csrc", "api", "include"),
+             src, "-o", out, "-L", tl, "-ltorch_python", "-ltorch", "-ltorch_cpu", "-lc10", "-Wl,-rpath," + tl])
+        print("  g++  ", os.path.relpath(src, ROOT), "->", os.path.relpath(out, ROOT))
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
@@ -165,6 +186,7 @@ def main(argv=None):
         return 0
     build_hip(a.j)
     build_pyext(build_host(a.j))
+    build_mapext()
     return 0
 
 
