@@ -68,7 +68,7 @@ PyObject* pack(PyObject*, PyObject* const* a, Py_ssize_t na) {
   bool rows_ok = false;
   const c10::StorageImpl* storage = nullptr;
   int64_t base_off = 0, d = 0, nrows = 0;
-  c10::ScalarType dtype = c10::ScalarType::Undefined;
+  caffe2::TypeMeta dtype;
   if (a[2] != Py_None) {
     if (!THPVariable_Check(a[2])) {
       PyErr_SetString(PyExc_TypeError, "pack: base must be a tensor or None");
@@ -85,7 +85,7 @@ PyObject* pack(PyObject*, PyObject* const* a, Py_ssize_t na) {
         storage = b.storage().unsafeGetStorageImpl();
         base_off = b.storage_offset();
         nrows = b.numel() / d;
-        dtype = b.scalar_type();
+        dtype = b.dtype();
         rows_ok = true;
       }
     }
@@ -110,10 +110,11 @@ PyObject* pack(PyObject*, PyObject* const* a, Py_ssize_t na) {
       if (!THPVariable_Check(v)) {
         rows_ok = false;
       } else {
-        const at::Tensor& t = THPVariable_Unpack(v);
-        const int64_t off = t.storage_offset() - base_off;
-        if (!t.defined() || !t.has_storage() || t.storage().unsafeGetStorageImpl() != storage ||
-            t.numel() != d || t.scalar_type() != dtype || !t.is_contiguous() || off < 0 || off % d != 0 || off / d >= nrows) {
+        // TensorImpl fields only: no Storage handle copy (two atomic refcount ops per value)
+        const c10::TensorImpl* t = THPVariable_Unpack(v).unsafeGetTensorImpl();
+        const int64_t off = t->storage_offset() - base_off;
+        if (!t->has_storage() || t->unsafe_storage().unsafeGetStorageImpl() != storage || t->numel() != d ||
+            t->dtype() != dtype || !t->is_contiguous() || off < 0 || off % d != 0 || off / d >= nrows) {
           rows_ok = false;
         } else {
           rows[i] = off / d;

@@ -321,7 +321,18 @@ class ProcessCommSlave:
         if mine == 1:
             from .sparse import TensorMap, _dictionary
             d = _dictionary(self.device)
-            if not (all_keys is None and isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d):
+            packed = None
+            if all_keys is None:
+                # the native walk finds the unseen keys AND the ids / rows the device op needs:
+                # one pass over the map instead of two (sparse._map_tensors takes it up)
+                from .sparse import _pack_native
+                packed = _pack_native(d, mapData)
+                self.device._prepacked = (mapData, packed) if packed is not None else None
+            if packed is not None:
+                if packed[1]:
+                    keys = list(mapData.keys())
+                    new = [keys[i] for i in np.flatnonzero(packed[0] < 0)]
+            elif not (all_keys is None and isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d):
                 new = d.unknown(list(mapData.keys()) if all_keys is None else list(all_keys))
         res = self.server.call("allgather_obj", self.rank, (mine, new))
         on_device = any(f == 1 for f, _ in res)

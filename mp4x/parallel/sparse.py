@@ -514,6 +514,15 @@ def _map_tensors(engine, mapData: Dict):
         _sync_new_keys(engine, [])          # every key is numbered already (collective round)
         rows = mapData._rows.view(len(mapData._ids), -1)
         return torch.from_numpy(mapData._ids).to(rows.device), rows, mapData._shape
+    pre = getattr(engine, "_prepacked", None)
+    engine._prepacked = None
+    if pre is not None and pre[0] is mapData and getattr(engine, "_keys_presynced", False):
+        ids, nmiss, rows, base = pre[1]           # walked by the agreement round (process_comm)
+        if nmiss:                                 # numbered by that round since
+            miss = np.flatnonzero(ids < 0)
+            keys = list(mapData.keys())
+            ids[miss] = d.id_array([keys[i] for i in miss])
+        return _map_tensors_packed(engine, d, mapData, ids, 0, rows, base)
     packed = _pack_native(d, mapData)
     if packed is not None:
         return _map_tensors_packed(engine, d, mapData, *packed)
