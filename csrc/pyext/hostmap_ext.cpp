@@ -1,0 +1,130 @@
+// mp4x._native._mp4x_hostmap — native passes of the HOST map collectives (values on the CPU:
+// Python scalars, numpy rows, objects).  Plain CPython API, no torch: a host-only job never pays
+// for importing libtorch.
+//
+// partition(map, p): the owner split every host ``*Map`` collective starts with
+// (ProcessCommSlave.allreduceMap / reduceMap / broadcastMap, J/comm/ProcessCommSlave.java:2053-2088,
+// 1490-1516, 842-883).  The Python rule hashes each key through ``str.encode('utf-16-be')`` and a
+// Python-level loop (~3.7 us per key); here it is one dict walk reading the str's PEP 393 buffer.
+// stack_rows(values, out): the value-row copy of the map codecs without np.stack's per-value checks.
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+
+#include <cstdint>
+#include <cstring>
+
+namespace {
+
+// java.lang.String.hashCode of a str: 31-polynomial over its UTF-16 code units, int32 wrap
+// (code points above U+FFFF count as their surrogate pair, as in Java).
+template <typename CH>
+uint32_t java_hash(const CH* s, Py_ssize_t n) {
+  uint32_t h = 0;
+  for (Py_ssize_t i = 0; i < n; ++i) {
+    const uint32_t c = s[i];
+    if (sizeof(CH) == 4 && c > 0xFFFF) {
+      const uint32_t u = c - 0x10000;
+      h = 31 * h + (0xD800 + (u >> 10));
+      h = 31 * h + (0xDC00 + (u & 0x3FF));
+    } else {
+      h = 31 * h + c;
+    }
+  }
+  return h;
+}
+
+// partition(map, p) -> [p dicts] | None
+// The host map collectives' owner rule ``key.hashCode() % p`` with Java's signed remainder and
+// negatives wrapped (mp4x/utils/hashing.py owner_of; reference ProcessCommSlave.java:2059-2072),
+// insertion order kept within each part.  None when a key is not a str (the Python rule decides).
+PyObject* partition(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 2 || !PyDict_Check(a[0])) {
+    PyErr_SetString(PyExc_TypeError, "partition(map: dict, p: int)");
+    return nullptr;
+  }
+  const long p = PyLong_AsLong(a[1]);
+  if (p <= 0) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "partition: p must be > 0");
+    return nullptr;
+  }
+  PyObject* map = a[0];
+  Py_ssize_t pos = 0;
+  PyObject *k, *v;
+  while (PyDict_Next(map, &pos, &k, &v))
+    if (!PyUnicode_CheckExact(k) || PyUnicode_READY(k) != 0) Py_RETURN_NONE;
+  PyObject* parts = PyList_New(p);
+  if (!parts) return nullptr;
+  for (long r = 0; r < p; ++r) {
+    PyObject* d = PyDict_New();
+    if (!d) {
+      Py_DECREF(parts);
+      return nullptr;
+    }
+    PyList_SET_ITEM(parts, r, d);
+  }
+  pos = 0;
+  while (PyDict_Next(map, &pos, &k, &v)) {
+    const Py_ssize_t n = PyUnicode_GET_LENGTH(k);
+    const void* data = PyUnicode_DATA(k);
+    uint32_t h;
+    switch (PyUnicode_KIND(k)) {
+      case PyUnicode_1BYTE_KIND: h = java_hash(static_cast<const Py_UCS1*>(data), n); break;
+      case PyUnicode_2BYTE_KIND: h = java_hash(static_cast<const Py_UCS2*>(data), n); break;
+      default: h = java_hash(static_cast<const Py_UCS4*>(data), n); break;
+    }
+    const int64_t hs = static_cast<int32_t>(h);
+    int64_t idx = (hs < 0 ? -hs : hs) % p;
+    if (hs < 0 && idx != 0) idx = p - idx;
+    if (PyDict_SetItem(PyList_GET_ITEM(parts, idx), k, v) != 0) {
+      Py_DECREF(parts);
+      return nullptr;
+    }
+  }
+  return parts;
+}
+
+// stack_rows(values: list, out) -> bool
+// np.stack for the map codecs (mp4x/parallel/wire.py): copy each value's bytes into row i of the
+// C-contiguous ``out`` through the buffer protocol.  False (nothing promised about ``out``) as
+// soon as a value is not a C-contiguous buffer of exactly one row with out's item format; the
+// caller then takes np.stack.  np.stack spends ~1.3 us per value on array checks and shape sets.
+PyObject* stack_rows(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 2 || !PyList_Check(a[0])) {
+    PyErr_SetString(PyExc_TypeError, "stack_rows(values: list, out)");
+    return nullptr;
+  }
+  Py_buffer ob;
+  if (PyObject_GetBuffer(a[1], &ob, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) return nullptr;
+  const Py_ssize_t n = PyList_GET_SIZE(a[0]);
+  bool ok = n > 0 && ob.len % n == 0 && ob.format != nullptr;
+  const Py_ssize_t row = ok ? ob.len / n : 0;
+  char* dst = static_cast<char*>(ob.buf);
+  for (Py_ssize_t i = 0; ok && i < n; ++i) {
+    Py_buffer vb;
+    if (PyObject_GetBuffer(PyList_GET_ITEM(a[0], i), &vb, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) != 0) {
+      PyErr_Clear();
+      ok = false;
+      break;
+    }
+    ok = vb.len == row && vb.itemsize == ob.itemsize && vb.format != nullptr && std::strcmp(vb.format, ob.format) == 0;
+    if (ok) std::memcpy(dst + i * row, vb.buf, row);
+    PyBuffer_Release(&vb);
+  }
+  PyBuffer_Release(&ob);
+  if (ok) Py_RETURN_TRUE;
+  Py_RETURN_FALSE;
+}
+
+PyMethodDef kMethods[] = {
+    {"partition", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(partition)), METH_FASTCALL,
+     "partition(map, p) -> [p dicts] by Java String.hashCode % p, or None for non-str keys"},
+    {"stack_rows", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(stack_rows)), METH_FASTCALL,
+     "stack_rows(values, out) -> bool: row i of out = bytes of values[i]"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_mp4x_hostmap", "native passes of the host map collectives", -1,
+                       kMethods};
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__mp4x_hostmap() { return PyModule_Create(&kModule); }

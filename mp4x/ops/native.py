@@ -190,6 +190,26 @@ def map_ext():
     return _map_ext or None
 
 
+_hostmap_ext = None
+
+
+def hostmap_ext():
+    """The native host-map passes (``_mp4x_hostmap``, csrc/pyext/hostmap_ext.cpp; no torch), or
+    None when not built or ``MP4X_MAP_EXT=0``."""
+    global _hostmap_ext
+    if _hostmap_ext is None:
+        with _lock:
+            if _hostmap_ext is None:
+                mod = False
+                if os.environ.get("MP4X_MAP_EXT", "1") != "0":
+                    try:
+                        mod = _load_ext("_mp4x_hostmap")
+                    except Exception:   # noqa: BLE001
+                        mod = False
+                _hostmap_ext = mod
+    return _hostmap_ext or None
+
+
 def available() -> bool:
     try:
         hip()

@@ -422,9 +422,7 @@ class ProcessCommSlave:
         p = self.slaveNum
         blocks = None
         if self.rank == rootRank:
-            blocks = [[{}] for _ in range(p)]
-            for k, v in mapData.items():
-                blocks[owner_of(k, p)][0][k] = v
+            blocks = [[d] for d in self._partition(mapData)]
         mine = self.engine.tree_scatter_maps(blocks, operand, rootRank)
         allb = self.engine.ring_allgather_maps(mine, operand)
         out: Dict = {}
@@ -539,7 +537,15 @@ class ProcessCommSlave:
         return operand.unbox(arr)
 
     def _partition(self, mapData: Dict) -> List[Dict]:
+        """p maps by the reference's owner rule ``key.hashCode() % p`` (utils/hashing.owner_of),
+        in ONE native walk for str keys (csrc/pyext/hostmap_ext.cpp ``partition``)."""
         p = self.slaveNum
+        if type(mapData) is dict and mapData:
+            from ..ops import native
+            ext = native.hostmap_ext()
+            parts = ext.partition(mapData, p) if ext is not None else None
+            if parts is not None:
+                return parts
         parts: List[Dict] = [{} for _ in range(p)]
         for k, v in mapData.items():
             parts[owner_of(k, p)][k] = v

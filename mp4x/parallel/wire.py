@@ -89,6 +89,35 @@ def unpack_segments(body, operand: Operand):
 VK_SCALAR, VK_VEC, VK_OBJ = 0, 1, 2
 
 
+def stack_rows(vals: List, dtype=None) -> np.ndarray:
+    """``np.stack(vals).astype(dtype, copy=False)`` for equal-shaped numpy rows — one native copy
+    per row (csrc/pyext/hostmap_ext.cpp ``stack_rows``) when they all share the dtype."""
+    v0 = vals[0]
+    dt = np.dtype(dtype) if dtype is not None else v0.dtype
+    if isinstance(vals, list) and isinstance(v0, np.ndarray) and v0.dtype == dt and v0.size:
+        from ..ops import native
+        ext = native.hostmap_ext()
+        if ext is not None:
+            out = np.empty((len(vals),) + v0.shape, dtype=dt)
+            if ext.stack_rows(vals, out):
+                return out
+    return np.stack(vals).astype(dt, copy=False)
+
+
+def _stack_like(vals: np.ndarray, rows: List):
+    """``rows`` stacked as a fresh [len(rows), dim] array of ``vals``' dtype, or None unless every
+    row is a 1-D-equivalent numpy row of exactly that dtype and size (the native copy checks each
+    row's buffer format and length in C; without the extension, the same checks in Python)."""
+    out = np.empty((len(rows),) + vals.shape[1:], dtype=vals.dtype)
+    from ..ops import native
+    ext = native.hostmap_ext()
+    if ext is not None:
+        return out if ext.stack_rows(rows, out) else None
+    if all(isinstance(r, np.ndarray) and r.dtype == vals.dtype and r.shape == vals.shape[1:] for r in rows):
+        return np.stack(rows)
+    return None
+
+
 def _encode_map(d: Dict, operand: Operand):
     keys = list(d.keys())
     kb = msgpack.packb(keys, use_bin_type=True)
@@ -96,8 +125,7 @@ def _encode_map(d: Dict, operand: Operand):
     if operand.is_primitive:
         if vals and isinstance(vals[0], np.ndarray):
             dim = int(vals[0].size)
-            vb = np.ascontiguousarray(np.stack(vals).astype(operand.np_dtype, copy=False)).tobytes() \
-                if vals else b""
+            vb = np.ascontiguousarray(stack_rows(vals, operand.np_dtype)).tobytes()
             return kb, vb, VK_VEC, dim
         vb = np.asarray(vals, dtype=operand.np_dtype).tobytes()
         return kb, vb, VK_SCALAR, 1
@@ -164,6 +192,22 @@ def merge_reduce(local: Dict, keys, vals, op) -> Dict:
                 if k not in local:
                     local[k] = v
         return local
+    if isinstance(vals, np.ndarray) and vals.ndim == 2 and not op.is_custom:
+        # vectorised over the shared keys: ONE stack of the local rows, ONE reduce, row views back
+        cur = list(map(local.get, keys))
+        shared_i = [i for i, c in enumerate(cur) if c is not None]
+        acc = _stack_like(vals, [cur[i] for i in shared_i]) if shared_i else vals[:0]
+        if acc is not None:
+            if shared_i:
+                with np.errstate(over="ignore", invalid="ignore"):
+                    op.reduce_into(acc, vals[shared_i])
+                for i, row in zip(shared_i, acc):
+                    local[keys[i]] = row
+            if len(shared_i) != len(keys):
+                for k, c, row in zip(keys, cur, vals):
+                    if c is None:
+                        local[k] = row
+            return local
     if isinstance(vals, np.ndarray) and vals.ndim == 2:
         for k, row in zip(keys, vals):
             cur = local.get(k)

@@ -142,3 +142,62 @@ def test_native_map_pack_matches_the_python_form():
     assert sparse._pack_native(d, OrderedDict(k0=base[0])) is None
     assert sparse._pack_native(d, {}) is None
     assert sparse._pack_native(d, {"k0": [1.0, 2.0]}) is None
+
+
+def test_native_host_partition_matches_java_hash_rule():
+    """csrc/pyext/hostmap_ext.cpp ``partition``: owner = Java String.hashCode % p (signed
+    remainder, negatives wrapped) exactly as utils/hashing.owner_of, incl. non-BMP keys (UTF-16
+    surrogate pairs), insertion order kept per part; non-str keys defer to Python."""
+    import random
+
+    import pytest
+    from mp4x.ops import native
+    from mp4x.utils.hashing import owner_of
+
+    ext = native.hostmap_ext()
+    if ext is None:
+        pytest.skip("_mp4x_hostmap not built")
+    rng = random.Random(7)
+    keys = ["", "a", "hello", "f123", "é", "日本語", "😀x", "\U0010ffff", "a" * 100]
+    for _ in range(2000):
+        keys.append("".join(chr(rng.choice([rng.randint(32, 126), rng.randint(160, 0xD7FF),
+                                            rng.randint(0x10000, 0x10FFFF)])) for _ in range(rng.randint(0, 12))))
+    m = {k: i for i, k in enumerate(keys)}
+    for p in (1, 2, 3, 5, 7, 8):
+        parts = ext.partition(m, p)
+        assert sum(map(len, parts)) == len(m)
+        for r, d in enumerate(parts):
+            assert all(owner_of(k, p) == r for k in d)
+            assert list(d) == [k for k in m if owner_of(k, p) == r]       # insertion order
+    assert ext.partition({1: 2}, 2) is None
+
+
+def test_native_stack_rows_and_vectorised_merge():
+    """``wire.stack_rows`` / ``merge_reduce`` with numpy rows equal the per-key reference."""
+    import numpy as np
+    from mp4x import Operators
+    from mp4x.parallel import wire
+
+    rng = np.random.default_rng(0)
+    rows = [rng.standard_normal(5).astype(np.float32) for _ in range(50)]
+    assert np.array_equal(wire.stack_rows(rows), np.stack(rows))
+    assert np.array_equal(wire.stack_rows(rows, np.float64), np.stack(rows).astype(np.float64))
+    mixed = rows[:3] + [rows[3].astype(np.float64)]
+    assert np.array_equal(wire.stack_rows(mixed), np.stack(mixed))            # falls back
+    local = {f"k{i}": rows[i].copy() for i in range(0, 50, 2)}
+    keys = [f"k{i}" for i in range(50)]
+    vals = np.stack(rows[::-1])
+    for op in (Operators.Float.SUM, Operators.Float.MAX):
+        expect = {k: v.copy() for k, v in local.items()}
+        for k, row in zip(keys, vals):
+            if k in expect:
+                op.reduce_into(expect[k], row)
+            else:
+                expect[k] = row
+        got = wire.merge_reduce({k: v.copy() for k, v in local.items()}, keys, vals, op)
+        assert got.keys() == expect.keys()
+        assert all(np.array_equal(got[k], expect[k]) for k in keys)
+    # a shared local value of another dtype takes the per-key path (its dtype is kept)
+    odd = {"k0": rows[0].astype(np.float64)}
+    got = wire.merge_reduce(odd, keys[:2], vals[:2], Operators.Float.SUM)
+    assert got["k0"].dtype == np.float64 and np.allclose(got["k0"], rows[0] + vals[0])

@@ -10,6 +10,10 @@
 * ``mp4x/_native/_mp4x_team*.so`` — CPython extension (csrc/pyext/team_ext.cpp) binding the
   host runtime's thread team for ThreadCommSlave (buffer protocol + one FASTCALL per phase),
   linked against libmp4x_host.so next to it (rpath $ORIGIN).
+* ``mp4x/_native/_mp4x_map*.so`` — CPython extension over libtorch (csrc/pyext/map_ext.cpp): the
+  device map collectives' Dict[key, Tensor] -> ids / rows walk.
+* ``mp4x/_native/_mp4x_hostmap*.so`` — plain CPython extension (csrc/pyext/hostmap_ext.cpp): the
+  host map collectives' Java-hash owner partition.
 
 Incremental: objects are rebuilt only when a source or header is newer.
 ``--debug`` builds ``libmp4x_hip_debug.so`` instead: ``-O1 -g -DMP4X_DEBUG``, which turns on the
@@ -148,6 +152,18 @@ def build_pyext(host_so):
     return out
 
 
+def build_hostmapext():
+    """``_mp4x_hostmap``: plain CPython extension (no torch) for the host map collectives."""
+    import sysconfig
+    src = os.path.join(CSRC, "pyext", "hostmap_ext.cpp")
+    out = os.path.join(OUT, "_mp4x_hostmap" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if os.path.exists(src) and newer(src, out, []):
+        run(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-shared", "-I", sysconfig.get_paths()["include"],
+             src, "-o", out])
+        print("  g++  ", os.path.relpath(src, ROOT), "->", os.path.relpath(out, ROOT))
+    return out
+
+
 def build_mapext():
     """``_mp4x_map``: CPython extension reading ``at::Tensor`` facts directly (libtorch headers,
     linked against the torch libraries PyTorch itself loads; rpath to torch/lib)."""
@@ -187,6 +203,7 @@ def main(argv=None):
     build_hip(a.j)
     build_pyext(build_host(a.j))
     build_mapext()
+    build_hostmapext()
     return 0
 
 
