@@ -320,3 +320,24 @@ def test_zs_codec_roundtrip_bits(dtype):
     out = torch.full_like(x, 7)
     K.zs_decode(masks, counts, vals, chunks, out)
     assert torch.equal(out.view(iv), x.view(iv))
+
+
+def test_device_map_pass_is_native_and_exact():
+    """The device Map API's dict walk (csrc/pyext/map_ext.cpp) is loaded on the GPU box, finds
+    the rows of a CUDA table, and the (ids, rows) it produces equal the per-key Python form."""
+    import numpy as np
+    from mp4x.ops import native
+    from mp4x.parallel import sparse
+
+    assert native.map_ext() is not None, "_mp4x_map not built/loaded"
+    table = torch.randn(4096, 32, device=DEV)
+    keys = [f"k{i}" for i in range(4096)]
+    order = np.random.default_rng(0).permutation(4096)
+    m = {keys[i]: table[i] for i in order}
+    d = sparse.KeyDictionary()
+    d.learn_round([keys[::2]])
+    ids, nmiss, rows, base = sparse._pack_native(d, m)
+    assert nmiss == 2048 and base is table
+    assert np.array_equal(ids, d.lookup(list(m.keys())))
+    got = base.reshape(-1, 32).index_select(0, torch.from_numpy(rows).to(DEV))
+    assert torch.equal(got, torch.stack(list(m.values())))
