@@ -671,7 +671,7 @@ def _map_kv(m: Dict, operator):
         if np.isscalar(vals[0]):
             return keys, np.asarray(vals, dtype=NP_DTYPE[operator.dtype])
         if isinstance(vals[0], np.ndarray):
-            return keys, np.stack(vals).astype(NP_DTYPE[operator.dtype], copy=False)
+            return keys, wire.stack_rows(vals, NP_DTYPE[operator.dtype])
     return keys, vals
 
 
