@@ -500,8 +500,8 @@ def _map_tensors_packed(engine, d: "KeyDictionary", mapData: Dict, ids_np, nmiss
     shape = tuple(first.shape)
     if rows is not None:
         v = base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(base.device))
-    else:
-        v = _stack_rows(list(mapData.values()))
+    else:                                           # (the walk already ruled out one base)
+        v = torch.stack(list(mapData.values())).view(len(ids_np), -1)
     return torch.from_numpy(ids_np).to(v.device), v, shape
 
 
@@ -599,7 +599,7 @@ def _maps_by_dest(engine, maps: List[Dict]):
             shape = tuple(first.shape)
             dev = first.device
             v = (base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(dev))
-                 if rows is not None else _stack_rows(list(m.values())))
+                 if rows is not None else torch.stack(list(m.values())).view(len(ids), -1))
             ks.append(torch.from_numpy(ids).to(dev))
             vs.append(v)
             counts.append(len(ids))
