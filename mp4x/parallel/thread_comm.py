@@ -311,6 +311,9 @@ class ThreadCommSlave:
                 if j == rt:
                     continue
                 for pos, m in enumerate(self._slots[j]):
+                    if _tensor_valued(m) or _tensor_valued(out[pos]):
+                        _merge_reduce_tensors(out[pos], m, operator)
+                        continue
                     keys, vals = _map_kv(m, operator)
                     wire.merge_reduce(out[pos], keys, vals, operator)
         self.threadBarrier()
@@ -660,6 +663,60 @@ class ThreadCommSlave:
         if len(tos) != self.slaveNum:
             raise Mp4jException(f"{nt} array length:{len(tos)} must be equal to slaveNum:{self.slaveNum}")
         CommUtils.isfromsTosLegal2D(froms, tos, self.threadNum)
+
+
+def _tensor_valued(m: Dict) -> bool:
+    return bool(m) and _is_torch(next(iter(m.values())))
+
+
+def _torch_reduce_(a, b, operator) -> None:
+    """a = op(a, b) in place for two equal [n, ...] tensors: ONE K1 launch on the GPU
+    (``device_ops.reduce_``, every built-in op incl. the *_LOC ones), numpy's reduce on CPU
+    tensors it can view, plain torch elementwise ops otherwise."""
+    from ..operators import OpCode
+    if a.is_cuda:
+        from ..ops import device_ops
+        device_ops.reduce_(a, [a, b], int(operator.code))
+        return
+    try:
+        operator.reduce_into(a.numpy().reshape(-1), b.numpy().reshape(-1))
+        return
+    except (TypeError, RuntimeError):          # e.g. bf16 CPU tensors: no numpy view
+        pass
+    import torch
+    name = {OpCode.SUM: "add", OpCode.PROD: "mul", OpCode.MAX: "maximum", OpCode.MIN: "minimum",
+            OpCode.BAND: "bitwise_and", OpCode.BOR: "bitwise_or", OpCode.BXOR: "bitwise_xor"}.get(operator.code)
+    if name is None:
+        raise Mp4jException(f"{operator} on {a.dtype} CPU tensors is not supported")
+    getattr(torch, name)(a, b, out=a)
+
+
+def _merge_reduce_tensors(local: Dict, m: Dict, operator) -> None:
+    """Thread-phase map merge for tensor values (reference MapReduce merge,
+    J/comm/ThreadCommSlave.java:259-303): the shared keys' rows are stacked and reduced with ONE
+    kernel (not one launch per key), new keys are inserted as they are.  Results of shared keys
+    are row views of one fresh tensor.  Custom operators apply per key."""
+    import torch
+    keys = list(m.keys())
+    vals = list(m.values())
+    cur = list(map(local.get, keys))
+    shared = [i for i, c in enumerate(cur) if c is not None]
+    if shared:
+        if getattr(operator, "is_custom", False):
+            for i in shared:
+                local[keys[i]] = operator.apply(cur[i], vals[i])
+        else:
+            a = torch.stack([cur[i] for i in shared])
+            b = torch.stack([vals[i] for i in shared])
+            if b.dtype != a.dtype or b.device != a.device:
+                b = b.to(device=a.device, dtype=a.dtype)
+            _torch_reduce_(a, b, operator)
+            for i, row in zip(shared, a.unbind(0)):
+                local[keys[i]] = row
+    if len(shared) != len(keys):
+        for k, c, v in zip(keys, cur, vals):
+            if c is None:
+                local[k] = v
 
 
 def _map_kv(m: Dict, operator):

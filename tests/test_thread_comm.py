@@ -278,3 +278,35 @@ def _process_passthroughs(tc):
 def test_every_process_passthrough_from_thread0(p):
     res, code, _ = run_ranks(p, _process_passthroughs, kind="thread", threads=2, timeout=120)
     assert code == 0 and len(res) == p
+
+
+def tensor_maps(tc):
+    """Thread-mode map collectives with TENSOR values (CPU tensors here; the GPU twin is in
+    test_thread_device_gpu.py): the thread phase reduces shared keys with one stacked reduce."""
+    import torch
+
+    p, r, T = tc.getSlaveNum(), tc.getRank(), tc.getThreadNum()
+
+    def body(t):
+        ops = Operators.Float
+        m = {"shared": torch.full((4,), float(t + 1)), f"u{r}_{t}": torch.full((4,), 1.0),
+             f"proc{r}": torch.full((4,), 2.0)}
+        res = tc.allreduceMap(m, Operands.FLOAT_OPERAND(), ops.SUM)
+        assert len(res) == 1 + p * T + p
+        assert torch.equal(res["shared"], torch.full((4,), float(p * T * (T + 1) // 2)))
+        assert all(torch.equal(res[f"u{i}_{j}"], torch.ones(4)) for i in range(p) for j in range(T))
+        assert all(torch.equal(res[f"proc{i}"], torch.full((4,), 2.0 * T)) for i in range(p))
+        mx = tc.allreduceMap({"k": torch.tensor([float(r * T + t), -float(r * T + t)])},
+                             Operands.FLOAT_OPERAND(), ops.MAX)
+        assert torch.equal(mx["k"], torch.tensor([float(p * T - 1), 0.0]))
+        red = tc.reduceMap({"k": torch.full((3,), 1.0)}, Operands.FLOAT_OPERAND(), ops.SUM, p - 1, T - 1)
+        if r == p - 1 and t == T - 1:
+            assert torch.equal(red["k"], torch.full((3,), float(p * T)))
+        return "ok"
+    return _run_threads(tc, body)
+
+
+@pytest.mark.parametrize("p,T", [(1, 3), (2, 2)])
+def test_thread_tensor_maps(p, T):
+    res, code, _ = run_ranks(p, tensor_maps, (), kind="thread", threads=T, timeout=180)
+    assert code == 0 and all(v == ["ok"] * T for v in res.values())

@@ -107,6 +107,12 @@ def device_thread_matrix(tc, kind):
         m = {"k": 1, f"u{r}_{t}": 1}
         res = tc.allreduceMap(m, operand, ops.SUM)
         assert res["k"] == p * T and len(res) == 1 + p * T
+        # maps of DEVICE tensors: thread phase = one stacked K1 reduce, process phase = K4b/K5
+        dm = {"k": torch.full((8,), t + 1, dtype=dt, device=dev), f"u{r}_{t}": torch.ones(8, dtype=dt, device=dev)}
+        res = tc.allreduceMap(dm, operand, ops.SUM)
+        assert len(res) == 1 + p * T
+        assert bool((res["k"] == p * T * (T + 1) // 2).all()), "device map allreduce"
+        assert all(bool((res[f"u{i}_{j}"] == 1).all()) for i in range(p) for j in range(T))
         # device *Process pass-throughs from thread 0 of every process
         if t == 0:
             pf = CommUtils.createProcessArrayFroms(n, p)
