@@ -212,7 +212,7 @@ def _row_counts(engine, n: int, device) -> List[int]:
     t = torch.tensor([n], dtype=torch.int64, device=device)
     ts = [torch.empty_like(t) for _ in range(engine.p)]
     engine.coll.all_gather(ts, t)
-    return [int(x.item()) for x in ts]
+    return torch.cat(ts).tolist()                  # one host sync, not p
 
 
 def _allgather_v(engine, t: torch.Tensor, sizes: Optional[List[int]] = None) -> torch.Tensor:
@@ -238,8 +238,9 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, k
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
     rkeys, rvals = _exchange_by_owner(engine, keys, v2)
     uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
-    all_k = _allgather_v(engine, uk)
-    all_v = _allgather_v(engine, uv)
+    sizes = _row_counts(engine, uk.shape[0], uk.device)     # one count round for keys AND rows
+    all_k = _allgather_v(engine, uk, sizes)
+    all_v = _allgather_v(engine, uv, sizes)
     return all_k, (all_v.view(-1) if squeeze else all_v)
 
 
