@@ -77,7 +77,46 @@ def main():
            "virtual_ranks": p, "result_keys": nkeys // 2 + p * (nkeys - nkeys // 2)}
     for k in ("total", "to_tensors", "kernels", "to_dict"):
         rec[f"{k}_ms"] = round(max(r[k] for r in res) * 1e3, 2)
+    rec.update(one_rank_host_pass(DEV, nkeys, dim, iters, sync))
     print(json.dumps(rec), flush=True)
+
+
+def one_rank_host_pass(dev, nkeys, dim, iters, sync):
+    """What ONE process (one rank per GPU) pays on the host to turn its dict into (ids, rows):
+    the virtual-rank numbers above serialise p ranks' Python on one GIL.  Native walk
+    (csrc/pyext/map_ext.cpp) vs the Python form of the same pass."""
+    import numpy as np
+    import torch
+    from mp4x.parallel import sparse
+    keys = [f"f{i}" for i in range(nkeys)]
+    d = sparse.KeyDictionary()
+    d.learn_round([keys])
+    base = torch.randn(nkeys, dim, device=dev)
+    m = dict(zip(keys, base.unbind(0)))
+
+    def native():
+        ids, _, rows, b = sparse._pack_native(d, m)
+        v = sparse._take_rows(b.reshape(-1, dim), rows)
+        return torch.from_numpy(ids).to(dev), v
+
+    def python():
+        ids = d.lookup(list(m.keys()))
+        v = sparse._stack_rows(list(m.values()))
+        return torch.from_numpy(ids).to(dev), v
+
+    out = {}
+    for name, fn in (("native", native), ("python", python)):
+        ts = []
+        for _ in range(iters + 1):
+            sync()
+            t0 = time.perf_counter()
+            fn()
+            sync()
+            ts.append(time.perf_counter() - t0)
+        out[f"one_rank_host_pass_{name}_ms"] = round(sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, 2)
+    a, b = native(), python()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    return out
 
 
 if __name__ == "__main__":

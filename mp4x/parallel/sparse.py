@@ -483,6 +483,18 @@ def _pack_native(d: "KeyDictionary", mapData):
     return ids, int(nmiss), rows if rows_ok else None, base
 
 
+def _take_rows(table: torch.Tensor, rows: np.ndarray) -> torch.Tensor:
+    """``table[rows]`` as a fresh tensor: ONE index_select launch on the GPU; numpy's take on the
+    CPU (torch's multi-threaded CPU index_select measured 30-70 ms for 20k x 64 f32 rows on an
+    8-CPU container, np.take 0.7 ms)."""
+    if not table.is_cuda and not table.requires_grad:
+        try:
+            return torch.from_numpy(np.take(table.numpy(), rows, axis=0))
+        except TypeError:                           # no numpy dtype (bf16 ...)
+            pass
+    return table.index_select(0, torch.from_numpy(rows).to(table.device))
+
+
 def _map_tensors_packed(engine, d: "KeyDictionary", mapData: Dict, ids_np, nmiss, rows, base):
     """:func:`_map_tensors` after the native walk: misses numbered in one sync round, values
     gathered as rows of their base tensor with ONE index_select (CPU or GPU) when every value is
@@ -500,7 +512,7 @@ def _map_tensors_packed(engine, d: "KeyDictionary", mapData: Dict, ids_np, nmiss
     first = next(iter(mapData.values()))
     shape = tuple(first.shape)
     if rows is not None:
-        v = base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(base.device))
+        v = _take_rows(base.reshape(-1, first.numel()), rows)
     else:                                           # (the walk already ruled out one base)
         v = torch.stack(list(mapData.values())).view(len(ids_np), -1)
     return torch.from_numpy(ids_np).to(v.device), v, shape
@@ -599,7 +611,7 @@ def _maps_by_dest(engine, maps: List[Dict]):
             first = next(iter(m.values()))
             shape = tuple(first.shape)
             dev = first.device
-            v = (base.reshape(-1, first.numel()).index_select(0, torch.from_numpy(rows).to(dev))
+            v = (_take_rows(base.reshape(-1, first.numel()), rows)
                  if rows is not None else torch.stack(list(m.values())).view(len(ids), -1))
             ks.append(torch.from_numpy(ids).to(dev))
             vs.append(v)
