@@ -326,7 +326,10 @@ class ProcessCommSlave:
                 # the native walk finds the unseen keys AND the ids / rows the device op needs:
                 # one pass over the map instead of two (sparse._map_tensors takes it up)
                 from .sparse import _pack_native
-                packed = _pack_native(d, mapData)
+                try:
+                    packed = _pack_native(d, mapData)
+                except Exception:   # noqa: BLE001 — never fail alone before the agreement round
+                    packed = None
                 self.device._prepacked = (mapData, packed) if packed is not None else None
             if packed is not None:
                 if packed[1]:
