@@ -318,7 +318,13 @@ class ProcessCommSlave:
         the map's), so the device op skips its own key-dictionary round (``_keys_presynced``)."""
         mine = -1 if not mapData else int(_is_torch(next(iter(mapData.values()))))
         new = []
-        if mine == 1:
+        if mine == 1 and self._device_engine is None:
+            # Creating the device engine is collective (process group, shared tuning table): it
+            # must not start before this round, or a rank with an empty map (which learns only
+            # here that the op is a device op) leaves this rank waiting in the engine's bootstrap
+            # while it waits in the round.  No engine yet = an empty dictionary: every key is new.
+            new = list(dict.fromkeys(mapData.keys() if all_keys is None else all_keys))
+        elif mine == 1:
             from .sparse import TensorMap, _dictionary
             d = _dictionary(self.device)
             packed = None
@@ -337,13 +343,20 @@ class ProcessCommSlave:
                     new = [keys[i] for i in np.flatnonzero(packed[0] < 0)]
             elif not (all_keys is None and isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d):
                 new = d.unknown(list(mapData.keys()) if all_keys is None else list(all_keys))
-        res = self.server.call("allgather_obj", self.rank, (mine, new))
-        on_device = any(f == 1 for f, _ in res)
+        # the value shape / dtype travels too: a rank with an empty map must still size its
+        # (empty) rows like everyone else's for the device exchange
+        meta = None
+        if mine == 1:
+            v0 = next(iter(mapData.values()))
+            meta = (tuple(v0.shape), str(v0.dtype).replace("torch.", ""))
+        res = self.server.call("allgather_obj", self.rank, (mine, new, meta))
+        on_device = any(f == 1 for f, _, _ in res)
         if on_device:
             from .sparse import _dictionary
             eng = self.device
-            _dictionary(eng).learn_round([ks for _, ks in res])
+            _dictionary(eng).learn_round([ks for _, ks, _ in res])
             eng._keys_presynced = True
+            eng._map_meta = next((m for _, _, m in res if m is not None), None)
         return on_device
 
     def gatherMap(self, mapData: Dict, operand: Operand, rootRank: int) -> Dict:

@@ -523,6 +523,7 @@ def _map_tensors(engine, mapData: Dict):
     Vectorised: ids through one ``np.fromiter`` + one host->device copy, values through one
     ``torch.stack`` (r1 built a Python list of ids and a reshaped view per value)."""
     d = _dictionary(engine)
+    meta, engine._map_meta = getattr(engine, "_map_meta", None), None   # (value shape, dtype) of the round
     if isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d:
         _sync_new_keys(engine, [])          # every key is numbered already (collective round)
         rows = mapData._rows.view(len(mapData._ids), -1)
@@ -555,6 +556,12 @@ def _map_tensors(engine, mapData: Dict):
     if vals:
         v = _stack_rows(vals)
         shape = tuple(vals[0].shape)
+    elif meta is not None:                          # the agreement round said what the rows are
+        shape = tuple(meta[0])
+        width = 1
+        for x in shape:
+            width *= x
+        v = torch.empty((0, width), dtype=getattr(torch, meta[1]), device=dev)
     else:
         v = torch.empty((0, 1), device=dev)
         shape = (1,)

@@ -404,3 +404,26 @@ def test_autotune_wall_cap(monkeypatch):
     assert code == 0
     for r, n in res.values():
         assert n == 2 and r["rhd"] >= 0.3, (r, n)    # warm-up + second probe call, no timed calls
+
+
+def first_op_is_a_map_with_an_empty_rank(comm):
+    """The job's FIRST device op is a map collective and rank 0's map is empty: rank 0 learns
+    "device" only in the agreement round, so no rank may bootstrap the (collective) device
+    engine before that round (it used to: rank 1 waited in the process-group bootstrap while
+    rank 0 waited in the round)."""
+    r = comm.getRank()
+    assert comm._device_engine is None
+    m = {} if r == 0 else {"a": torch.ones(3), f"b{r}": torch.full((3,), 2.0)}
+    out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), Operators.Float.SUM)
+    p = comm.getSlaveNum()
+    assert torch.equal(out["a"], torch.full((3,), float(p - 1)))
+    assert len(out) == 1 + (p - 1)
+    out = comm.allreduceMap({"a": torch.ones(3)}, Operands.FLOAT_OPERAND(), Operators.Float.SUM)
+    assert torch.equal(out["a"], torch.full((3,), float(p)))
+    return "ok"
+
+
+@pytest.mark.parametrize("p", [2, 3])
+def test_first_device_op_is_a_map_with_an_empty_rank(p):
+    res, code, _ = run_ranks(p, first_op_is_a_map_with_an_empty_rank, timeout=90)
+    assert code == 0 and set(res.values()) == {"ok"}
