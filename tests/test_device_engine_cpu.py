@@ -420,6 +420,12 @@ def first_op_is_a_map_with_an_empty_rank(comm):
     assert len(out) == 1 + (p - 1)
     out = comm.allreduceMap({"a": torch.ones(3)}, Operands.FLOAT_OPERAND(), Operators.Float.SUM)
     assert torch.equal(out["a"], torch.full((3,), float(p)))
+    # the other map collectives with one empty rank (engine up by now)
+    red = comm.reduceMap({} if r == 1 else {"a": torch.ones(3)}, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0)
+    if r == 0:
+        assert torch.equal(red["a"], torch.full((3,), float(p - 1)))
+    lst = comm.allgatherMap({} if r == 1 else {f"x{r}": torch.full((3,), float(r))}, Operands.FLOAT_OPERAND())
+    assert len(lst) == p and len(lst[1]) == 0 and torch.equal(lst[0]["x0"], torch.zeros(3))
     return "ok"
 
 
