@@ -25,6 +25,11 @@ def main():
     from mp4x import Operators
     from mp4x.parallel import sparse
 
+    # p virtual ranks are p threads of ONE process: with the default 5 ms GIL switch interval
+    # every rendezvous between them can wait out switch intervals, a cost one-process-per-GPU
+    # ranks never pay.  MAP_SWITCH_S sets a shorter one (A/B of the harness artifact).
+    if os.environ.get("MAP_SWITCH_S"):
+        sys.setswitchinterval(float(os.environ["MAP_SWITCH_S"]))
     DEV = os.environ.get("MAP_DEVICE", "cuda:0")
     p = int(os.environ.get("MAP_P", 8))
     nkeys = int(os.environ.get("MAP_KEYS", 200_000))

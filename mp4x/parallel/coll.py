@@ -47,6 +47,20 @@ class TorchColl:
         self.gather_into_tensor_ok = backend != "gloo"
         self.reduce_scatter_ok = backend != "gloo"
 
+    def _exchange_apply(self, obj, fn):
+        """Publish obj, run ``fn(every rank's obj)`` while all of them are still published (the
+        closing barrier keeps every peer's tensor alive and unmodified until everyone has
+        copied from it): the data-movement collectives read peers' tensors directly instead of
+        publishing clones."""
+        self._sync()
+        self.hub.slots[self.rank] = obj
+        self.hub.bar.wait()
+        try:
+            fn(list(self.hub.slots))
+            self._sync()
+        finally:
+            self.hub.bar.wait()
+
     def all_reduce(self, t, code, avg: bool = False):
         """``avg``: SUM then divide by the group size inside the collective (ncclAvg)."""
         dist.all_reduce(t, op=dist.ReduceOp.AVG if avg else _RCCL_OPS[code], group=self.pg)
@@ -138,6 +152,20 @@ class LoopbackColl:
         self.hub.bar.wait()
         return out
 
+    def _exchange_apply(self, obj, fn):
+        """Publish obj, run ``fn(every rank's obj)`` while all of them are still published (the
+        closing barrier keeps every peer's tensor alive and unmodified until everyone has
+        copied from it): the data-movement collectives read peers' tensors directly instead of
+        publishing clones."""
+        self._sync()
+        self.hub.slots[self.rank] = obj
+        self.hub.bar.wait()
+        try:
+            fn(list(self.hub.slots))
+            self._sync()
+        finally:
+            self.hub.bar.wait()
+
     def all_reduce(self, t, code, avg: bool = False):
         xs = self._exchange(t.clone())
         acc = xs[0].clone()
@@ -170,26 +198,30 @@ class LoopbackColl:
         offs = [0]
         for s in in_splits:
             offs.append(offs[-1] + s)
-        pieces = [inp[offs[j]:offs[j + 1]].clone() for j in range(p)]
-        allp = self._exchange(pieces)
-        got = [allp[j][self.rank] for j in range(p)]
-        o = 0
-        for g in got:
-            out[o:o + g.shape[0]].copy_(g)
-            o += g.shape[0]
-        self._sync()
+        r = self.rank
+
+        def take(slots):
+            o = 0
+            for src, so in slots:
+                g = src[so[r]:so[r + 1]]
+                out[o:o + g.shape[0]].copy_(g)
+                o += g.shape[0]
+        self._exchange_apply((inp, offs), take)
 
     def all_gather_into_tensor(self, out, inp):
-        xs = self._exchange(inp.clone())
-        torch.cat([x.reshape(-1) for x in xs]).view(-1)
-        out.view(-1).copy_(torch.cat([x.reshape(-1) for x in xs]))
-        self._sync()
+        flat = out.view(-1)
+        n = inp.numel()
+
+        def take(xs):
+            for j, x in enumerate(xs):
+                flat[j * n:(j + 1) * n].copy_(x.reshape(-1))
+        self._exchange_apply(inp, take)
 
     def all_gather(self, outs, t):
-        xs = self._exchange(t.clone())
-        for o, x in zip(outs, xs):
-            o.copy_(x)
-        self._sync()
+        def take(xs):
+            for o, x in zip(outs, xs):
+                o.copy_(x)
+        self._exchange_apply(t, take)
 
     def reduce_scatter_tensor(self, out, inp, code):
         xs = self._exchange(inp.clone())
