@@ -197,8 +197,7 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     skeys, svals, hist = _pack_by_owner(keys, vals, p)
     recv_counts = torch.empty_like(hist)
     engine.coll.all_to_all_single(recv_counts, hist)
-    send = hist.tolist()
-    recv = recv_counts.tolist()
+    send, recv = torch.stack([hist, recv_counts]).tolist()      # one host sync for both
     rkeys = torch.empty(sum(recv), dtype=keys.dtype, device=keys.device)
     engine.coll.all_to_all_single(rkeys, skeys, recv, send)
     rvals = None
