@@ -201,3 +201,43 @@ def test_native_stack_rows_and_vectorised_merge():
     odd = {"k0": rows[0].astype(np.float64)}
     got = wire.merge_reduce(odd, keys[:2], vals[:2], Operators.Float.SUM)
     assert got["k0"].dtype == np.float64 and np.allclose(got["k0"], rows[0] + vals[0])
+
+
+def test_native_partition_property():
+    """Hypothesis: any str keys (any code points, incl. lone surrogates, which Java also hashes
+    as code units), any p: the native partition equals the Python rule."""
+    import pytest
+    hyp = pytest.importorskip("hypothesis")
+    st = hyp.strategies
+    from mp4x.ops import native
+    from mp4x.utils.hashing import owner_of
+
+    ext = native.hostmap_ext()
+    if ext is None:
+        pytest.skip("_mp4x_hostmap not built")
+
+    def java_units(s):           # owner_of via UTF-16 code units (surrogatepass for lone ones)
+        h = 0
+        b = s.encode("utf-16-be", "surrogatepass")
+        for i in range(0, len(b), 2):
+            h = (31 * h + ((b[i] << 8) | b[i + 1])) & 0xFFFFFFFF
+        return h - (1 << 32) if h >= (1 << 31) else h
+
+    @hyp.settings(max_examples=200, deadline=None)
+    @hyp.given(st.lists(st.text(max_size=20), max_size=60, unique=True), st.integers(1, 9))
+    def check(keys, p):
+        parts = ext.partition({k: None for k in keys}, p)
+        if not keys:
+            assert parts == [{} for _ in range(p)]
+            return
+        for r, d in enumerate(parts):
+            for k in d:
+                h = java_units(k)
+                idx = abs(h) % p
+                if h < 0 and idx:
+                    idx = p - idx
+                assert idx == r
+                if not any(0xD800 <= ord(c) <= 0xDFFF for c in k):
+                    assert owner_of(k, p) == r
+        assert sum(map(len, parts)) == len(keys)
+    check()
