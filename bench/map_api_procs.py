@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""BASELINE config 4 with REAL processes: ``ProcessCommSlave.allreduceMap`` of a
+``Dict[str, Tensor]`` (200k keys x float[64] per rank, half shared) with p processes, one
+``ProcessCommSlave`` each — the deployment shape (one process per GPU), unlike
+``bench/map_api.py`` whose p virtual ranks share one interpreter and one GIL.
+
+On a one-GPU box every process uses ``cuda:0`` and gloo stands in for RCCL in the exchange
+(``MP4X_DEVICE_BACKEND=gloo``: device tensors staged through host memory), so the
+``exchange_and_kernels`` phase is NOT an xGMI number.  The host phases are what a rank pays
+per call whatever the transport:
+
+* ``agree_ms``  — the device/host agreement round through the control plane, which also runs
+  the native dict walk (csrc/pyext/map_ext.cpp) and carries unseen keys (none in steady state);
+* ``to_tensors_ms`` — dict -> (ids, rows): the walk's rows gathered with one K3 launch;
+* ``exchange_and_kernels_ms`` — K4b partition, all-to-all, K5 reduce-by-key, all-gather-v;
+* ``to_dict_ms`` — the lazy ``TensorMap`` result.
+
+Reference: ProcessCommSlave.allreduceMap (J/comm/ProcessCommSlave.java:2053-2088).
+  python bench/map_api_procs.py [--p 4] [--keys 200000] [--dim 64] [--iters 5]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def body(comm, nkeys, dim, iters):
+    import torch
+    from mp4x import Operands, Operators
+    from mp4x.parallel import sparse
+
+    r, p = comm.getRank(), comm.getSlaveNum()
+    dev = torch.device("cuda", torch.cuda.current_device())
+    op = Operators.Float.SUM
+    base = torch.randn(nkeys, dim, device=dev, generator=torch.Generator(device=dev).manual_seed(r))
+    keys = [f"f{i}" for i in range(nkeys // 2)] + [f"r{r}_{i}" for i in range(nkeys - nkeys // 2)]
+    m = dict(zip(keys, base.unbind(0)))
+    out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)      # numbering round (first call)
+    assert len(out) == nkeys // 2 + p * (nkeys - nkeys // 2)
+    ph = {"total": [], "agree": [], "to_tensors": [], "exchange_and_kernels": [], "to_dict": []}
+    for _ in range(iters):
+        torch.cuda.synchronize()
+        comm.barrier()
+        t0 = time.perf_counter()
+        comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        # the same call, phase by phase (what allreduceMap runs, in order)
+        comm.barrier()
+        a = time.perf_counter()
+        assert comm._map_on_device(m)
+        b = time.perf_counter()
+        eng = comm.device
+        k, v, shape = sparse._map_tensors(eng, m)
+        torch.cuda.synchronize()
+        c = time.perf_counter()
+        rk, rv = sparse.allreduce_sparse(eng, k, v, op, sparse._dictionary(eng).bits)
+        torch.cuda.synchronize()
+        d = time.perf_counter()
+        res = sparse._tensors_map(eng, rk, rv, shape)
+        e = time.perf_counter()
+        assert len(res) == len(out)
+        for name, dt in (("total", t1 - t0), ("agree", b - a), ("to_tensors", c - b),
+                         ("exchange_and_kernels", d - c), ("to_dict", e - d)):
+            ph[name].append(dt)
+    return {k: sorted(v)[len(v) // 2] for k, v in ph.items()}
+
+
+def main():
+    from spawn_ranks import run_spawn
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--p", type=int, default=4)
+    ap.add_argument("--keys", type=int, default=200_000)
+    ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    res = run_spawn(a.p, body, args=(a.keys, a.dim, a.iters), timeout=600)
+    rec = {"config": f"allreduceMap Dict[str, float[{a.dim}]] {a.keys} keys/rank (50% shared)",
+           "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)"}
+    for k in ("total", "agree", "to_tensors", "exchange_and_kernels", "to_dict"):
+        rec[f"{k}_ms_max_rank"] = round(max(v[k] for v in res.values()) * 1e3, 2)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
