@@ -379,9 +379,20 @@ class TensorMap(MutableMapping):
     ``len``, ``items``, ``==``, assignment / deletion through an overlay).  Passed back into a
     map collective unmodified, its ids and rows are used directly (no per-key work at all)."""
 
-    def __init__(self, d: "KeyDictionary", ids: np.ndarray, rows: torch.Tensor, shape):
+    def __init__(self, d: "KeyDictionary", ids, rows: torch.Tensor, shape):
         self._d = d
-        self._ids = ids
+        # ids stay where the collective left them: a device result is NOT copied to the host
+        # (and the host does not wait for the GPU) until a key is actually looked at; fed back
+        # into the next map collective unmodified it never leaves the GPU
+        if isinstance(ids, torch.Tensor):
+            self._kdev, self._ids_np = ids, None
+            self._ev = None
+            if ids.is_cuda:
+                self._ev = torch.cuda.Event()
+                self._ev.record()
+        else:
+            self._kdev, self._ids_np, self._ev = None, ids, None
+        self._n = int(ids.shape[0])
         self._rows = rows
         self._shape = tuple(shape)
         self._keys = None          # key list (lazy)
@@ -392,6 +403,14 @@ class TensorMap(MutableMapping):
     def pristine(self) -> bool:
         return not self._over and not self._dead
 
+    @property
+    def _ids(self) -> np.ndarray:
+        if self._ids_np is None:
+            if self._ev is not None:
+                self._ev.synchronize()           # the producing stream's kernels are done
+            self._ids_np = self._kdev.cpu().numpy()
+        return self._ids_np
+
     def _klist(self) -> List:
         if self._keys is None:
             self._keys = self._d.keys_of(self._ids)
@@ -399,7 +418,7 @@ class TensorMap(MutableMapping):
 
     def _idx(self) -> Dict:
         if self._index is None:
-            self._index = dict(zip(self._klist(), range(len(self._ids))))
+            self._index = dict(zip(self._klist(), range(self._n)))
         return self._index
 
     def __getitem__(self, k):
@@ -438,13 +457,13 @@ class TensorMap(MutableMapping):
 
     def __len__(self):
         if self.pristine():
-            return len(self._ids)
+            return self._n
         idx = self._idx()
         return len(idx) - len(self._dead) + sum(1 for k in self._over if k not in idx or k in self._dead)
 
     def values(self):
         if self.pristine():
-            return list(self._rows.view((len(self._ids),) + self._shape).unbind(0))
+            return list(self._rows.view((self._n,) + self._shape).unbind(0))
         return super().values()
 
     def __repr__(self):
@@ -552,7 +571,9 @@ def _map_tensors(engine, mapData: Dict):
     meta, engine._map_meta = getattr(engine, "_map_meta", None), None   # (value shape, dtype) of the round
     if isinstance(mapData, TensorMap) and mapData.pristine() and mapData._d is d:
         _sync_new_keys(engine, [])          # every key is numbered already (collective round)
-        rows = mapData._rows.view(len(mapData._ids), -1)
+        rows = mapData._rows.view(mapData._n, -1)
+        if mapData._kdev is not None and mapData._kdev.device == rows.device:
+            return mapData._kdev, rows, mapData._shape        # ids never left the GPU
         return torch.from_numpy(mapData._ids).to(rows.device), rows, mapData._shape
     pre = getattr(engine, "_prepacked", None)
     engine._prepacked = None
@@ -596,7 +617,7 @@ def _map_tensors(engine, mapData: Dict):
 
 
 def _tensors_map(engine, k: torch.Tensor, v: torch.Tensor, shape) -> "TensorMap":
-    return TensorMap(_dictionary(engine), k.cpu().numpy(), v, shape)
+    return TensorMap(_dictionary(engine), k, v, shape)
 
 
 def allreduce_map_device(engine, mapData: Dict, operator) -> Dict:
