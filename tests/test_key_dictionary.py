@@ -241,3 +241,27 @@ def test_native_partition_property():
                     assert owner_of(k, p) == r
         assert sum(map(len, parts)) == len(keys)
     check()
+
+
+def test_tensor_map_with_tensor_ids_is_lazy():
+    """A TensorMap made from an id TENSOR (what the device collectives return) converts the ids
+    to the host only on first key access, and hands the same id tensor back when fed into the
+    next map collective unmodified."""
+    import torch
+    from mp4x.parallel.sparse import KeyDictionary, TensorMap, _map_tensors
+
+    d = KeyDictionary()
+    d.learn_round([["a", "b", "c"]])
+    ids = torch.tensor([2, 0], dtype=torch.int64)
+    rows = torch.arange(8.0).view(2, 4)
+    tm = TensorMap(d, ids, rows, (4,))
+    assert len(tm) == 2 and tm._ids_np is None            # nothing converted yet
+
+    class Eng:                                             # no sync round needed: pristine map
+        _keydict = d
+        device = torch.device("cpu")
+        _keys_presynced = True
+    k, v, shape = _map_tensors(Eng, tm)
+    assert k is ids and torch.equal(v, rows) and shape == (4,) and tm._ids_np is None
+    assert list(tm) == ["c", "a"] and torch.equal(tm["a"], rows[1])
+    assert tm._ids_np is not None
