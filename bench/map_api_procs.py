@@ -9,6 +9,7 @@ On a one-GPU box every process uses ``cuda:0`` and gloo stands in for RCCL in th
 ``exchange_and_kernels`` phase is NOT an xGMI number.  The host phases are what a rank pays
 per call whatever the transport:
 
+* ``walk_only_ms`` — the native dict walk alone (part of the agreement round below);
 * ``agree_ms``  — the device/host agreement round through the control plane, which also runs
   the native dict walk (csrc/pyext/map_ext.cpp) and carries unseen keys (none in steady state);
 * ``to_tensors_ms`` — dict -> (ids, rows): the walk's rows gathered with one K3 launch;
@@ -42,7 +43,7 @@ def body(comm, nkeys, dim, iters):
     m = dict(zip(keys, base.unbind(0)))
     out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)      # numbering round (first call)
     assert len(out) == nkeys // 2 + p * (nkeys - nkeys // 2)
-    ph = {"total": [], "agree": [], "to_tensors": [], "exchange_and_kernels": [], "to_dict": []}
+    ph = {"total": [], "walk_only": [], "agree": [], "to_tensors": [], "exchange_and_kernels": [], "to_dict": []}
     for _ in range(iters):
         torch.cuda.synchronize()
         comm.barrier()
@@ -51,6 +52,10 @@ def body(comm, nkeys, dim, iters):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         # the same call, phase by phase (what allreduceMap runs, in order)
+        comm.barrier()
+        w0 = time.perf_counter()
+        sparse._pack_native(sparse._dictionary(comm.device), m)       # the walk alone
+        walk = time.perf_counter() - w0
         comm.barrier()
         a = time.perf_counter()
         assert comm._map_on_device(m)
@@ -65,7 +70,7 @@ def body(comm, nkeys, dim, iters):
         res = sparse._tensors_map(eng, rk, rv, shape)
         e = time.perf_counter()
         assert len(res) == len(out)
-        for name, dt in (("total", t1 - t0), ("agree", b - a), ("to_tensors", c - b),
+        for name, dt in (("total", t1 - t0), ("walk_only", walk), ("agree", b - a), ("to_tensors", c - b),
                          ("exchange_and_kernels", d - c), ("to_dict", e - d)):
             ph[name].append(dt)
     return {k: sorted(v)[len(v) // 2] for k, v in ph.items()}
@@ -82,7 +87,7 @@ def main():
     res = run_spawn(a.p, body, args=(a.keys, a.dim, a.iters), timeout=600)
     rec = {"config": f"allreduceMap Dict[str, float[{a.dim}]] {a.keys} keys/rank (50% shared)",
            "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)"}
-    for k in ("total", "agree", "to_tensors", "exchange_and_kernels", "to_dict"):
+    for k in ("total", "walk_only", "agree", "to_tensors", "exchange_and_kernels", "to_dict"):
         rec[f"{k}_ms_max_rank"] = round(max(v[k] for v in res.values()) * 1e3, 2)
     print(json.dumps(rec), flush=True)
 
