@@ -79,7 +79,9 @@ def main():
 
     res = run_virtual(p, body, device=DEV)
     rec = {"config": "allreduceMap Dict[str, float[%d]] %d keys/rank (50%% shared)" % (dim, nkeys),
-           "virtual_ranks": p, "result_keys": nkeys // 2 + p * (nkeys - nkeys // 2)}
+           "virtual_ranks": p, "result_keys": nkeys // 2 + p * (nkeys - nkeys // 2),
+           "dict_per_call": "same dict every call (walk cached by PEP 509 version tag; "
+                            "one_rank_host_pass_native_ms is the uncached walk)"}
     for k in ("total", "to_tensors", "kernels", "to_dict"):
         rec[f"{k}_ms"] = round(max(r[k] for r in res) * 1e3, 2)
     rec.update(one_rank_host_pass(DEV, nkeys, dim, iters, sync))
@@ -109,8 +111,15 @@ def one_rank_host_pass(dev, nkeys, dim, iters, sync):
         v = sparse._stack_rows(list(m.values()))
         return torch.from_numpy(ids).to(dev), v
 
+    def native_cached():
+        return native()
+
     out = {}
-    for name, fn in (("native", native), ("python", python)):
+    for name, fn in (("native", native), ("python", python), ("native_same_dict_cached", native_cached)):
+        # "native": the full walk every call (walk cache off); "..._cached": the same dict passed
+        # again unmodified, which skips the walk (PEP 509 version tag, sparse._pack_native)
+        sparse._WALK_CACHE = name == "native_same_dict_cached"
+        d._walk_cache = None
         ts = []
         for _ in range(iters + 1):
             sync()
@@ -119,6 +128,7 @@ def one_rank_host_pass(dev, nkeys, dim, iters, sync):
             sync()
             ts.append(time.perf_counter() - t0)
         out[f"one_rank_host_pass_{name}_ms"] = round(sorted(ts[1:])[len(ts[1:]) // 2] * 1e3, 2)
+    sparse._WALK_CACHE = True
     a, b = native(), python()
     assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
     return out

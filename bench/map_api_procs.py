@@ -17,7 +17,7 @@ per call whatever the transport:
 * ``to_dict_ms`` — the lazy ``TensorMap`` result.
 
 Reference: ProcessCommSlave.allreduceMap (J/comm/ProcessCommSlave.java:2053-2088).
-  python bench/map_api_procs.py [--p 4] [--keys 200000] [--dim 64] [--iters 5]
+  python bench/map_api_procs.py [--p 4] [--keys 200000] [--dim 64] [--iters 5] [--fresh-dict]
 """
 import argparse
 import json
@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def body(comm, nkeys, dim, iters):
+def body(comm, nkeys, dim, iters, fresh):
     import torch
     from mp4x import Operands, Operators
     from mp4x.parallel import sparse
@@ -44,7 +44,10 @@ def body(comm, nkeys, dim, iters):
     out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)      # numbering round (first call)
     assert len(out) == nkeys // 2 + p * (nkeys - nkeys // 2)
     ph = {"total": [], "walk_only": [], "agree": [], "to_tensors": [], "exchange_and_kernels": [], "to_dict": []}
+    rows_list = list(m.values())
     for _ in range(iters):
+        if fresh:      # a new dict object per call (same keys / rows): the full walk every call
+            m = dict(zip(keys, rows_list))
         torch.cuda.synchronize()
         comm.barrier()
         t0 = time.perf_counter()
@@ -52,10 +55,14 @@ def body(comm, nkeys, dim, iters):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         # the same call, phase by phase (what allreduceMap runs, in order)
+        if fresh:
+            m = dict(zip(keys, rows_list))
         comm.barrier()
         w0 = time.perf_counter()
         sparse._pack_native(sparse._dictionary(comm.device), m)       # the walk alone
         walk = time.perf_counter() - w0
+        if fresh:
+            m = dict(zip(keys, rows_list))
         comm.barrier()
         a = time.perf_counter()
         assert comm._map_on_device(m)
@@ -83,10 +90,13 @@ def main():
     ap.add_argument("--keys", type=int, default=200_000)
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--fresh-dict", action="store_true",
+                    help="a new dict object every call (no walk cache hit); default: the same dict again")
     a = ap.parse_args()
-    res = run_spawn(a.p, body, args=(a.keys, a.dim, a.iters), timeout=600)
+    res = run_spawn(a.p, body, args=(a.keys, a.dim, a.iters, a.fresh_dict), timeout=600)
     rec = {"config": f"allreduceMap Dict[str, float[{a.dim}]] {a.keys} keys/rank (50% shared)",
-           "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)"}
+           "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)",
+           "dict_per_call": "fresh" if a.fresh_dict else "same (walk cached by PEP 509 version tag)"}
     for k in ("total", "walk_only", "agree", "to_tensors", "exchange_and_kernels", "to_dict"):
         rec[f"{k}_ms_max_rank"] = round(max(v[k] for v in res.values()) * 1e3, 2)
     print(json.dumps(rec), flush=True)

@@ -130,9 +130,22 @@ PyObject* pack(PyObject*, PyObject* const* a, Py_ssize_t na) {
   return Py_BuildValue("(LO)", static_cast<long long>(missing), rows_ok ? Py_True : Py_False);
 }
 
+// dict_version(d) -> int: CPython's per-dict modification tag (PEP 509, ``ma_version_tag``).
+// Every insert, delete or value replacement gives the dict a new, globally unique tag, so an
+// equal tag means the same dict with the same key -> value objects: the walk's result for it
+// (ids, rows) still holds, and the device Map API skips the walk for a map passed again as is.
+PyObject* dict_version(PyObject*, PyObject* d) {
+  if (!PyDict_Check(d)) {
+    PyErr_SetString(PyExc_TypeError, "dict_version(dict)");
+    return nullptr;
+  }
+  return PyLong_FromUnsignedLongLong(reinterpret_cast<PyDictObject*>(d)->ma_version_tag);
+}
+
 PyMethodDef kMethods[] = {
     {"pack", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(pack)), METH_FASTCALL,
      "pack(map, key2id, base, ids, rows) -> (n_missing, rows_ok)"},
+    {"dict_version", reinterpret_cast<PyCFunction>(dict_version), METH_O, "dict_version(d) -> PEP 509 tag"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_mp4x_map", "native Dict[key, Tensor] -> ids/rows pass", -1,

@@ -24,6 +24,7 @@ take int64 id tensors directly and are what a training loop should call.
 from __future__ import annotations
 
 import itertools
+import os
 from collections.abc import MutableMapping
 from typing import Dict, List, Optional
 
@@ -48,6 +49,7 @@ class KeyDictionary:
     def __init__(self):
         self.id2key: List = []
         self.key2id: Dict = {}
+        self._walk_cache = None    # (dict version, dict, base, ids, rows) of the last full walk
 
     def unknown(self, keys) -> List:
         """Keys this rank has never numbered (first-seen order, de-duplicated)."""
@@ -518,11 +520,23 @@ def _pack_native(d: "KeyDictionary", mapData):
         return None
     b = first._base
     base = b if b is not None and b.is_contiguous() else None
+    # the same dict passed again unmodified (equal PEP 509 version tag): its walk still holds
+    ver = ext.dict_version(mapData)
+    c = d._walk_cache
+    if c is not None and c[0] == ver and c[1] is mapData and c[2] is base:
+        return c[3].copy(), 0, (c[4].copy() if c[4] is not None else None), base
     n = len(mapData)
     ids = np.empty(n, dtype=np.int64)
     rows = np.empty(n, dtype=np.int64)
     nmiss, rows_ok = ext.pack(mapData, d.key2id, base, ids, rows)
-    return ids, int(nmiss), rows if rows_ok else None, base
+    rows = rows if rows_ok else None
+    # cache only complete walks (every key numbered; ids never change once given)
+    d._walk_cache = (ver, mapData, base, ids.copy(), rows.copy() if rows is not None else None) \
+        if not nmiss and _WALK_CACHE else None
+    return ids, int(nmiss), rows, base
+
+
+_WALK_CACHE = os.environ.get("MP4X_MAP_WALK_CACHE", "1") == "1"
 
 
 def _take_rows(table: torch.Tensor, rows: np.ndarray) -> torch.Tensor:

@@ -265,3 +265,33 @@ def test_tensor_map_with_tensor_ids_is_lazy():
     assert k is ids and torch.equal(v, rows) and shape == (4,) and tm._ids_np is None
     assert list(tm) == ["c", "a"] and torch.equal(tm["a"], rows[1])
     assert tm._ids_np is not None
+
+
+def test_walk_cache_follows_the_dict_version():
+    """The device Map API skips the dict walk for the same dict passed again unmodified (equal
+    PEP 509 version tag) and walks again after any insert / delete / value replacement."""
+    import numpy as np
+    import pytest
+    import torch
+    from mp4x.ops import native
+    from mp4x.parallel import sparse
+
+    if native.map_ext() is None:
+        pytest.skip("_mp4x_map not built")
+    base = torch.arange(24.0).view(6, 4)
+    d = KeyDictionary()
+    d.learn_round([[f"k{i}" for i in range(7)]])
+    m = {f"k{i}": base[i] for i in range(6)}
+    ids1, n1, rows1, _ = sparse._pack_native(d, m)
+    assert d._walk_cache is not None and d._walk_cache[1] is m
+    ids2, n2, rows2, _ = sparse._pack_native(d, m)            # cache hit: equal results, own copies
+    assert np.array_equal(ids1, ids2) and np.array_equal(rows1, rows2) and ids2 is not d._walk_cache[3]
+    m["k1"] = base[5]                                         # value replaced -> new version
+    ids3, _, rows3, _ = sparse._pack_native(d, m)
+    assert rows3[1] == 5
+    m["k6"] = torch.zeros(4)                                  # foreign value -> no rows
+    ids4, _, rows4, _ = sparse._pack_native(d, m)
+    assert rows4 is None and ids4[-1] == 6
+    m2 = {"k0": base[0], "new": base[1]}                      # a miss is never cached
+    _, nm, _, _ = sparse._pack_native(d, m2)
+    assert nm == 1 and d._walk_cache is None
