@@ -49,7 +49,8 @@ class KeyDictionary:
     def __init__(self):
         self.id2key: List = []
         self.key2id: Dict = {}
-        self._walk_cache = None    # (dict version, dict, base, ids, rows) of the last full walk
+        # (dict version, dict, base, ids, rows, {device copies}) of the last complete walk
+        self._walk_cache = None
 
     def unknown(self, keys) -> List:
         """Keys this rank has never numbered (first-seen order, de-duplicated)."""
@@ -531,7 +532,7 @@ def _pack_native(d: "KeyDictionary", mapData):
     nmiss, rows_ok = ext.pack(mapData, d.key2id, base, ids, rows)
     rows = rows if rows_ok else None
     # cache only complete walks (every key numbered; ids never change once given)
-    d._walk_cache = (ver, mapData, base, ids.copy(), rows.copy() if rows is not None else None) \
+    d._walk_cache = (ver, mapData, base, ids.copy(), rows.copy() if rows is not None else None, {}) \
         if not nmiss and _WALK_CACHE else None
     return ids, int(nmiss), rows, base
 
@@ -570,10 +571,30 @@ def _map_tensors_packed(engine, d: "KeyDictionary", mapData: Dict, ids_np, nmiss
         ids_np[miss] = d.id_array(mk)
     first = next(iter(mapData.values()))
     shape = tuple(first.shape)
+    # the walk cache's entry for this very dict state (if any) also keeps the ids / row indices
+    # already on the device: the same dict passed again costs no host->device copies either
+    c = d._walk_cache
+    dev_cache = None
+    if c is not None and c[1] is mapData and c[2] is base and not nmiss:
+        from ..ops import native
+        if c[0] == native.map_ext().dict_version(mapData):
+            dev_cache = c[5]
+    dev = first.device
     if rows is not None:
-        v = _take_rows(base.reshape(-1, first.numel()), rows)
+        table = base.reshape(-1, first.numel())
+        if dev_cache is not None and table.is_cuda:
+            if "rows" not in dev_cache:
+                dev_cache["rows"] = torch.from_numpy(rows).to(dev)
+            from ..ops.device_ops import gather_rows
+            v = gather_rows(table.contiguous(), dev_cache["rows"])
+        else:
+            v = _take_rows(table, rows)
     else:                                           # (the walk already ruled out one base)
         v = torch.stack(list(mapData.values())).view(len(ids_np), -1)
+    if dev_cache is not None and v.is_cuda:
+        if "ids" not in dev_cache:
+            dev_cache["ids"] = torch.from_numpy(ids_np).to(v.device)
+        return dev_cache["ids"], v, shape
     return torch.from_numpy(ids_np).to(v.device), v, shape
 
 
