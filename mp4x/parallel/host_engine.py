@@ -25,6 +25,7 @@ with ``barrier()``, :731, :1367).
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List
 
 import numpy as np
@@ -110,6 +111,10 @@ def choose_allreduce(p: int, nbytes: int, custom: bool) -> str:
         return "rhd"
     lim = int(os.environ.get("MP4X_RHD_MAX_BYTES", RHD_MAX_BYTES_DEFAULT))
     return "rhd" if nbytes <= lim else "ring"
+
+
+# MAP collectives: direct exchange over the mesh (default) or the reference's ring (MP4X_HOST_MAP_ALGO=ring)
+_MAP_DIRECT = os.environ.get("MP4X_HOST_MAP_ALGO", "direct") != "ring"
 
 
 class HostEngine:
@@ -284,6 +289,18 @@ class HostEngine:
         if p == 1:
             return out
         tag = self.next_tag()
+        if _MAP_DIRECT and p > 2:
+            # direct: ONE encode, sent to every peer over its own mesh connection (the sender
+            # never blocks: readers drain into mailboxes), decoded as it arrives — one step of
+            # latency instead of p - 1 store-and-forward ring steps
+            body = wire.pack_maps([(r, d) for d in block], operand)
+            for j in range(1, p):
+                self.t.send((r + j) % p, tag, body)
+            for j in range(1, p):
+                src = (r - j) % p
+                got = wire.unpack_maps(self.t.recv(src, tag), operand)
+                out[src] = [wire.to_dict(k, v) for _, k, v in got]
+            return out
         nxt, prv = (r + 1) % p, (r - 1) % p
         self.t.send(nxt, tag, wire.pack_maps([(r, d) for d in block], operand))
         for step in range(1, p):
@@ -304,6 +321,20 @@ class HostEngine:
         J/operand/DoubleOperand.java:130-134).
         """
         p, r = self.p, self.rank
+        if _MAP_DIRECT and p > 2:
+            # direct: block b goes straight to its owner b (p - 1 concurrent sends), the owner
+            # merges the p - 1 received blocks in arrival-independent ring order — each merge
+            # sees one rank's map, not the growing union a ring step re-encodes and forwards
+            tag = self.next_tag()
+            for j in range(1, p):
+                b = (r + j) % p
+                self.t.send(b, tag, wire.pack_maps([(r, d) for d in blocks[b]], operand))
+            mine = [dict(d) for d in blocks[r]]
+            for j in range(1, p):
+                got = wire.unpack_maps(self.t.recv((r - j) % p, tag), operand)
+                for jj, (_, keys, vals) in enumerate(got):
+                    wire.merge_reduce(mine[jj], keys, vals, op)
+            return mine
         local = [[dict(d) for d in blk] for blk in blocks]
         if p == 1:
             return local[0]
