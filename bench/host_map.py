@@ -49,7 +49,7 @@ def main():
     assert n == {a.keys // 2 + a.p * (a.keys - a.keys // 2)}, n
     print(json.dumps({"config": f"host allreduceMap Dict[str, float32[{a.dim}]] {a.keys} keys/rank (50% shared)",
                       "procs": a.p, "result_keys": n.pop(),
-                      "map_algo": os.environ.get("MP4X_HOST_MAP_ALGO", "direct"),
+                      "map_algo": os.environ.get("MP4X_HOST_MAP_ALGO", "auto"),
                       "native_ext": os.environ.get("MP4X_MAP_EXT", "1") != "0",
                       "p50_ms_max_rank": round(max(v[1] for v in res.values()) * 1e3, 2)}))
 

@@ -113,8 +113,19 @@ def choose_allreduce(p: int, nbytes: int, custom: bool) -> str:
     return "rhd" if nbytes <= lim else "ring"
 
 
-# MAP collectives: direct exchange over the mesh (default) or the reference's ring (MP4X_HOST_MAP_ALGO=ring)
-_MAP_DIRECT = os.environ.get("MP4X_HOST_MAP_ALGO", "direct") != "ring"
+# MAP collectives: direct exchange over the mesh or the reference's ring.  Measured on the box
+# (profiles/r2/host_map_algo_box.jsonl, 50k keys x float[16] per rank): direct 38 vs ring 78 ms at
+# p = 4, but 112 vs 92 ms at p = 8 (p - 1 reader threads per process then contend for the GIL
+# with the merging thread), so direct is the default up to MP4X_HOST_MAP_DIRECT_MAX_P = 4.
+# MP4X_HOST_MAP_ALGO=ring | direct forces one.
+_MAP_ALGO = os.environ.get("MP4X_HOST_MAP_ALGO", "auto")
+_MAP_DIRECT_MAX_P = int(os.environ.get("MP4X_HOST_MAP_DIRECT_MAX_P", 4))
+
+
+def _map_direct(p: int) -> bool:
+    if p <= 2 or _MAP_ALGO == "ring":
+        return False
+    return _MAP_ALGO == "direct" or p <= _MAP_DIRECT_MAX_P
 
 
 class HostEngine:
@@ -289,7 +300,7 @@ class HostEngine:
         if p == 1:
             return out
         tag = self.next_tag()
-        if _MAP_DIRECT and p > 2:
+        if _map_direct(p):
             # direct: ONE encode, sent to every peer over its own mesh connection (the sender
             # never blocks: readers drain into mailboxes), decoded as it arrives — one step of
             # latency instead of p - 1 store-and-forward ring steps
@@ -321,7 +332,7 @@ class HostEngine:
         J/operand/DoubleOperand.java:130-134).
         """
         p, r = self.p, self.rank
-        if _MAP_DIRECT and p > 2:
+        if _map_direct(p):
             # direct: block b goes straight to its owner b (p - 1 concurrent sends), the owner
             # merges the p - 1 received blocks in arrival-independent ring order — each merge
             # sees one rank's map, not the growing union a ring step re-encodes and forwards
