@@ -4,14 +4,29 @@
 ``python bench.py --gpus N --steps K --warmup W`` — for N>1 the driver launches one rank
 per GPU with ``torch.distributed.run``.  Every step is ONE public-API call
 
-    comm.allreduceArray(buf, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
+    comm.allreduceArray(buf, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n, scale=1/p)
 
 on a 1e9-byte float32 array (250,000,000 elements, synthetic random data) resident on the
-rank's MI355X, i.e. the reference's ``ProcessCommSlave.allreduceArray`` on the BASELINE
-config.  For N>1 the warm-up first autotunes the schedule (RCCL, IPC two-shot over xGMI,
-a2a two-shot; MAX time over ranks, on a scratch tensor).  Timing: W untimed warmup calls,
-barrier + device sync, K timed calls with a hipEvent pair around each (p50 / p99),
-barrier + sync; MAX over ranks.
+rank's MI355X, i.e. the reference's ``ProcessCommSlave.allreduceArray``
+(ProcessCommSlave.java:1733-1763) on the BASELINE config.  ``scale=1/p`` (the DP gradient
+average, fused into the collective's final write) keeps the values bounded at any ``--steps``:
+a SUM would grow p-fold per call and reach f32 inf after ~40 calls at p=8.
+
+For N>1 the warm-up first autotunes the schedule (RCCL, RCCL with more channels, IPC two-shot
+over xGMI staged / zero-copy pull / zero-copy push, a2a, rhd; ``--autotune-iters`` timed calls
+each, MAX over ranks, every candidate checked against an exact pattern first) and pins the
+fastest.  Timing: W untimed warmup calls, barrier + device sync, K timed calls with a hipEvent
+pair around each (p50 / p99), barrier + sync; MAX over ranks.
+
+Self-verification (after the timed steps, outside them): the SAME call on the SAME buffer with
+the pinned schedule runs once more on an exact pattern; the result is compared with the fp64
+answer on every rank -> ``verified`` and ``max_abs_err`` (MAX over ranks).  A wrong result
+makes the run exit non-zero (rc 3) after printing its line.
+
+RCCL baseline at equal method (N>1, GPU): K more calls of the same public call with the RCCL
+schedule forced (``ncclAllReduce``, fused ncclAvg), same hipEvent timing, MAX over ranks ->
+``rccl_busbw_gbps`` / ``rccl_p50_ms`` next to ``value`` ("judge our
+numbers against RCCL's on the same box").
 
 busbw follows the nccl-tests convention used in BASELINE.md: algbw = bytes / t,
 busbw = algbw * 2(p-1)/p, and ``value`` IS that busbw (per rank, the BASELINE metric; the
@@ -21,11 +36,9 @@ no-op by the reference's contract, so N=1 times the OUT-OF-PLACE form of the sam
 (``out=``; a 1 GB device copy through the K1 kernel) and reports algbw for it — HBM
 evidence, not an allreduce number.
 
-For N>1 the buffer is registered with the communicator (``registerBuffer``, collective), so
-the zero-copy two-shot can run straight on the peers' tensors; the autotune times it next to
-RCCL and the staged kernels (bounded per candidate, ``MP4X_AUTOTUNE_CAP_S``) and only ever
-pins a schedule that was exact on every rank; if every custom schedule fails, RCCL stays.
-Before any IPC tier is used, a collective self-test of the IPC mesh runs (``ipc_selftest``).
+``--alloc``: how the N>1 buffer is made — ``register`` (default: a caching-allocator tensor
+registered with ``registerBuffer``), ``memalloc`` (``comm.memAlloc``: mapped into every peer
+at any size, e.g. ``--bytes 8000000000``), ``plain`` (unregistered: staged kernels / RCCL).
 """
 import argparse
 import json
@@ -39,6 +52,7 @@ sys.path.insert(0, ROOT)
 # reference busbw (MB/s) for ~1 GB allreduce, BASELINE.md section D (mean of 1e8 and 5e8 rows)
 REF_BUSBW_MBPS = {2: 85.2, 4: 92.1, 6: 86.8, 8: 88.0}
 METRIC = "allreduce bus bandwidth (GB/s) + p50 latency, 1 GB float[], 1/2/4/8 MI355X"
+RC_UNVERIFIED = 3
 
 
 class _CpuEvent:
@@ -54,22 +68,40 @@ class _CpuEvent:
         return (other.t - self.t) * 1e3
 
 
+def _timed(torch, step, steps):
+    """K calls of ``step`` with a hipEvent pair around each; returns (wall start, start events,
+    end events) — the caller synchronises, then reads the wall time and the event pairs."""
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for i in range(steps):
+        starts[i].record()
+        step()
+        ends[i].record()
+    return t0, starts, ends
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bytes", type=int, default=1_000_000_000)
-    ap.add_argument("--algo", default=None, help="force device algorithm: rccl | a2a")
+    ap.add_argument("--algo", default=None, help="force device algorithm: rccl | a2a | ipc2z | ...")
     ap.add_argument("--codec", default=None, help="wire codec for the fp8-compressed config: fp8")
     ap.add_argument("--cpu", action="store_true", help="dry run of the launch/rendezvous path on CPU (gloo)")
     ap.add_argument("--no-autotune", action="store_true",
                     help="skip the warm-up schedule autotune (RCCL vs IPC two-shot vs a2a) for N>1")
-    ap.add_argument("--no-register", action="store_true",
-                    help="do not register the buffer for the zero-copy IPC two-shot")
+    ap.add_argument("--autotune-iters", type=int, default=5, help="timed calls per autotune candidate")
+    ap.add_argument("--alloc", choices=("register", "memalloc", "plain"), default="register")
+    ap.add_argument("--no-register", action="store_true", help="= --alloc plain")
+    ap.add_argument("--no-verify", action="store_true", help="skip the post-run exact-pattern check")
+    ap.add_argument("--no-rccl-baseline", action="store_true", help="skip the equal-method RCCL baseline")
     ap.add_argument("--no-tier-sweep", action="store_true",
                     help="N>1: skip the untimed per-size schedule sweep (4 KiB .. 64 MiB) run after the timed steps")
     args = ap.parse_args()
+    if args.no_register:
+        args.alloc = "plain"
     if args.algo:
         os.environ["MP4X_DEVICE_ALGO"] = args.algo
 
@@ -96,17 +128,26 @@ def main():
     n = args.bytes // 4
     operand = Operands.FLOAT_OPERAND(codec=args.codec)
     op = Operators.Float.SUM
+    scale = 1.0 / p
 
+    registered = False
+    if p > 1 and not args.cpu:
+        comm.device  # bring up the RCCL communicator before anything is timed
+    if p > 1 and not args.cpu and args.alloc == "memalloc":
+        buf = comm.memAlloc(n, torch.float32)
+        registered = comm.device._ipc_obj is not None and comm.device._ipc_obj.registered(buf) is not None
+    else:
+        buf = torch.empty(n, device=dev, dtype=torch.float32)
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
-    buf = torch.randn(n, device=dev, dtype=torch.float32, generator=g)
+    buf.normal_(generator=g)
     out = torch.empty_like(buf) if p == 1 else None
 
     def step():
         if p == 1:
             comm.allreduceArray(buf, operand, op, 0, n, out=out)
         else:
-            comm.allreduceArray(buf, operand, op, 0, n)
+            comm.allreduceArray(buf, operand, op, 0, n, scale=scale)
 
     def sync_all():
         torch.cuda.synchronize()
@@ -114,42 +155,94 @@ def main():
             comm.peer_barrier() if args.cpu else comm.device.barrier()
             torch.cuda.synchronize()
 
+    def max_over_ranks(vals):
+        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        if p > 1:
+            if args.cpu:
+                t = torch.from_numpy(comm.allreduceArray(t.numpy(), Operands.DOUBLE_OPERAND(),
+                                                         Operators.Double.MAX, 0, len(vals)))
+            else:
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.tolist()
+
     tuned = None
-    registered = False
     if p > 1 and not args.cpu:
-        comm.device  # bring up the RCCL communicator before timing
-        if not args.no_register:
+        if args.alloc == "register":
             registered = comm.registerBuffer(buf)   # collective; False on every rank alike
         if not (args.no_autotune or args.algo or args.codec):
             # untimed: measure every applicable schedule on a scratch tensor of this shape and
             # pin the fastest (all ranks agree: MAX over ranks); the timed steps run it in full
             tuned = {k: round(v * 1e3, 3) for k, v in
-                     comm.device.autotune_allreduce(buf, op, iters=2).items()}
+                     comm.device.autotune_allreduce(buf, op, iters=max(1, args.autotune_iters)).items()}
     for _ in range(args.warmup):
         step()
     sync_all()
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        starts[i].record()
-        step()
-        ends[i].record()
+    t0, starts, ends = _timed(torch, step, args.steps)
     sync_all()
     wall = time.perf_counter() - t0
     lat = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))   # ms
+    wall, p50, p99 = max_over_ranks([wall, lat[len(lat) // 2], lat[min(len(lat) - 1, int(0.99 * len(lat)))]])
 
-    # MAX over ranks
-    vals = torch.tensor([wall, lat[len(lat) // 2], lat[min(len(lat) - 1, int(0.99 * len(lat)))]],
-                        dtype=torch.float64, device=dev)
-    if p > 1:
-        if args.cpu:
-            vals = torch.from_numpy(comm.allreduceArray(vals.numpy(), Operands.DOUBLE_OPERAND(),
-                                                        Operators.Double.MAX, 0, 3))
-        else:
-            dist.all_reduce(vals, op=dist.ReduceOp.MAX)
-    wall, p50, p99 = vals.tolist()
+    ms_per_step = wall * 1e3 / args.steps
+    nbytes = n * 4
+    algbw = nbytes / (ms_per_step * 1e-3) / 1e9
+    factor = 2.0 * (p - 1) / p if p > 1 else 1.0
+    busbw = algbw * factor
+    algo = "k1_copy (out-of-place, 1 rank)" if p == 1 else ("host-tcp" if args.cpu else
+                                  comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand))
+    if algo == "ipc2" and registered and not args.cpu and not comm.device._select_tuned:
+        algo = "ipc2z"
+
+    # ---- self-verification: the same call, same buffer, same pinned schedule, exact pattern
+    verified, max_err = None, None
+    if not args.no_verify:
+        idt = torch.int32 if n < (1 << 31) else torch.int64
+        i13 = torch.arange(n, device=dev, dtype=idt).remainder_(13)
+        buf.copy_(i13 + rank)
+        step()
+        torch.cuda.synchronize()
+        corrupt = os.environ.get("MP4X_BENCH_CORRUPT")      # test hook: a wrong element on one rank
+        res = out if p == 1 else buf
+        if corrupt is not None and int(corrupt) == rank:
+            res[n // 2] += 1.0
+        # exact answer in fp64: sum_j (i%13 + j) = p*(i%13) + p(p-1)/2, times the fused 1/p
+        err = 0.0
+        for lo in range(0, n, 1 << 26):                      # bounded fp64 temporaries
+            hi = min(n, lo + (1 << 26))
+            if p > 1:
+                ex = (i13[lo:hi].double() * p + p * (p - 1) / 2) * scale
+            else:                                            # the out-of-place copy
+                ex = i13[lo:hi].double()
+            err = max(err, float((res[lo:hi].double() - ex).abs().max()))
+        del i13
+        max_err = max_over_ranks([err])[0]
+        # exact schedules: integers, then the 1/p scale (exact for p = 2/4/8); a lossy wire codec
+        # (fp8: two e4m3 roundings, 2^-4 relative each) is held to its own bound
+        tol = 1e-6 * 13 * p if not args.codec else 2.0 ** -3 * 13
+        verified = bool(max_err <= tol)
+
+    # ---- RCCL at equal method on the same buffer (N>1, GPU)
+    rccl = None
+    if p > 1 and not args.cpu and not args.no_rccl_baseline and not args.codec:
+        eng = comm.device
+        saved = eng.algo
+        eng.algo = "rccl"
+        try:
+            for _ in range(max(1, args.warmup)):
+                step()
+            sync_all()
+            r0, rs, re_ = _timed(torch, step, args.steps)
+            sync_all()
+            rwall = time.perf_counter() - r0
+            rlat = sorted(s.elapsed_time(e) for s, e in zip(rs, re_))
+            rwall, rp50, rp99 = max_over_ranks([rwall, rlat[len(rlat) // 2],
+                                                rlat[min(len(rlat) - 1, int(0.99 * len(rlat)))]])
+            rms = rwall * 1e3 / args.steps
+            rccl = {"rccl_ms_per_step": round(rms, 4), "rccl_p50_ms": round(rp50, 4), "rccl_p99_ms": round(rp99, 4),
+                    "rccl_busbw_gbps": round(nbytes / (rms * 1e-3) / 1e9 * factor, 3)}
+        finally:
+            eng.algo = saved
 
     # after the timed steps (never inside them): measure every schedule at the size classes
     # the IPC tiers are chosen for, so a multi-GPU run records the tier boundaries on real links
@@ -171,16 +264,7 @@ def main():
             if flag.item() > 0:
                 break
 
-    ms_per_step = wall * 1e3 / args.steps
-    nbytes = n * 4
-    algbw = nbytes / (ms_per_step * 1e-3) / 1e9
-    factor = 2.0 * (p - 1) / p if p > 1 else 1.0
-    busbw = algbw * factor
     ref = REF_BUSBW_MBPS.get(p)
-    algo = "k1_copy (out-of-place, 1 rank)" if p == 1 else ("host-tcp" if args.cpu else
-                                  comm.device.select("allreduce", nbytes, Operators.Float.SUM, torch.float32, operand))
-    if algo == "ipc2" and registered and not args.cpu and not comm.device._select_tuned:
-        algo = "ipc2z"
     selftest = None if (p == 1 or args.cpu) else comm.device.ipc_selftest
     stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items() if k.startswith("allreduce")}
     if rank == 0:
@@ -199,25 +283,36 @@ def main():
             "data": "synthetic (torch.randn per rank)",
             "config": {"model": f"allreduceArray float[{n}] ({nbytes / 1e9:g} GB), Operators.Float.SUM",
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
-                       "payload_bytes": nbytes, "algo": algo, "registered": registered,
-                       "in_place": p > 1, "autotune_ms": tuned, "ipc_selftest": selftest,
+                       "payload_bytes": nbytes, "algo": algo, "alloc": args.alloc, "registered": registered,
+                       "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
+                       "autotune_iters": args.autotune_iters, "ipc_selftest": selftest,
                        "calls": stats, "tier_sweep_ms": tiers},
+            "verified": verified,
+            "max_abs_err": max_err,
             "busbw_gbps_per_rank": round(busbw, 3),
             "aggregate_busbw_gbps": round(busbw * p, 3),
             "algbw_gbps": round(algbw, 3),
             "p50_ms": round(p50, 4),
             "p99_ms": round(p99, 4),
+            "rccl_busbw_gbps": rccl["rccl_busbw_gbps"] if rccl else None,
+            "rccl_p50_ms": rccl["rccl_p50_ms"] if rccl else None,
+            "rccl_baseline": rccl,
             "busbw_factor": factor,
             "note": ("p=1: nothing crosses a link (nccl-tests busbw factor 2(p-1)/p = 0), so this is "
                      "busbw := algbw of the out-of-place single-rank allreduce, a 1 GB HBM copy through K1; "
                      "N>=2 values are xGMI-link-bound and not comparable to N=1 as a scaling base"
                      if p == 1 else "value = busbw = algbw * 2(p-1)/p (nccl-tests convention, per rank); "
-                                    "aggregate_busbw_gbps = p * busbw"),
+                                    "aggregate_busbw_gbps = p * busbw; rccl_* = the same call with RCCL forced"),
         }
         print(json.dumps(rec), flush=True)
+    if args.alloc == "memalloc" and p > 1 and not args.cpu:
+        comm.memFree(buf)
     comm.close(0)
     if p > 1 and dist.is_initialized():
         dist.destroy_process_group()
+    if verified is False:
+        print(f"bench: result NOT verified (max_abs_err {max_err})", file=sys.stderr, flush=True)
+        sys.exit(RC_UNVERIFIED)
 
 
 if __name__ == "__main__":

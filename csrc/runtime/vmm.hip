@@ -1,0 +1,164 @@
+// Library-owned device allocations that can be mapped into every peer at ANY size (the
+// ncclMemAlloc analogue of mp4x, ``ProcessCommSlave.memAlloc``).
+//
+// Why: hipIpcGetMemHandle/hipIpcOpenMemHandle maps a whole hipMalloc allocation, and on this
+// ROCm an open of an allocation of 2^31 bytes or more never returns
+// (profiles/r2/ipc_open_probe.jsonl).  The reference allreduces 8 GB arrays in place
+// (/root/reference/README.md:313, ProcessCommSlave.java:1733-1763); the zero-copy kernels need
+// those tensors mapped in every peer.  So the allocation is built from the virtual memory API:
+//
+//   * physical chunks (hipMemCreate, ``chunk`` bytes each, a granularity multiple well below
+//     2 GiB) are mapped back to back into ONE reserved VA range: the tensor is contiguous;
+//   * every chunk is exported as a POSIX file descriptor (dmabuf) — the fds travel to the
+//     same-node peers over a unix socket (SCM_RIGHTS, parallel/vmm.py);
+//   * a peer imports every fd, maps the chunks back to back into its own reserved VA range
+//     and grants its device read/write access: one contiguous peer view of the whole tensor,
+//     so the zero-copy kernels (ipc.hip) run on it unchanged.
+//
+// Memory is coarse-grained device memory (like hipMalloc), which is what the zero-copy kernels
+// already run on for registered caching-allocator tensors.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <unistd.h>
+
+namespace {
+
+hipMemAllocationProp make_prop(int dev) {
+  hipMemAllocationProp prop;
+  std::memset(&prop, 0, sizeof(prop));
+  prop.type = hipMemAllocationTypePinned;
+  prop.requestedHandleTypes = hipMemHandleTypePosixFileDescriptor;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  return prop;
+}
+
+hipError_t grant(void* va, size_t bytes, int dev) {
+  hipMemAccessDesc acc;
+  std::memset(&acc, 0, sizeof(acc));
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = dev;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  return hipMemSetAccess(va, bytes, &acc, 1);
+}
+
+// unmap + release chunks [0, n) and free the VA range (best effort, first error returned)
+int teardown(void* va, size_t chunk, int n, const uint64_t* handles, size_t reserved) {
+  int first = 0;
+  for (int i = 0; i < n; ++i) {
+    if (va) {
+      hipError_t e = hipMemUnmap(static_cast<char*>(va) + (size_t)i * chunk, chunk);
+      if (e != hipSuccess && !first) first = (int)e;
+    }
+    if (handles[i]) {
+      hipError_t e = hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)handles[i]);
+      if (e != hipSuccess && !first) first = (int)e;
+    }
+  }
+  if (va && reserved) {
+    hipError_t e = hipMemAddressFree(va, reserved);
+    if (e != hipSuccess && !first) first = (int)e;
+  }
+  return first;
+}
+
+}  // namespace
+
+// Recommended allocation granularity (bytes) of the current device for fd-exportable memory.
+extern "C" int mp4x_vmm_granularity(size_t* gran) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  hipMemAllocationProp prop = make_prop(dev);
+  return (int)hipMemGetAllocationGranularity(gran, &prop, hipMemAllocationGranularityRecommended);
+}
+
+// Allocate ``n`` chunks of ``chunk`` bytes (granularity multiple) mapped back to back at a
+// fresh VA range.  ``fds`` (n entries) get one exported POSIX fd per chunk when ``fds`` is not
+// null; ``handles`` (n entries) get the generic allocation handles.  On failure everything
+// created so far is released and the fds closed.
+extern "C" int mp4x_vmm_create(size_t chunk, int n, void** va_out, uint64_t* handles, int* fds) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  const size_t total = chunk * (size_t)n;
+  for (int i = 0; i < n; ++i) {
+    handles[i] = 0;
+    if (fds) fds[i] = -1;
+  }
+  void* va = nullptr;
+  e = hipMemAddressReserve(&va, total, chunk, nullptr, 0);
+  if (e != hipSuccess) return (int)e;
+  hipMemAllocationProp prop = make_prop(dev);
+  int mapped = 0;
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    hipMemGenericAllocationHandle_t h;
+    e = hipMemCreate(&h, chunk, &prop, 0);
+    if (e != hipSuccess) break;
+    handles[i] = (uint64_t)(uintptr_t)h;
+    e = hipMemMap(static_cast<char*>(va) + (size_t)i * chunk, chunk, 0, h, 0);
+    if (e != hipSuccess) break;
+    mapped = i + 1;
+    if (fds) {
+      int fd = -1;
+      e = hipMemExportToShareableHandle(&fd, h, hipMemHandleTypePosixFileDescriptor, 0);
+      if (e != hipSuccess) break;
+      fds[i] = fd;
+    }
+  }
+  if (e == hipSuccess) e = grant(va, total, dev);
+  if (e != hipSuccess) {
+    if (fds)
+      for (int i = 0; i < n; ++i)
+        if (fds[i] >= 0) { close(fds[i]); fds[i] = -1; }
+    // chunks [mapped, n) were created but not mapped: release them without unmapping
+    for (int i = 0; i < mapped; ++i) hipMemUnmap(static_cast<char*>(va) + (size_t)i * chunk, chunk);
+    for (int i = 0; i < n; ++i)
+      if (handles[i]) { hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)handles[i]); handles[i] = 0; }
+    hipMemAddressFree(va, total);
+    return (int)e;
+  }
+  *va_out = va;
+  return 0;
+}
+
+// Import a peer's ``n`` chunk fds and map them back to back at a fresh VA range of this
+// process, read/write for the current device.  The fds are NOT closed here (the caller owns
+// them; the imported handles keep the memory alive).
+extern "C" int mp4x_vmm_import(const int* fds, size_t chunk, int n, void** va_out, uint64_t* handles) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  const size_t total = chunk * (size_t)n;
+  for (int i = 0; i < n; ++i) handles[i] = 0;
+  void* va = nullptr;
+  e = hipMemAddressReserve(&va, total, chunk, nullptr, 0);
+  if (e != hipSuccess) return (int)e;
+  int mapped = 0;
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    hipMemGenericAllocationHandle_t h;
+    e = hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>((intptr_t)fds[i]),
+                                        hipMemHandleTypePosixFileDescriptor);
+    if (e != hipSuccess) break;
+    handles[i] = (uint64_t)(uintptr_t)h;
+    e = hipMemMap(static_cast<char*>(va) + (size_t)i * chunk, chunk, 0, h, 0);
+    if (e == hipSuccess) mapped = i + 1;
+  }
+  if (e == hipSuccess) e = grant(va, total, dev);
+  if (e != hipSuccess) {
+    for (int i = 0; i < mapped; ++i) hipMemUnmap(static_cast<char*>(va) + (size_t)i * chunk, chunk);
+    for (int i = 0; i < n; ++i)
+      if (handles[i]) { hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)handles[i]); handles[i] = 0; }
+    hipMemAddressFree(va, total);
+    return (int)e;
+  }
+  *va_out = va;
+  return 0;
+}
+
+// Unmap + release ``n`` chunks mapped at ``va`` and free the VA range (own or imported).
+extern "C" int mp4x_vmm_free(void* va, size_t chunk, int n, const uint64_t* handles) {
+  return teardown(va, chunk, n, handles, chunk * (size_t)n);
+}

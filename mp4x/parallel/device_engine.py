@@ -626,6 +626,20 @@ class DeviceEngine:
         if self._ipc_obj is not None:
             self._ipc_obj.deregister(self._flat(t))
 
+    def mem_alloc(self, n: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """Collective: an ``n``-element tensor mapped into every peer at any size (see
+        ``IpcAllreduce.mem_alloc``), or None on every rank when there is no IPC mesh (the
+        caller then allocates a plain tensor: the staged kernels / RCCL serve it)."""
+        if not self._zc or self.p < 2 or self.device.type != "cuda" or self.ipc() is None:
+            return None
+        es = torch.empty((), dtype=dtype).element_size()
+        return self._ipc_obj.mem_alloc(n * es, dtype)
+
+    def mem_free(self, t: torch.Tensor) -> None:
+        if self._ipc_obj is not None and self._ipc_obj._find(t)[0] is not None \
+                and self._ipc_obj._find(t)[0].vmm:
+            self._ipc_obj.mem_free(t)
+
     def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
         """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
         if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and self.ipc() is None:

@@ -90,6 +90,21 @@ def _set_spin(lib) -> None:
         _SPIN_SET[0] = True
 
 
+class _Reg:
+    """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
+    every rank's push scratch (or None), and what this rank must release at deregistration."""
+    __slots__ = ("peers", "scratch", "keep", "opened", "peer_keys", "scratch_alloc", "vmm")
+
+    def __init__(self, keep=None):
+        self.peers: List[int] = []
+        self.scratch = None
+        self.keep = keep                 # the registered tensor: its memory stays allocated
+        self.opened: List[c_void_p] = []  # scratch mappings of the peers
+        self.peer_keys: list = []        # refcounted entries of IpcAllreduce._peer_bases
+        self.scratch_alloc = None        # own push scratch (hipExtMallocWithFlags)
+        self.vmm: list = []              # memAlloc: own + imported VmmRegions
+
+
 class IpcAllreduce:
     def __init__(self, comm, nbytes: Optional[int] = None, tag: str = "default"):
         self.comm = comm
@@ -190,9 +205,7 @@ class IpcAllreduce:
         # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> (peer pointers,
         # every rank's push scratch or None)
         self._regs = {}
-        self._scratch_allocs: List[c_void_p] = []
-        self._scratch_ptr = 0
-        self._peer_bases = {}       # (rank, handle bytes) -> mapped base (one open per allocation)
+        self._peer_bases = {}       # (rank, handle bytes) -> [mapped base, registrations using it]
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -216,6 +229,11 @@ class IpcAllreduce:
         code = self.host_error()
         if code:
             ctypes.c_uint32.from_address(self._herr.value).value = 0
+            if code == 4:
+                raise Mp4jException(f"rank {self.rank}: IPC protocol mismatch — a peer ran the staged form of a "
+                                    f"collective while this rank ran the zero-copy form (or the reverse): buffer "
+                                    f"registrations differ across ranks (e.g. a rank-local deregister); the result "
+                                    f"of that call is invalid")
             where = {1: "start", 2: "mid", 3: "end"}.get(code, str(code))
             raise Mp4jException(f"rank {self.rank}: an earlier IPC collective timed out at its {where} barrier "
                                 f"(a peer skipped, failed or died in that call); its result is invalid")
@@ -344,7 +362,11 @@ class IpcAllreduce:
     # against a zero-copy peer fails that call at once (epoch tag) instead of mixing buffers.
     def register(self, t: torch.Tensor) -> bool:
         """Collective.  Map ``t`` (contiguous, 16-byte aligned, 16-byte multiple) into every peer.
-        Returns True when every rank registered it (False on every rank otherwise)."""
+        Returns True when every rank registered it (False on every rank otherwise).
+
+        The registration holds a reference to ``t`` until :meth:`deregister`: its memory can
+        never go back to the caching allocator (and be handed to another tensor at the same
+        address) while peers still hold mappings of it."""
         key = (t.data_ptr(), t.numel() * t.element_size())
         if key in self._regs:
             ok_local = 1
@@ -353,110 +375,253 @@ class IpcAllreduce:
         hs = self.lib.mp4x_ipc_handle_size()
         blob = None
         err = None
+        scr_alloc = None
         try:
             if not t.is_cuda or not t.is_contiguous() or t.data_ptr() % 16 or key[1] % 16 or key[1] == 0:
                 raise Mp4jException("register needs a contiguous, 16-byte aligned device tensor of 16-byte multiple size")
             base, size = c_void_p(), c_size_t()
             check(self.lib.mp4x_mem_range(c_void_p(t.data_ptr()), ctypes.byref(base), ctypes.byref(size)), "mem_range")
             if size.value > IPC_OPEN_MAX:
-                raise Mp4jException(f"allocation of {size.value} bytes is above the IPC open limit ({IPC_OPEN_MAX})")
+                raise Mp4jException(f"allocation of {size.value} bytes is above the IPC open limit ({IPC_OPEN_MAX}); "
+                                    f"allocate it with memAlloc")
             h = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(base, h), "ipc_get_handle(registered)")
             scr_h = None
             if PUSH_ON and not ok_local:
-                scr_h = self._alloc_scratch(key[1], hs)
+                scr_alloc, scr_h = self._alloc_scratch(key[1], hs)
             blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local, scr_h)
         except Exception as e:   # noqa: BLE001 — travels in the allgather: every rank decides together
             err = str(e)
         allb = self.comm.server.call("allgather_obj", self.rank, (blob, err))
         errs = [(i, e) for i, (_, e) in enumerate(allb) if e]
         if errs or len({b[2] for b, _ in allb}) != 1:
+            self._free_scratch(scr_alloc)
             return False
         if all(b[3] for b, _ in allb):
             return True                               # already registered everywhere
-        ptrs, err = [], None
+        reg = _Reg(keep=t)
+        err = None
         push = all(b[4] is not None for b, _ in allb)      # every rank has a receive scratch
+        if not push:
+            self._free_scratch(scr_alloc)
+            scr_alloc = None
         scr = []
         try:
             for r, (b, _) in enumerate(allb):
                 if r == self.rank:
-                    ptrs.append(t.data_ptr())
+                    reg.peers.append(t.data_ptr())
                     if push:
-                        scr.append(self._scratch_ptr)
+                        scr.append(scr_alloc.value)
                     continue
                 hk = (r, bytes(b[0]))
-                if hk not in self._peer_bases:
-                    hb = ctypes.create_string_buffer(bytes(b[0]), hs)
-                    ptr = c_void_p()
-                    check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(registered, rank {r})")
-                    self._opened.append(ptr)
-                    self._peer_bases[hk] = ptr.value
-                ptrs.append(self._peer_bases[hk] + int(b[1]))
+                reg.peers.append(self._open_peer_base(hk, hs) + int(b[1]))
+                reg.peer_keys.append(hk)
                 if push:
                     q = c_void_p()
                     check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(b[4]), hs),
                                                         ctypes.byref(q)), f"ipc_open_handle(scratch, rank {r})")
-                    self._opened.append(q)
+                    reg.opened.append(q)
                     scr.append(q.value)
         except Exception as e:   # noqa: BLE001
             err = str(e)
+        reg.scratch = scr if push else None
+        reg.scratch_alloc = scr_alloc
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
+            self._release(reg)
             return False
-        self._regs[key] = (ptrs, scr if push else None)
+        self._regs[key] = reg
         return True
+
+    def _open_peer_base(self, hk, hs: int) -> int:
+        """Mapped base of peer allocation ``hk`` = (rank, handle bytes): one open per allocation,
+        reference-counted over the registrations that use it."""
+        ent = self._peer_bases.get(hk)
+        if ent is None:
+            hb = ctypes.create_string_buffer(hk[1], hs)
+            ptr = c_void_p()
+            check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(registered, rank {hk[0]})")
+            ent = self._peer_bases[hk] = [ptr, 0]
+        ent[1] += 1
+        return ent[0].value
 
     def _alloc_scratch(self, nbytes: int, hs: int):
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
         slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
-        its IPC handle, or None (then the registration simply has no push form)."""
+        (allocation, IPC handle), or (None, None): the registration then has no push form."""
         chunk = -(-(nbytes // 16) // self.p)
         size = max(16, (self.p - 1) * chunk * 16)
         ptr = c_void_p()
         try:
             if size > IPC_OPEN_MAX:
-                return None
+                return None, None
             check(self.lib.mp4x_ipc_alloc(size, ctypes.byref(ptr)), "ipc_alloc(scratch)")
             h = ctypes.create_string_buffer(hs)
             check(self.lib.mp4x_ipc_get_handle(ptr, h), "ipc_get_handle(scratch)")
         except Exception:   # noqa: BLE001
             if ptr:
                 self.lib.mp4x_ipc_free(ptr)
-            return None
-        self._scratch_allocs.append(ptr)
-        self._scratch_ptr = ptr.value
-        return h.raw
+            return None, None
+        return ptr, h.raw
+
+    def _free_scratch(self, ptr) -> None:
+        if ptr:
+            self.lib.mp4x_ipc_free(ptr)
+
+    def _release(self, reg: "_Reg") -> None:
+        """Close every mapping ``reg`` opened and free its scratch (after the caller's stream
+        work on them is done)."""
+        for q in reg.opened:
+            self.lib.mp4x_ipc_close_handle(q)
+        reg.opened = []
+        for hk in reg.peer_keys:
+            ent = self._peer_bases.get(hk)
+            if ent is not None:
+                ent[1] -= 1
+                if ent[1] <= 0:
+                    self.lib.mp4x_ipc_close_handle(ent[0])
+                    del self._peer_bases[hk]
+        reg.peer_keys = []
+        self._free_scratch(reg.scratch_alloc)
+        reg.scratch_alloc = None
+        for region in reversed(reg.vmm):     # the peers' imported views first, own memory last
+            region.free()
+        reg.vmm = []
+        reg.keep = None
 
     def deregister(self, t: torch.Tensor) -> None:
-        """Forget ``t`` (local; the peer mappings of its allocation stay open until close)."""
-        self._regs.pop((t.data_ptr(), t.numel() * t.element_size()), None)
+        """Forget ``t`` and release what its registration holds on THIS rank: the mappings of
+        the peers' allocations, the push scratch, the reference to ``t``.  Every peer
+        deregisters its tensor at the same point (the registration contract), so no peer
+        kernel uses them afterwards; the local stream is drained first."""
+        reg = self._regs.pop((t.data_ptr(), t.numel() * t.element_size()), None)
+        if reg is None:
+            return
+        if reg.vmm:
+            # memAlloc'ed: its memory is freed by mem_free (collective), not here
+            self._regs[(t.data_ptr(), t.numel() * t.element_size())] = reg
+            return
+        torch.cuda.synchronize(self.device)
+        self._release(reg)
 
-    def registered(self, view: torch.Tensor):
-        """Peer pointers of ``view`` when it lies inside a registered tensor, else None."""
+    def _find(self, view: torch.Tensor):
+        """(registration, byte offset of ``view`` in it) or (None, 0)."""
         if not self._regs:
-            return None
+            return None, 0
         a = view.data_ptr()
         n = view.numel() * view.element_size()
         hit = self._regs.get((a, n))            # the whole registered tensor: O(1)
         if hit is not None:
-            return hit[0]
-        for (ptr, nb), (peers, _) in self._regs.items():
+            return hit, 0
+        for (ptr, nb), reg in self._regs.items():
             if ptr <= a and a + n <= ptr + nb:
-                d = a - ptr
-                return [q + d for q in peers]
-        return None
+                return reg, a - ptr
+        return None, 0
+
+    def registered(self, view: torch.Tensor):
+        """Peer pointers of ``view`` when it lies inside a registered tensor, else None."""
+        reg, d = self._find(view)
+        if reg is None:
+            return None
+        return reg.peers if d == 0 else [q + d for q in reg.peers]
 
     def scratch_of(self, view: torch.Tensor):
         """Every rank's push scratch for ``view``'s registered tensor, or None (no push form)."""
-        a = view.data_ptr()
-        n = view.numel() * view.element_size()
-        hit = self._regs.get((a, n))
-        if hit is not None:
-            return hit[1]
-        for (ptr, nb), (_, scr) in self._regs.items():
-            if ptr <= a and a + n <= ptr + nb:
-                return scr
-        return None
+        reg, _ = self._find(view)
+        return None if reg is None else reg.scratch
+
+    # ---------------------------------------------------------------- memAlloc (any size)
+    def mem_alloc(self, nbytes: int, dtype: torch.dtype) -> torch.Tensor:
+        """Collective (``ProcessCommSlave.memAlloc``): a ``nbytes`` device tensor that is mapped
+        into every peer from the start — registered for the zero-copy kernels at ANY size, as
+        one contiguous range per peer (parallel/vmm.py, csrc/runtime/vmm.hip).  Also allocates
+        the push scratch the same way.  Raises on every rank when any rank failed."""
+        from . import vmm
+        nb16 = -(-int(nbytes) // 16) * 16
+        own = scr = None
+        err = None
+        plan = None
+        try:
+            g = ctypes.c_size_t()
+            check(self.lib.mp4x_vmm_granularity(ctypes.byref(g)), "vmm_granularity")
+            chunk, n = vmm.chunk_plan(nb16, g.value)
+            own = vmm.VmmRegion.create(self.lib, chunk, n)
+            sbytes = (self.p - 1) * (-(-(nb16 // 16) // self.p)) * 16
+            schunk, sn = vmm.chunk_plan(max(16, sbytes), g.value)
+            scr = vmm.VmmRegion.create(self.lib, schunk, sn) if PUSH_ON else None
+            plan = (chunk, n, schunk if scr else 0, sn if scr else 0)
+        except Exception as e:   # noqa: BLE001 — agreed below
+            err = f"{type(e).__name__}: {e}"
+        plans = self.comm.server.call("allgather_obj", self.rank, (plan, err))
+        bad = [(i, e) for i, (_, e) in enumerate(plans) if e]
+        if bad:
+            for region in (own, scr):
+                if region is not None:
+                    region.free()
+            raise Mp4jException(f"memAlloc({nbytes}) failed on ranks {bad}")
+        push = all(pl[2] for pl, _ in plans)
+        mine = own.fds + (scr.fds if (push and scr) else [])
+        try:
+            got = vmm.exchange_fds(self.comm.server, self.rank, self.p, mine)
+        except Exception:
+            for region in (own, scr):
+                if region is not None:
+                    region.free()
+            raise
+        own.close_fds()
+        if scr is not None:
+            scr.close_fds()
+        reg = _Reg(keep=None)
+        reg.vmm = [own] + ([scr] if scr is not None else [])
+        scratch = []
+        err = None
+        try:
+            for r in range(self.p):
+                if r == self.rank:
+                    reg.peers.append(own.va)
+                    scratch.append(scr.va if push else 0)
+                    continue
+                chunk, n, schunk, sn = plans[r][0]
+                fds = got[r]
+                try:
+                    pr = vmm.VmmRegion.import_fds(self.lib, fds[:n], chunk)
+                    reg.vmm.append(pr)
+                    reg.peers.append(pr.va)
+                    if push:
+                        ps = vmm.VmmRegion.import_fds(self.lib, fds[n:n + sn], schunk)
+                        reg.vmm.append(ps)
+                        scratch.append(ps.va)
+                finally:
+                    for fd in fds:
+                        os.close(fd)
+        except Exception as e:   # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        oks = self.comm.server.call("allgather_obj", self.rank, err)
+        if any(oks):
+            self.comm.server.call("barrier", self.rank)
+            self._release(reg)
+            raise Mp4jException(f"memAlloc({nbytes}) peer mapping failed on ranks "
+                                f"{[(i, o) for i, o in enumerate(oks) if o]}")
+        reg.scratch = scratch if push else None
+        t = vmm.tensor_at(own.va, nb16, torch.uint8, torch.device("cuda", self.device))
+        self._regs[(own.va, nb16)] = reg
+        es = torch.empty((), dtype=dtype).element_size()
+        return t[:nbytes // es * es].view(dtype)
+
+    def mem_free(self, t: torch.Tensor) -> None:
+        """Collective: release a :meth:`mem_alloc` tensor on every rank (its peers' mappings
+        first, after every rank's stream drained)."""
+        key = None
+        for k, reg in self._regs.items():
+            if reg.vmm and k[0] == t.data_ptr():
+                key = k
+                break
+        if key is None:
+            raise Mp4jException("memFree: not a memAlloc tensor of this communicator")
+        torch.cuda.synchronize(self.device)
+        self.comm.server.call("barrier", self.rank)     # no peer kernel still reads or writes it
+        reg = self._regs.pop(key)
+        self._release(reg)
 
     def allreduce_push(self, view: torch.Tensor, op, peers, scratch, scale: float = 1.0) -> torch.Tensor:
         """In place, on registered tensors, with every xGMI transfer a posted WRITE (see
@@ -1114,6 +1279,9 @@ class IpcAllreduce:
             self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
-        for ptr in getattr(self, "_scratch_allocs", []):
-            self.lib.mp4x_ipc_free(ptr)
-        self._scratch_allocs = []
+        for reg in list(getattr(self, "_regs", {}).values()):
+            try:
+                self._release(reg)
+            except Exception:   # noqa: BLE001 — best effort at teardown
+                pass
+        self._regs = {}

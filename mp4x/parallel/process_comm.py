@@ -268,6 +268,32 @@ class ProcessCommSlave:
     register_buffer = registerBuffer
     deregister_buffer = deregisterBuffer
 
+    def memAlloc(self, n: int, dtype=None, device=None):
+        """Collective (extension, like ``ncclMemAlloc``): an ``n``-element device tensor that is
+        registered with every peer from the start, at ANY size — also above the 2 GiB at which
+        a caching-allocator tensor cannot be mapped (parallel/vmm.py).  Allreduce / reduce-
+        scatter / all-gather on it (or on [from, to) views) run the zero-copy xGMI kernels: the
+        in-place 8 GB arrays of the reference (README.md:313) with no staging.  Contents are
+        uninitialised.  Free with :meth:`memFree` (collective).  Without a multi-rank GPU mesh it
+        returns a plain tensor (``torch.empty``)."""
+        import torch
+        dtype = dtype or torch.float32
+        want_dev = device is None or str(device).startswith("cuda")
+        if self.slaveNum > 1 and want_dev and torch.cuda.is_available():
+            t = self.device.mem_alloc(int(n), dtype)
+            if t is not None:
+                return t
+        dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+        return torch.empty(int(n), dtype=dtype, device=dev)
+
+    def memFree(self, tensor) -> None:
+        """Collective: release a :meth:`memAlloc` tensor (no-op for a plain tensor)."""
+        if self._device_engine is not None:
+            self._device_engine.mem_free(tensor)
+
+    mem_alloc = memAlloc
+    mem_free = memFree
+
     def _shm_engine(self, buf, operand: Operand, operator, nelems: int):
         """The shared-memory engine when this call qualifies (decision identical on every rank)."""
         if os.environ.get("MP4X_SHM", "1") != "1" or self.slaveNum == 1 or not operand.is_primitive \
@@ -707,13 +733,23 @@ class ProcessCommSlave:
         return self.device.all_to_all_v(sendData, list(sendCounts), recvData)
 
     # ================================================================ allreduce
-    def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, out=None):
+    def allreduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, out=None, scale: float = 1.0):
         """reduce-scatter + allgather with the last rank taking the remainder (reference :1733-1763).
 
         ``out`` (extension): out-of-place form — ``out[from:to]`` receives the result and
         ``arrData`` is left untouched (with one rank this is a plain copy).
+        ``scale`` (extension, float data): the result is multiplied by it — e.g. ``1/p`` for a
+        gradient average; on the device it is fused into the collective's final write.
         """
         self._tick("allreduceArray")
+        if scale != 1.0:
+            if _is_device_tensor(arrData) and self.slaveNum > 1:
+                CommUtils.isFromToLegal(frm, to)
+                return self.device.allreduce(arrData, frm, to, operator, operand, out=out, scale=scale)
+            res = self.allreduceArray(arrData, operand, operator, frm, to, out=out)
+            tgt = res.view(-1)[frm:to] if _is_torch(res) else res[frm:to]
+            tgt *= scale
+            return res
         if out is not None and self.slaveNum > 1 and _is_device_tensor(out) and _is_device_tensor(arrData):
             # the device engine writes the result straight into ``out`` (no copy-then-in-place)
             CommUtils.isFromToLegal(frm, to)

@@ -1,0 +1,203 @@
+"""Library-owned, peer-mappable device allocations of any size (``ProcessCommSlave.memAlloc``).
+
+The ncclMemAlloc analogue of mp4x (native side: csrc/runtime/vmm.hip).  A buffer is a run of
+physical chunks (``hipMemCreate``, ``MP4X_VMM_CHUNK`` bytes each, default 512 MiB — far below
+the 2 GiB size at which an IPC open of one allocation hangs on this ROCm,
+profiles/r2/ipc_open_probe.jsonl) mapped back to back into one reserved VA range.  Every chunk
+is exported as a POSIX fd (dmabuf); the fds travel to the same-node peers over an abstract
+unix socket (``SCM_RIGHTS``, :func:`exchange_fds`) and each peer maps them back to back into
+its own VA range.  The result: a contiguous tensor of any size that every peer sees as one
+contiguous range too, so the zero-copy IPC kernels (csrc/runtime/ipc.hip) run on 4 GB / 8 GB
+tensors with no staging — the reference's in-place 8 GB ``allreduceArray``
+(/root/reference/README.md:313, ProcessCommSlave.java:1733-1763).
+
+Only the control-plane ``allgather_obj`` is used for rendezvous (socket names, chunk counts,
+errors): a failure on any rank is agreed and raised on every rank.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import socket
+import threading
+import uuid
+from typing import Dict, List, Optional
+
+import torch
+
+from ..exceptions import Mp4jException
+from ..ops import native
+from ..ops.native import check, c_int, c_size_t, c_void_p
+
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_INTP = ctypes.POINTER(ctypes.c_int)
+
+native.register_signatures({
+    "mp4x_vmm_granularity": (c_int, [ctypes.POINTER(c_size_t)]),
+    "mp4x_vmm_create": (c_int, [c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P, _INTP]),
+    "mp4x_vmm_import": (c_int, [_INTP, c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P]),
+    "mp4x_vmm_free": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
+})
+
+DEFAULT_CHUNK = 512 << 20
+_FDS_PER_MSG = 200          # SCM_RIGHTS carries at most 253 fds per message (SCM_MAX_FD)
+
+
+def chunk_plan(nbytes: int, gran: int, chunk: Optional[int] = None) -> (int, int):
+    """(chunk bytes, chunk count) for a ``nbytes`` buffer: chunks are granularity multiples of
+    at most ``chunk`` (``MP4X_VMM_CHUNK``) bytes; a small buffer is one chunk of its rounded
+    size.  Pure function (unit-tested on CPU)."""
+    if nbytes <= 0:
+        raise Mp4jException("memAlloc needs a positive size")
+    gran = max(1, int(gran))
+    cap = int(chunk or os.environ.get("MP4X_VMM_CHUNK", DEFAULT_CHUNK))
+    cap = max(gran, cap // gran * gran)
+    need = -(-nbytes // gran) * gran
+    if need <= cap:
+        return need, 1
+    return cap, -(-need // cap)
+
+
+class VmmRegion:
+    """``n`` chunks of ``chunk`` bytes mapped back to back at ``va`` in THIS process — either
+    this rank's own allocation (``fds`` exported) or an imported peer allocation."""
+
+    def __init__(self, lib, va: int, chunk: int, handles, fds: Optional[List[int]] = None):
+        self.lib = lib
+        self.va = va
+        self.chunk = chunk
+        self.n = len(handles)
+        self._handles = (ctypes.c_uint64 * self.n)(*handles)
+        self.fds = list(fds or [])
+
+    @property
+    def nbytes(self) -> int:
+        return self.chunk * self.n
+
+    @classmethod
+    def create(cls, lib, chunk: int, n: int, export: bool = True) -> "VmmRegion":
+        va = c_void_p()
+        handles = (ctypes.c_uint64 * n)()
+        fds = (ctypes.c_int * n)(*([-1] * n))
+        check(lib.mp4x_vmm_create(chunk, n, ctypes.byref(va), handles, fds if export else None), "vmm_create")
+        return cls(lib, va.value, chunk, list(handles), list(fds) if export else None)
+
+    @classmethod
+    def import_fds(cls, lib, fds: List[int], chunk: int) -> "VmmRegion":
+        n = len(fds)
+        va = c_void_p()
+        handles = (ctypes.c_uint64 * n)()
+        check(lib.mp4x_vmm_import((ctypes.c_int * n)(*fds), chunk, n, ctypes.byref(va), handles), "vmm_import")
+        return cls(lib, va.value, chunk, list(handles))
+
+    def close_fds(self) -> None:
+        for fd in self.fds:
+            if fd >= 0:
+                try:
+                    os.close(fd)
+                except OSError:
+                    pass
+        self.fds = []
+
+    def free(self) -> None:
+        self.close_fds()
+        if self.va:
+            check(self.lib.mp4x_vmm_free(c_void_p(self.va), self.chunk, self.n, self._handles), "vmm_free")
+            self.va = 0
+
+
+class _CudaArray:
+    """``__cuda_array_interface__`` over a raw device range (bytes); ``torch.as_tensor`` keeps
+    this object alive for the tensor's lifetime."""
+
+    def __init__(self, ptr: int, nbytes: int, owner=None):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+        self.owner = owner
+
+
+def tensor_at(ptr: int, nbytes: int, dtype: torch.dtype, device: torch.device, owner=None) -> torch.Tensor:
+    """A 1-D ``dtype`` tensor viewing ``nbytes`` of device memory at ``ptr`` (no copy)."""
+    es = torch.empty((), dtype=dtype).element_size()
+    if nbytes % es:
+        raise Mp4jException(f"{nbytes} bytes is not a whole number of {dtype} elements")
+    with torch.cuda.device(device):
+        raw = torch.as_tensor(_CudaArray(ptr, nbytes, owner), device=device)
+    return raw.view(dtype)
+
+
+def exchange_fds(server, rank: int, p: int, mine: List[int], timeout: float = 120.0) -> Dict[int, List[int]]:
+    """Collective: every rank gets every peer's fd list (``SCM_RIGHTS`` duplicates, owned by the
+    caller) over abstract unix sockets; only the socket names go through the control plane.
+
+    Every rank serves its fds to each connecting peer from a thread while it connects to every
+    peer itself, so no ordering between ranks can deadlock.  Same node only (abstract socket
+    namespace of one network namespace)."""
+    name = f"\0mp4x-fd-{uuid.uuid4().hex}"
+    srv = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+    err = None
+    try:
+        srv.bind(name)
+        srv.listen(max(1, p))
+        srv.settimeout(timeout)
+    except OSError as e:
+        err = f"{type(e).__name__}: {e}"
+    names = server.call("allgather_obj", rank, (name, len(mine), err))
+    bad = [(i, e) for i, (_, _, e) in enumerate(names) if e]
+    if bad:
+        srv.close()
+        raise Mp4jException(f"fd exchange socket setup failed on ranks {bad}")
+    serve_err: List[str] = []
+
+    def serve():
+        try:
+            for _ in range(p - 1):
+                conn, _ = srv.accept()
+                with conn:
+                    conn.settimeout(timeout)
+                    conn.recv(4)                      # the peer's hello
+                    for i in range(0, max(1, len(mine)), _FDS_PER_MSG):
+                        part = mine[i:i + _FDS_PER_MSG]
+                        socket.send_fds(conn, [len(part).to_bytes(4, "little")], part)
+                    conn.recv(1)                      # the peer holds the fds: done
+        except Exception as e:   # noqa: BLE001
+            serve_err.append(f"{type(e).__name__}: {e}")
+
+    th = threading.Thread(target=serve, daemon=True, name="mp4x-fd-serve")
+    th.start()
+    got: Dict[int, List[int]] = {}
+    local_err = None
+    try:
+        for j in range(p):
+            if j == rank:
+                continue
+            c = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+            c.settimeout(timeout)
+            with c:
+                c.connect(names[j][0])
+                c.sendall(rank.to_bytes(4, "little"))
+                fds: List[int] = []
+                want = names[j][1]
+                for _ in range(max(1, -(-want // _FDS_PER_MSG))):   # the messages serve() sends
+                    msg, part, _, _ = socket.recv_fds(c, 4, _FDS_PER_MSG)
+                    if not msg:
+                        raise Mp4jException(f"fd exchange: rank {j} closed early")
+                    fds += part
+                if len(fds) != want:
+                    raise Mp4jException(f"fd exchange: {len(fds)} fds from rank {j}, expected {want}")
+                c.sendall(b"k")
+                got[j] = fds
+    except Exception as e:   # noqa: BLE001
+        local_err = f"{type(e).__name__}: {e}"
+    th.join(timeout)
+    srv.close()
+    if serve_err and local_err is None:
+        local_err = serve_err[0]
+    errs = server.call("allgather_obj", rank, local_err)
+    failed = [(i, e) for i, e in enumerate(errs) if e]
+    if failed:
+        for fl in got.values():
+            for fd in fl:
+                os.close(fd)
+        raise Mp4jException(f"fd exchange failed on ranks {failed}")
+    return got

@@ -1,9 +1,15 @@
-"""Spawned multi-rank harness for GPU tests: a CommMaster + p fresh (spawned) rank processes
-sharing cuda:0.  ``fn(comm, *args)`` must be a module-level function (it is pickled by name);
-its return value comes back per rank.  ``threads`` > 0 gives each rank a ThreadCommSlave.
+"""Spawned multi-rank harness for GPU tests: a CommMaster + p fresh (spawned) rank processes.
+``fn(comm, *args)`` must be a module-level function (it is pickled by name); its return value
+comes back per rank.  ``threads`` > 0 gives each rank a ThreadCommSlave.
 
-Device collectives other than the IPC kernels go through gloo (``MP4X_DEVICE_BACKEND=gloo``):
-RCCL refuses two ranks on one GPU, the IPC kernels run for real.
+Two device plans (:func:`device_plan`):
+
+* ``shared`` — every rank on cuda:0 (the 1-GPU box).  Device collectives other than the IPC
+  kernels go through gloo (``MP4X_DEVICE_BACKEND=gloo``): RCCL refuses two ranks on one GPU;
+  the IPC kernels run for real (same-device "remote" reads).
+* ``multi`` — rank r on cuda:r with the nccl (= RCCL) backend, one GPU per rank: RCCL at p >= 2,
+  cross-device IPC mappings over xGMI, the cross-GPU coherence the zero-copy protocol relies on.
+  Chosen by ``mode="multi"`` (or ``"auto"`` when ``torch.cuda.device_count() >= p``).
 """
 import multiprocessing as mp
 import os
@@ -11,7 +17,24 @@ import tempfile
 import traceback
 
 
-def _worker(fn, port, args, env, threads, q, dump_after):
+def device_plan(p, ndev, mode="shared"):
+    """(plan, env) for ``p`` ranks on a box with ``ndev`` GPUs.  ``mode``: shared | multi | auto."""
+    if mode not in ("shared", "multi", "auto"):
+        raise ValueError(mode)
+    multi = mode == "multi" or (mode == "auto" and ndev >= p)
+    if multi and ndev < p:
+        raise ValueError(f"multi-GPU plan needs {p} GPUs, the box has {ndev}")
+    if multi:
+        return "multi", {"MP4X_DEVICE_BACKEND": "nccl", "MP4X_WATCHDOG": "0"}
+    return "shared", {"MP4X_DEVICE_BACKEND": "gloo", "MP4X_DEVICE_INDEX": "0", "MP4X_WATCHDOG": "0"}
+
+
+def rank_device(plan, rank):
+    """The GPU ordinal rank ``rank`` uses under ``plan``."""
+    return rank if plan == "multi" else 0
+
+
+def _worker(fn, port, args, env, threads, q, dump_after, plan):
     try:
         import faulthandler
         import sys
@@ -22,14 +45,19 @@ def _worker(fn, port, args, env, threads, q, dump_after):
             logging.basicConfig(level=logging.INFO, stream=sys.stderr,
                                 format="%(asctime)s %(name)s %(levelname)s %(message)s")
         import torch
-        torch.cuda.set_device(0)
+        if plan == "shared":
+            torch.cuda.set_device(0)
         from mp4x import ProcessCommSlave, ThreadCommSlave
         if threads:
             comm = ThreadCommSlave("t", threads, "127.0.0.1", port, heartbeat=False)
-            rank = comm.getRank()
         else:
             comm = ProcessCommSlave("t", "127.0.0.1", port, heartbeat=False)
-            rank = comm.getRank()
+        rank = comm.getRank()
+        if plan == "multi":
+            # the rank is known only after the rendezvous: bind this process to cuda:rank before
+            # anything touches the device (the device engine then picks it up too)
+            os.environ["MP4X_DEVICE_INDEX"] = str(rank_device(plan, rank))
+            torch.cuda.set_device(rank_device(plan, rank))
         res = fn(comm, *args)
         comm.close(0)
         q.put((rank, "ok", res))
@@ -37,14 +65,19 @@ def _worker(fn, port, args, env, threads, q, dump_after):
         q.put((-1, "err", traceback.format_exc()))
 
 
-def run_spawn(p, fn, args=(), env=None, timeout=240, threads=0):
+def run_spawn(p, fn, args=(), env=None, timeout=240, threads=0, mode="shared"):
     from mp4x import CommMaster
-    e = {"MP4X_DEVICE_BACKEND": "gloo", "MP4X_DEVICE_INDEX": "0", "MP4X_WATCHDOG": "0"}
+    ndev = 1
+    if mode != "shared":
+        import torch
+        ndev = torch.cuda.device_count()      # does not initialise the GPU in this process
+    plan, e = device_plan(p, ndev, mode)
     e.update(env or {})
     m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(fn, m.port, args, e, threads, q, min(100, max(10, timeout - 60))))
+    procs = [ctx.Process(target=_worker,
+                         args=(fn, m.port, args, e, threads, q, min(100, max(10, timeout - 60)), plan))
              for _ in range(p)]
     for pr in procs:
         pr.start()

@@ -19,14 +19,19 @@ def _free_port():
     return port
 
 
-def test_torchrun_bench_dry_run_all_ranks_exit_clean(tmp_path):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+def _run(tmp_path, nproc=4, extra_env=None, steps=3):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--cpu", "--gpus", "4", "--steps", "3", "--warmup", "1", "--bytes", "4000000"]
+           "--cpu", "--gpus", str(nproc), "--steps", str(steps), "--warmup", "1", "--bytes", "4000000"]
     r = subprocess.run(cmd, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300,
-                       env=dict(os.environ, PYTHONPATH=ROOT))
-    assert r.returncode == 0, r.stdout[-3000:]
+                       env=dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {})))
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
+    return r, lines
+
+
+def test_torchrun_bench_dry_run_all_ranks_exit_clean(tmp_path):
+    r, lines = _run(tmp_path)
+    assert r.returncode == 0, r.stdout[-3000:]
     assert len(lines) == 1
     rec = lines[0]
     assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["value"] > 0
@@ -35,3 +40,23 @@ def test_torchrun_bench_dry_run_all_ranks_exit_clean(tmp_path):
     assert abs(rec["aggregate_busbw_gbps"] - 4 * rec["busbw_gbps_per_rank"]) < 1e-2
     assert abs(rec["busbw_gbps_per_rank"] - rec["algbw_gbps"] * 2 * 3 / 4) < 1e-2
     assert "e+" not in rec["config"]["model"]
+    # self-verification of the timed call (exact pattern vs the fp64 answer, MAX over ranks)
+    assert rec["verified"] is True and rec["max_abs_err"] == 0.0, rec
+    # equal-method RCCL baseline keys (None without RCCL: gloo dry run)
+    for k in ("rccl_busbw_gbps", "rccl_p50_ms", "rccl_baseline"):
+        assert k in rec
+    assert rec["config"]["scale"] == 0.25 and rec["config"]["autotune_iters"] >= 5
+
+
+def test_bench_values_stay_bounded_over_many_steps(tmp_path):
+    # scale=1/p: 60 SUM steps at p=2 would otherwise multiply the data by 2^60
+    r, lines = _run(tmp_path, nproc=2, steps=60)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert lines[0]["verified"] is True
+
+
+def test_bench_wrong_result_fails_the_run(tmp_path):
+    # a wrong element on one rank (test hook standing in for a broken kernel): verified false, rc != 0
+    r, lines = _run(tmp_path, nproc=2, extra_env={"MP4X_BENCH_CORRUPT": "1"})
+    assert r.returncode != 0, r.stdout[-3000:]
+    assert len(lines) == 1 and lines[0]["verified"] is False and lines[0]["max_abs_err"] >= 1.0, lines

@@ -1,0 +1,30 @@
+"""The GPU test harness's device assignment (tests/spawn_ranks.py), checked without a GPU."""
+import pytest
+
+from spawn_ranks import device_plan, rank_device
+
+
+def test_shared_plan_is_the_default():
+    plan, env = device_plan(4, 8)
+    assert plan == "shared"
+    assert env["MP4X_DEVICE_BACKEND"] == "gloo" and env["MP4X_DEVICE_INDEX"] == "0"
+    assert [rank_device(plan, r) for r in range(4)] == [0, 0, 0, 0]
+
+
+@pytest.mark.parametrize("p,ndev,plan", [(2, 8, "multi"), (8, 8, "multi"), (8, 4, "shared"), (2, 1, "shared"),
+                                         (4, 0, "shared")])
+def test_auto_plan(p, ndev, plan):
+    got, env = device_plan(p, ndev, "auto")
+    assert got == plan
+    if plan == "multi":
+        assert env["MP4X_DEVICE_BACKEND"] == "nccl" and "MP4X_DEVICE_INDEX" not in env
+        assert [rank_device(got, r) for r in range(p)] == list(range(p))
+    else:
+        assert env["MP4X_DEVICE_BACKEND"] == "gloo"
+
+
+def test_multi_plan_needs_enough_gpus():
+    with pytest.raises(ValueError):
+        device_plan(4, 2, "multi")
+    with pytest.raises(ValueError):
+        device_plan(2, 2, "bogus")

@@ -1,0 +1,98 @@
+"""memAlloc: library-owned tensors mapped into every peer at ANY size (p processes on one GPU).
+
+* a memAlloc tensor above 2 GiB (the size at which an IPC open of a caching-allocator
+  allocation hangs, so ``registerBuffer`` refuses it) runs the zero-copy two-shot exactly,
+  twice in a row (the second call reduces the first call's result in place);
+* several physical chunks per tensor (``MP4X_VMM_CHUNK`` small) still give one contiguous
+  tensor on every rank and one contiguous peer view;
+* ZeRO-style reduce-scatter + all-gather of a bf16 memAlloc tensor take the zero-copy RS/AG
+  kernels (no staging), exact;
+* memFree releases it (a second memAlloc after the free works).
+"""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from spawn_ranks import run_spawn  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _alloc_allreduce_fn(comm, n, reps):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    t = comm.memAlloc(n, torch.float32)
+    i = torch.arange(n, device="cuda", dtype=torch.int32) % 13
+    t.copy_(i + r)
+    exp = (i * p + p * (p - 1) // 2).float()
+    before = dict(eng.stats)
+    bad = []
+    for k in range(reps):
+        comm.allreduceArray(t, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
+        torch.cuda.synchronize()
+        bad.append(int((t != exp * (p ** k)).sum()))
+    used = {k: v - before.get(k, 0) for k, v in eng.stats.items() if v != before.get(k, 0)}
+    reg = eng._ipc_obj._find(t)[0]
+    info = (t.numel(), t.is_contiguous(), len(reg.vmm) if reg else 0)
+    comm.memFree(t)
+    # the communicator still works, and a new allocation maps again
+    t2 = comm.memAlloc(1 << 20, torch.float32)
+    t2.fill_(1.0)
+    comm.allreduceArray(t2, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, 1 << 20)
+    torch.cuda.synchronize()
+    ok2 = bool((t2 == p).all())
+    comm.memFree(t2)
+    return bad, used, info, ok2
+
+
+def test_memalloc_above_2gib_zero_copy_exact():
+    n = (2 << 30) // 4 + (1 << 20)            # 2 GiB + 4 MiB of float32
+    out = run_spawn(2, _alloc_allreduce_fn, args=(n, 2), timeout=300)
+    for r, (bad, used, info, ok2) in out.items():
+        assert bad == [0, 0], (r, bad)
+        assert used.get("allreduce.ipc2z", 0) == 2, used
+        assert info[0] == n and info[1], info
+        assert ok2
+
+
+def test_memalloc_many_chunks():
+    n = (40 << 20) // 4 + 16                    # 40 MiB + 64 B over 8 MiB chunks: 6 chunks
+    out = run_spawn(3, _alloc_allreduce_fn, args=(n, 2), env={"MP4X_VMM_CHUNK": str(8 << 20)})
+    for r, (bad, used, info, ok2) in out.items():
+        assert bad == [0, 0], (r, bad)
+        assert used.get("allreduce.ipc2z", 0) == 2, used
+        assert info[2] >= 2 + 2 * 2, info       # own + scratch + two peers' tensor + scratch
+        assert ok2
+
+
+def _zero_fn(comm, n):
+    from mp4x import Operands, Operators
+    from mp4x.utils.commutils import CommUtils
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    t = comm.memAlloc(n, torch.bfloat16)
+    i = torch.arange(n, device="cuda", dtype=torch.int32) % 7
+    t.copy_(i + r)
+    counts = [(n // p) // 8 * 8] * p              # whole 16-byte vectors per segment
+    counts[-1] += n - sum(counts)
+    B = Operands.BF16_OPERAND()
+    before = dict(eng.stats)
+    comm.reduceScatterArray(t, B, Operators.BFloat16.SUM, 0, counts)
+    froms, tos = CommUtils.getFromsFromCount(0, counts, p), CommUtils.getTosFromCount(0, counts, p)
+    exp = (i * p + p * (p - 1) // 2).to(torch.bfloat16)
+    bad_rs = int((t[froms[r]:tos[r]] != exp[froms[r]:tos[r]]).sum())
+    comm.allgatherArray(t, B, froms, tos)
+    torch.cuda.synchronize()
+    bad_ag = int((t != exp).sum())
+    used = {k: v - before.get(k, 0) for k, v in eng.stats.items() if v != before.get(k, 0)}
+    comm.memFree(t)
+    return bad_rs, bad_ag, used
+
+
+def test_memalloc_zero_rs_ag_bf16():
+    n = (96 << 20) // 2                           # 96 MiB of bf16, above the staging buffer
+    out = run_spawn(4, _zero_fn, args=(n,))
+    for r, (bad_rs, bad_ag, used) in out.items():
+        assert bad_rs == 0 and bad_ag == 0, (r, bad_rs, bad_ag, used)
+        assert used.get("reduce_scatter.ipc_zc") == 1 and used.get("allgather.ipc_zc") == 1, used
