@@ -23,7 +23,20 @@
 //    the same element offsets, so block b only has to meet block b of the peers;
 //  * every spin is bounded (s_memrealtime, 100 MHz): on timeout the block records an
 //    error word and exits instead of hanging the GPU;
-//  * data buffers are uncached as well, so remote reads never see stale L2 lines.
+//  * the STAGED forms' data buffers are uncached as well, so remote reads never see stale L2
+//    lines;
+//  * the ZERO-COPY forms read and write the peers' own tensors (coarse-grained hipMalloc or
+//    memAlloc/VMM memory, L2-cached on their home GPU).  What they rely on: (a) every remote
+//    WRITE of a call is followed by the writer's system-scope release (L2 write-back) before
+//    its barrier flag, and (b) every block of the home GPU passes a system-scope ACQUIRE after
+//    that barrier (block_barrier below: `buffer_inv sc0 sc1`, run by blocks on every XCD), so
+//    the lines of its own tensor it cached before the peers' writes (phase 1 reads) are
+//    invalidated before the kernel ends — the next kernel reads the peers' values from memory.
+//    This is the protocol argument, not an architectural guarantee for every topology: the
+//    collective self-test (device_engine._ipc_self_test -> selftest_zero_copy) runs every form
+//    TWICE on the same tensor at mesh creation (the second call reduces the first call's
+//    results in place, so a stale line would show as a wrong element), autotune repeats that
+//    probe per candidate, and tests/test_multigpu_gpu.py runs it across real GPUs.
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 

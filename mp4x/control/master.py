@@ -37,7 +37,7 @@ import threading
 import time
 from typing import Dict, List, Optional
 
-from .protocol import recv_frame, send_frame, local_ip
+from .protocol import recv_frame, recv_frame_sized, send_frame, local_ip
 
 LOG = logging.getLogger("mp4x.master")
 
@@ -165,6 +165,8 @@ class CommMaster:
         self._threads: List[threading.Thread] = []
         self.timeout_code: Optional[int] = None
         self.logs: List[str] = []   # remote log history (also emitted through logging)
+        self.rpc_bytes: Dict[str, int] = {}   # request bytes received per RPC method
+        self._bytes_lock = threading.Lock()
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "CommMaster":
@@ -239,10 +241,12 @@ class CommMaster:
         try:
             while not self._stop_evt.is_set():
                 try:
-                    req = recv_frame(conn)
+                    req, nb = recv_frame_sized(conn)
                 except (ConnectionError, OSError):
                     return
                 m = req.get("m")
+                with self._bytes_lock:          # control-plane load per method (rpc_stats)
+                    self.rpc_bytes[str(m)] = self.rpc_bytes.get(str(m), 0) + nb
                 args = req.get("a", [])
                 fn = getattr(self, "rpc_" + str(m), None)
                 if fn is None:
@@ -424,6 +428,11 @@ class CommMaster:
 
     def rpc_allgather_obj(self, rank: int, payload):
         return self._gather.contribute(int(rank), payload, self._stop_evt)
+
+    def rpc_stats(self):
+        """Request bytes the master received per RPC method (control-plane load)."""
+        with self._bytes_lock:
+            return dict(self.rpc_bytes)
 
     def rpc_kv_set(self, key: str, value: bytes):
         with self._kv_cv:

@@ -40,10 +40,15 @@ def send_frame(sock: socket.socket, obj) -> None:
 
 
 def recv_frame(sock: socket.socket):
+    return recv_frame_sized(sock)[0]
+
+
+def recv_frame_sized(sock: socket.socket):
+    """(decoded frame, body bytes)."""
     (n,) = _LEN.unpack(recv_exact(sock, _LEN.size))
     if n > MAX_FRAME:
         raise ConnectionError(f"frame too large: {n}")
-    return msgpack.unpackb(recv_exact(sock, n), raw=False, strict_map_key=False)
+    return msgpack.unpackb(recv_exact(sock, n), raw=False, strict_map_key=False), n
 
 
 def local_ip() -> str:

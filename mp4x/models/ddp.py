@@ -8,8 +8,8 @@ has been accumulated — on a dedicated HIP stream, so RCCL / the IPC kernels ov
 rest of the backward pass.  The 1/p average is fused into the allreduce itself (the IPC
 kernels scale the reduced value before their final store, RCCL uses ncclAvg, the fp8 path
 scales before re-quantising), so no separate pass over the buckets runs; ``finish()`` only
-joins the streams.  Bucket buffers are registered with the communicator, so the two-shot
-runs zero-copy on them.
+joins the streams.  Buckets are views of one ``memAlloc`` arena per dtype (mapped into every
+peer at any size), so the two-shot runs zero-copy on them; ``close()`` frees it.
 
 Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X) and RCCL splits a
 message over channels/links; buckets of 32-128 MiB keep every link busy while leaving
@@ -27,10 +27,9 @@ from ..operators import Operators, for_dtype, dtype_of_torch
 
 
 class _Bucket:
-    def __init__(self, params: List[torch.nn.Parameter], device, dtype):
+    def __init__(self, params: List[torch.nn.Parameter], buffer: torch.Tensor):
         self.params = params
-        n = sum(p.numel() for p in params)
-        self.buffer = torch.zeros(n, device=device, dtype=dtype)
+        self.buffer = buffer
         self.pending = len(params)
         self.event = None
         self.averaged = False
@@ -53,28 +52,53 @@ class GradientSynchronizer:
         if not params:
             raise ValueError("no trainable parameters")
         cap = int((bucket_mb or float(os.environ.get("MP4X_BUCKET_MB", 64))) * (1 << 20))
-        self.buckets: List[_Bucket] = []
+        groups: List[List[torch.nn.Parameter]] = []
         cur: List[torch.nn.Parameter] = []
         size = 0
         for p in reversed(params):
             if cur and (size + p.numel() * p.element_size() > cap or p.dtype != cur[0].dtype):
-                self.buckets.append(_Bucket(cur, cur[0].device, cur[0].dtype))
+                groups.append(cur)
                 cur, size = [], 0
             cur.append(p)
             size += p.numel() * p.element_size()
         if cur:
-            self.buckets.append(_Bucket(cur, cur[0].device, cur[0].dtype))
+            groups.append(cur)
+        self.cuda = groups[0][0].is_cuda
+        # One arena per dtype holds every bucket of that dtype, 16-byte aligned bucket offsets.
+        # On a GPU mesh it is a memAlloc tensor: mapped into every peer once, at any size, so
+        # every bucket's allreduce runs the zero-copy kernels (no caching-allocator segment that
+        # might be too large to map, no registration to forget).
+        self._arenas: List[torch.Tensor] = []
+        self._memalloc = self.cuda and self.p > 1 and hasattr(self.comm, "memAlloc")
+        sizes, offs, totals = [], [], {}
+        for g in groups:                                  # bucket offsets inside its dtype's arena
+            es = g[0].element_size()
+            align = max(1, 16 // es)
+            n = -(-sum(p.numel() for p in g) // align) * align
+            sizes.append(n)
+            offs.append(totals.get(g[0].dtype, 0))
+            totals[g[0].dtype] = offs[-1] + n
+        arenas = {}
+        for dt, total in totals.items():                  # same order on every rank: collective
+            dev = next(g[0].device for g in groups if g[0].dtype == dt)
+            if self._memalloc:
+                arena = self.comm.memAlloc(total, dt, device=dev)
+            else:
+                arena = torch.empty(total, dtype=dt, device=dev)
+            arena.zero_()
+            arenas[dt] = arena
+            self._arenas.append(arena)
+        self.buckets: List[_Bucket] = [_Bucket(g, arenas[g[0].dtype][o:o + n])     # backward order
+                                       for g, o, n in zip(groups, offs, sizes)]
         self._owner = {}
         for b in self.buckets:
-            for p, v in zip(b.params, b.views):
-                p.grad = v                      # grads accumulate straight into the bucket
+            off = 0
+            for p in b.params:
+                p.grad = b.buffer[off:off + p.numel()].view_as(p)   # grads accumulate in the bucket
+                off += p.numel()
                 self._owner[p] = b
                 p.register_post_accumulate_grad_hook(self._hook)
-        self.cuda = self.buckets[0].buffer.is_cuda
         self.stream = torch.cuda.Stream() if self.cuda else None
-        if self.cuda and self.p > 1 and hasattr(self.comm, "registerBuffer"):
-            for b in self.buckets:        # collective; False on every rank alike (then staged)
-                self.comm.registerBuffer(b.buffer)
         self._launched: List[_Bucket] = []
         self.tuned = {}
         if autotune:
@@ -141,3 +165,18 @@ class GradientSynchronizer:
     def zero_grad(self):
         for b in self.buckets:
             b.buffer.zero_()
+
+    def close(self):
+        """Collective: release the bucket arenas (``memFree``: the peers' mappings of them and
+        the push scratch).  The parameters' ``.grad`` views are dropped first."""
+        if self.cuda:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        for b in self.buckets:
+            for p in b.params:
+                p.grad = None
+        self.buckets = []
+        self._owner = {}
+        if self._memalloc:
+            for a in self._arenas:
+                self.comm.memFree(a)
+        self._arenas = []

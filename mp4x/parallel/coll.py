@@ -35,7 +35,10 @@ def _mv(t: torch.Tensor) -> torch.Tensor:
 
 
 def _scale(splits, t: torch.Tensor):
-    if splits is None or t.dtype in _MOVE_DTYPES:
+    """all_to_all splits of ``t`` as moved by :func:`_mv`: the uint8 view widens only the LAST
+    dimension, so dim-0 splits grow by the element size for 1-D tensors only (an [n, dim] int16
+    tensor keeps its row splits)."""
+    if splits is None or t.dtype in _MOVE_DTYPES or t.dim() > 1:
         return splits
     return [x * t.element_size() for x in splits]
 
@@ -46,20 +49,6 @@ class TorchColl:
         self.backend = backend
         self.gather_into_tensor_ok = backend != "gloo"
         self.reduce_scatter_ok = backend != "gloo"
-
-    def _exchange_apply(self, obj, fn):
-        """Publish obj, run ``fn(every rank's obj)`` while all of them are still published (the
-        closing barrier keeps every peer's tensor alive and unmodified until everyone has
-        copied from it): the data-movement collectives read peers' tensors directly instead of
-        publishing clones."""
-        self._sync()
-        self.hub.slots[self.rank] = obj
-        self.hub.bar.wait()
-        try:
-            fn(list(self.hub.slots))
-            self._sync()
-        finally:
-            self.hub.bar.wait()
 
     def all_reduce(self, t, code, avg: bool = False):
         """``avg``: SUM then divide by the group size inside the collective (ncclAvg)."""

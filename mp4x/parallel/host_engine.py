@@ -404,6 +404,26 @@ class HostEngine:
             self.t.send(parent, tag, wire.pack_maps([(r, acc)], operand))
         return acc
 
+    def allgather_bytes(self, payload: bytes) -> List[bytes]:
+        """Every rank's opaque byte string, rank order, peer to peer over the mesh: one send to
+        every peer (the readers drain into mailboxes, so no ordering between ranks can block),
+        then one receive from every peer.  Used for the map key-dictionary rounds, so new key
+        strings never travel through the master (the reference's master carries only control:
+        J/rpc/Server.java:131-137; its map contents move slave to slave, ProcessCommSlave.java:
+        1329-1373)."""
+        p, r = self.p, self.rank
+        out: List[bytes] = [b""] * p
+        out[r] = payload
+        if p == 1:
+            return out
+        tag = self.next_tag()
+        for j in range(1, p):
+            self.t.send((r + j) % p, tag, [payload])
+        for j in range(1, p):
+            src = (r - j) % p
+            out[src] = bytes(self.t.recv(src, tag))
+        return out
+
     def tree_bcast_obj(self, payload: bytes, root: int) -> bytes:
         """Broadcast an opaque byte string down the scatter tree."""
         p, r = self.p, self.rank

@@ -339,9 +339,12 @@ class ProcessCommSlave:
 
     def _map_on_device(self, mapData: Dict, all_keys=None) -> bool:
         """Do this map collective's values live on the GPU?  A rank with an empty map cannot
-        tell, so the ranks agree over the control plane — in ONE round that also carries every
-        rank's not-yet-numbered keys (``all_keys``: every key the device op will number; default
-        the map's), so the device op skips its own key-dictionary round (``_keys_presynced``)."""
+        tell, so the ranks agree over the control plane — a round of a few bytes per rank: the
+        placement flag, whether the rank has not-yet-numbered keys (``all_keys``: every key the
+        device op will number; default the map's), and the value shape.  The new key strings
+        themselves then travel PEER TO PEER (``sparse.allgather_keys`` over the host mesh), so
+        the master's load does not grow with the keys, and the device op skips its own
+        key-dictionary round (``_keys_presynced``)."""
         mine = -1 if not mapData else int(_is_torch(next(iter(mapData.values()))))
         new = []
         if mine == 1 and self._device_engine is None:
@@ -375,12 +378,13 @@ class ProcessCommSlave:
         if mine == 1:
             v0 = next(iter(mapData.values()))
             meta = (tuple(v0.shape), str(v0.dtype).replace("torch.", ""))
-        res = self.server.call("allgather_obj", self.rank, (mine, new, meta))
+        res = self.server.call("allgather_obj", self.rank, (mine, len(new), meta))
         on_device = any(f == 1 for f, _, _ in res)
         if on_device:
-            from .sparse import _dictionary
+            from .sparse import _dictionary, allgather_keys
             eng = self.device
-            _dictionary(eng).learn_round([ks for _, ks, _ in res])
+            if any(nn for _, nn, _ in res):
+                _dictionary(eng).learn_round(allgather_keys(eng, new))
             eng._keys_presynced = True
             eng._map_meta = next((m for _, _, m in res if m is not None), None)
         return on_device

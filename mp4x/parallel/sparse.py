@@ -106,17 +106,61 @@ def _dictionary(engine) -> KeyDictionary:
     return d
 
 
-def _sync_new_keys(engine, new: List) -> None:
-    """One sync round: allgather (control plane) of every rank's unseen keys, numbered in rank
-    order on every rank.  Collective — ranks with nothing new still take part.
+_SEP = "\0"
 
-    When the caller's device/host agreement round already carried the new keys
+
+def encode_keys(keys) -> bytes:
+    """Wire form of a key list for the peer-to-peer key rounds.  ``S`` + the UTF-8 of the keys
+    joined by NUL when every key is a ``str`` without NUL (the reference's keys are Strings:
+    one C-level join / split, ~10 ms for 200k keys); ``E`` = no keys; otherwise ``P`` + pickle
+    (any hashable keys, between this job's own ranks)."""
+    keys = list(keys)
+    if not keys:
+        return b"E"
+    if all(type(k) is str for k in keys):
+        j = _SEP.join(keys)
+        if j.count(_SEP) == len(keys) - 1:
+            return b"S" + j.encode("utf-8", "surrogatepass")
+    import pickle
+    return b"P" + pickle.dumps(keys, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def decode_keys(blob: bytes) -> List:
+    tag = blob[:1]
+    if tag == b"E" or not blob:
+        return []
+    if tag == b"S":
+        return blob[1:].decode("utf-8", "surrogatepass").split(_SEP)
+    if tag == b"P":
+        import pickle
+        return pickle.loads(blob[1:])
+    raise ValueError(f"bad key block tag {tag!r}")
+
+
+def allgather_keys(engine, new: List) -> List[List]:
+    """Every rank's key list, rank order — over the DATA plane: the host TCP mesh of the
+    communicator (peer to peer, never through the master), the in-process hub for loopback
+    ranks, the control plane only when neither exists."""
+    if hasattr(engine.coll, "_exchange"):
+        return engine.coll._exchange(list(new))
+    host = getattr(engine.comm, "engine", None)
+    if host is not None and hasattr(host, "allgather_bytes"):
+        return [decode_keys(b) for b in host.allgather_bytes(encode_keys(new))]
+    return engine.all_gather_object(list(new))
+
+
+def _sync_new_keys(engine, new: List) -> None:
+    """One sync round: allgather (data plane, :func:`allgather_keys`) of every rank's unseen
+    keys, numbered in rank order on every rank.  Collective — ranks with nothing new still take
+    part.
+
+    When the caller's device/host agreement round already numbered the new keys
     (``ProcessCommSlave._map_on_device`` sets ``engine._keys_presynced`` on EVERY rank), this
-    round is skipped: one control-plane round trip per map collective instead of two."""
+    round is skipped."""
     if getattr(engine, "_keys_presynced", False):
         engine._keys_presynced = False
         return
-    _dictionary(engine).learn_round(engine.all_gather_object(list(new)))
+    _dictionary(engine).learn_round(allgather_keys(engine, new))
 
 
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins

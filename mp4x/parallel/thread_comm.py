@@ -237,6 +237,14 @@ class ThreadCommSlave:
     def deregisterBuffer(self, tensor) -> None:
         self.processCommSlave.deregisterBuffer(tensor)
 
+    def memAlloc(self, n: int, dtype=None, device=None):
+        """Pass-through to ``ProcessCommSlave.memAlloc`` (one thread per process, collective over
+        the processes)."""
+        return self.processCommSlave.memAlloc(n, dtype, device)
+
+    def memFree(self, tensor) -> None:
+        self.processCommSlave.memFree(tensor)
+
     # ------------------------------------------------------------------ thread-phase primitives
     def _publish(self, obj) -> None:
         self._slots[self.getThreadId()] = obj
