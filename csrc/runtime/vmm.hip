@@ -35,6 +35,11 @@ hipMemAllocationProp make_prop(int dev) {
   return prop;
 }
 
+// VA alignment of a reservation: 2 MiB (large-fragment friendly) when the chunk size is a 2 MiB
+// multiple, else the runtime default (the alignment must be a power of two; a chunk size in
+// general is not).
+size_t va_alignment(size_t chunk) { return chunk % (2u << 20) == 0 ? (2u << 20) : 0; }
+
 hipError_t grant(void* va, size_t bytes, int dev) {
   hipMemAccessDesc acc;
   std::memset(&acc, 0, sizeof(acc));
@@ -89,7 +94,7 @@ extern "C" int mp4x_vmm_create(size_t chunk, int n, void** va_out, uint64_t* han
     if (fds) fds[i] = -1;
   }
   void* va = nullptr;
-  e = hipMemAddressReserve(&va, total, chunk, nullptr, 0);
+  e = hipMemAddressReserve(&va, total, va_alignment(chunk), nullptr, 0);
   if (e != hipSuccess) return (int)e;
   hipMemAllocationProp prop = make_prop(dev);
   int mapped = 0;
@@ -134,13 +139,16 @@ extern "C" int mp4x_vmm_import(const int* fds, size_t chunk, int n, void** va_ou
   const size_t total = chunk * (size_t)n;
   for (int i = 0; i < n; ++i) handles[i] = 0;
   void* va = nullptr;
-  e = hipMemAddressReserve(&va, total, chunk, nullptr, 0);
+  e = hipMemAddressReserve(&va, total, va_alignment(chunk), nullptr, 0);
   if (e != hipSuccess) return (int)e;
   int mapped = 0;
   for (int i = 0; i < n && e == hipSuccess; ++i) {
     hipMemGenericAllocationHandle_t h;
-    e = hipMemImportFromShareableHandle(&h, reinterpret_cast<void*>((intptr_t)fds[i]),
-                                        hipMemHandleTypePosixFileDescriptor);
+    // HIP reads the POSIX fd THROUGH the osHandle pointer (passing the fd value itself, the
+    // CUDA convention, makes the runtime dereference a small integer: measured SIGSEGV on
+    // ROCm 7 / gfx950, tools/vmm_probe.py)
+    int fd = fds[i];
+    e = hipMemImportFromShareableHandle(&h, static_cast<void*>(&fd), hipMemHandleTypePosixFileDescriptor);
     if (e != hipSuccess) break;
     handles[i] = (uint64_t)(uintptr_t)h;
     e = hipMemMap(static_cast<char*>(va) + (size_t)i * chunk, chunk, 0, h, 0);
@@ -161,4 +169,17 @@ extern "C" int mp4x_vmm_import(const int* fds, size_t chunk, int n, void** va_ou
 // Unmap + release ``n`` chunks mapped at ``va`` and free the VA range (own or imported).
 extern "C" int mp4x_vmm_free(void* va, size_t chunk, int n, const uint64_t* handles) {
   return teardown(va, chunk, n, handles, chunk * (size_t)n);
+}
+
+// System-scope release on every XCD: each workgroup's lane 0 issues a release fence at system
+// scope (L2 write-back of that XCD's dirty lines), with enough workgroups that every XCD runs
+// several of them.  Makes what earlier kernels wrote into coarse-grained memory visible to
+// readers that do not go through this GPU's L2 (a peer over xGMI, or another mapping).
+__global__ void __launch_bounds__(64) k_release_all_xcds() {
+  if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+extern "C" int mp4x_release_all(void* stream) {
+  hipLaunchKernelGGL(k_release_all_xcds, dim3(1024), dim3(64), 0, static_cast<hipStream_t>(stream));
+  return (int)hipGetLastError();
 }

@@ -25,7 +25,9 @@ def recv_exact(sock: socket.socket, n: int) -> bytearray:
     mv = memoryview(buf)
     got = 0
     while got < n:
-        r = sock.recv_into(mv[got:], n - got)
+        # MSG_WAITALL: one syscall for the whole remainder, slept in with the GIL released (the
+        # mesh's reader threads then do not contend with the merging thread chunk by chunk)
+        r = sock.recv_into(mv[got:], n - got, socket.MSG_WAITALL)
         if r == 0:
             raise ConnectionError("peer closed connection")
         got += r

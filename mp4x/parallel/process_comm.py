@@ -48,6 +48,8 @@ HEARTBEAT_PERIOD = float(os.environ.get("MP4X_HEARTBEAT_PERIOD", 15.0))
 HEARTBEAT_MAX_FAIL = int(os.environ.get("MP4X_HEARTBEAT_MAX_FAIL", 4))
 BCAST_TREE_BYTES = int(os.environ.get("MP4X_BCAST_TREE_BYTES", 1 << 16))
 SHM_ON = os.environ.get("MP4X_SHM", "1") == "1"
+# host allreduceMap of primitive values through the columnar path (parallel/hostmap.py)
+HOST_MAP_COLUMNAR = os.environ.get("MP4X_HOST_MAP_COLUMNAR", "1") == "1"
 # same-host ranks take /dev/shm at every size: 4 procs, 16 doubles 34 us vs 500 us over the TCP
 # mesh; 800 KB 0.36 vs 1.8 ms; 8 procs 0.14 vs 1.3 ms (profiles/r1/host_shm_vs_tcp.jsonl)
 SHM_MIN_BYTES = 0
@@ -849,6 +851,10 @@ class ProcessCommSlave:
             return mapData
         if self._map_on_device(mapData):
             return self.device.allreduce_map(mapData, operator)
+        from . import hostmap
+        if HOST_MAP_COLUMNAR and hostmap.supported(operand, operator):
+            # primitive values: keys + one value column per block, vectorised owner merge
+            return hostmap.allreduce_map(self.engine, mapData, operand, operator)
         mine = self.engine.ring_reduce_scatter_maps([[d] for d in self._partition(mapData)], operand, operator)
         allb = self.engine.ring_allgather_maps(mine, operand)
         out: Dict = {}

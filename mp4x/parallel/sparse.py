@@ -32,6 +32,7 @@ import numpy as np
 import torch
 
 from ..operators import dtype_of_torch, for_dtype
+from .wire import decode_keys, encode_keys  # noqa: F401 — the key codec of the map rounds
 
 
 class KeyDictionary:
@@ -104,37 +105,6 @@ def _dictionary(engine) -> KeyDictionary:
     if d is None:
         d = engine._keydict = KeyDictionary()
     return d
-
-
-_SEP = "\0"
-
-
-def encode_keys(keys) -> bytes:
-    """Wire form of a key list for the peer-to-peer key rounds.  ``S`` + the UTF-8 of the keys
-    joined by NUL when every key is a ``str`` without NUL (the reference's keys are Strings:
-    one C-level join / split, ~10 ms for 200k keys); ``E`` = no keys; otherwise ``P`` + pickle
-    (any hashable keys, between this job's own ranks)."""
-    keys = list(keys)
-    if not keys:
-        return b"E"
-    if all(type(k) is str for k in keys):
-        j = _SEP.join(keys)
-        if j.count(_SEP) == len(keys) - 1:
-            return b"S" + j.encode("utf-8", "surrogatepass")
-    import pickle
-    return b"P" + pickle.dumps(keys, protocol=pickle.HIGHEST_PROTOCOL)
-
-
-def decode_keys(blob: bytes) -> List:
-    tag = blob[:1]
-    if tag == b"E" or not blob:
-        return []
-    if tag == b"S":
-        return blob[1:].decode("utf-8", "surrogatepass").split(_SEP)
-    if tag == b"P":
-        import pickle
-        return pickle.loads(blob[1:])
-    raise ValueError(f"bad key block tag {tag!r}")
 
 
 def allgather_keys(engine, new: List) -> List[List]:

@@ -37,9 +37,11 @@ native.register_signatures({
     "mp4x_vmm_create": (c_int, [c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P, _INTP]),
     "mp4x_vmm_import": (c_int, [_INTP, c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P]),
     "mp4x_vmm_free": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
+    "mp4x_release_all": (c_int, [c_void_p]),
 })
 
 DEFAULT_CHUNK = 512 << 20
+_BIG_FRAG = 2 << 20
 _FDS_PER_MSG = 200          # SCM_RIGHTS carries at most 253 fds per message (SCM_MAX_FD)
 
 
@@ -50,6 +52,8 @@ def chunk_plan(nbytes: int, gran: int, chunk: Optional[int] = None) -> (int, int
     if nbytes <= 0:
         raise Mp4jException("memAlloc needs a positive size")
     gran = max(1, int(gran))
+    if nbytes >= _BIG_FRAG and _BIG_FRAG % gran == 0:
+        gran = _BIG_FRAG          # 2 MiB multiples: large TLB fragments, 2 MiB aligned VA
     cap = int(chunk or os.environ.get("MP4X_VMM_CHUNK", DEFAULT_CHUNK))
     cap = max(gran, cap // gran * gran)
     need = -(-nbytes // gran) * gran

@@ -82,9 +82,22 @@ def run_spawn(p, fn, args=(), env=None, timeout=240, threads=0, mode="shared"):
     for pr in procs:
         pr.start()
     out = {}
+    import queue as _queue
+    import time as _time
+    deadline = _time.monotonic() + timeout
     try:
-        for _ in range(p):
-            r, st, val = q.get(timeout=timeout)
+        while len(out) < p:
+            try:
+                r, st, val = q.get(timeout=1.0)
+            except _queue.Empty:
+                # a rank that died without reporting (segfault, abort) fails the test now instead
+                # of leaving it waiting silently until the timeout
+                dead = [pr.exitcode for pr in procs if pr.exitcode not in (None, 0)]
+                if dead and q.empty():
+                    raise AssertionError(f"rank process(es) died with exit codes {dead}")
+                if _time.monotonic() > deadline:
+                    raise AssertionError(f"ranks did not finish within {timeout} s")
+                continue
             assert st == "ok", val
             out[r] = val
     finally:

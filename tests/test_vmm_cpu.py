@@ -21,6 +21,10 @@ def test_chunk_plan():
     # a cap that is not a granularity multiple is rounded down to one
     c, n = chunk_plan(10 * g, g, 3 * g + 7)
     assert c == 3 * g and n == 4
+    # 4 KiB device granularity: buffers of 2 MiB and up take 2 MiB multiples
+    assert chunk_plan(2796224, 4096, 8 << 20) == (4 << 20, 1)
+    assert chunk_plan(5000, 4096, 8 << 20) == (8192, 1)
+    assert chunk_plan((40 << 20) + 64, 4096, 8 << 20) == (8 << 20, 6)
     with pytest.raises(Mp4jException):
         chunk_plan(0, g)
 
@@ -40,8 +44,9 @@ def _fd_fn(comm, nfds):
     for j, fds in got.items():
         vals = []
         for fd in fds:
-            os.lseek(fd, 0, os.SEEK_SET)
-            vals.append(os.read(fd, 64).decode())
+            # pread: the received fd shares its file offset with the sender's and with every
+            # other receiver's copy (one open file description), so no lseek + read
+            vals.append(os.pread(fd, 64, 0).decode())
             os.close(fd)
         seen[j] = vals
     return seen

@@ -12,8 +12,8 @@
   linked against libmp4x_host.so next to it (rpath $ORIGIN).
 * ``mp4x/_native/_mp4x_map*.so`` — CPython extension over libtorch (csrc/pyext/map_ext.cpp): the
   device map collectives' Dict[key, Tensor] -> ids / rows walk.
-* ``mp4x/_native/_mp4x_hostmap*.so`` — plain CPython extension (csrc/pyext/hostmap_ext.cpp): the
-  host map collectives' Java-hash owner partition.
+* ``mp4x/_native/_mp4x_hostmap*.so`` — CPython + numpy C-API extension (csrc/pyext/hostmap_ext.cpp):
+  the host map collectives' Java-hash owner partition and value-row stacking.
 
 Incremental: objects are rebuilt only when a source or header is newer.
 ``--debug`` builds ``libmp4x_hip_debug.so`` instead: ``-O1 -g -DMP4X_DEBUG``, which turns on the
@@ -158,8 +158,9 @@ def build_hostmapext():
     src = os.path.join(CSRC, "pyext", "hostmap_ext.cpp")
     out = os.path.join(OUT, "_mp4x_hostmap" + sysconfig.get_config_var("EXT_SUFFIX"))
     if os.path.exists(src) and newer(src, out, []):
+        import numpy
         run(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-shared", "-I", sysconfig.get_paths()["include"],
-             src, "-o", out])
+             "-I", numpy.get_include(), src, "-o", out])
         print("  g++  ", os.path.relpath(src, ROOT), "->", os.path.relpath(out, ROOT))
     return out
 
