@@ -263,6 +263,28 @@ def main():
             dist.all_reduce(flag, op=dist.ReduceOp.MAX)
             if flag.item() > 0:
                 break
+        # the rooted collectives' schedules (RCCL vs IPC copy plans / two-shot vs composites)
+        # at sizes on both sides of the IPC direct tier, recorded the same way
+        rooted = {}
+        for nb in (1 << 20, 16 << 20, 128 << 20):
+            failed = 0.0
+            like = torch.empty(nb // 4, device=dev)
+            row = {}
+            try:
+                for kind, fn in (("reduce", lambda: comm.device.autotune_reduce(like, op, root=p - 1)),
+                                 ("broadcast", lambda: comm.device.autotune_broadcast(like, root=p - 1)),
+                                 ("gather", lambda: comm.device.autotune_gather(like, root=p - 1)),
+                                 ("scatter", lambda: comm.device.autotune_scatter(like, root=p - 1))):
+                    row[kind] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in fn().items()}
+            except Exception as e:   # noqa: BLE001 — evidence only
+                row["error"] = str(e)[:200]
+                failed = 1.0
+            rooted[str(nb)] = row
+            flag = torch.tensor([failed], dtype=torch.float64, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            if flag.item() > 0:
+                break
+        tiers["rooted"] = rooted
 
     ref = REF_BUSBW_MBPS.get(p)
     selftest = None if (p == 1 or args.cpu) else comm.device.ipc_selftest

@@ -831,19 +831,22 @@ class DeviceEngine:
                                    probe)
 
     def _autotune_kind(self, kind: str, view: torch.Tensor, op, cands, run, iters: int,
-                       probe=None) -> Dict[str, float]:
+                       probe=None, pin_rccl: bool = False) -> Dict[str, float]:
+        """``pin_rccl``: the kind's default path is not plain RCCL at every size (reduce /
+        broadcast / gather / scatter take IPC tiers below the two-shot size), so RCCL is timed and
+        pinned explicitly as the schedule ``rccl`` instead of as "nothing pinned"."""
         key = self._rsag_key(kind, view, op)
         times = []
         if self.watchdog is not None:
             self.watchdog.paused += 1
         try:
             for c in cands:
-                if c == "rccl":
+                if c == "rccl" and not pin_rccl:
                     self._tuned.pop(key, None)
                 else:
                     self._tuned[key] = c
-                times.append(self._time_fn(run, uses_ipc=c == "ipc", iters=iters, name=f"{kind}:{c}",
-                                           probe=probe))
+                times.append(self._time_fn(run, uses_ipc=c not in ("rccl", "p2p"), iters=iters,
+                                           name=f"{kind}:{c}", probe=probe))
         finally:
             self._tuned.pop(key, None)
             if self.watchdog is not None:
@@ -852,10 +855,110 @@ class DeviceEngine:
         self.coll.all_reduce(tt, OpCode.MAX)
         res = dict(zip(cands, tt.cpu().tolist()))
         best = min(res, key=res.get) if res else None
-        if best is not None and best != "rccl" and res[best] != float("inf"):
+        if best is not None and (best != "rccl" or pin_rccl) and res[best] != float("inf"):
             self._tuned[key] = best
         self._autosave()
         return res
+
+    # ------------------------------------------------------------------ reduce / broadcast / gather / scatter
+    def _root_tuned(self, kind: str, view: torch.Tensor, op) -> Optional[str]:
+        """Schedule pinned by the autotuners below for this (kind, dtype, op, size class), or
+        None.  Only for unforced, uncaptured calls (a capture keeps the tier logic)."""
+        if not self._tuned or self.algo not in ("", "auto") or (view.is_cuda and capturing_now()):
+            return None
+        return self._tuned.get(self._rsag_key(kind, view, op))
+
+    def autotune_reduce(self, like: torch.Tensor, operator, root: int = 0, iters: int = 3) -> Dict[str, float]:
+        """``reduce`` schedules timed side by side (RCCL ``ncclReduce``; ``ipc`` = the IPC two-shot
+        allreduce, whose result every rank gets — the reduce contract leaves non-root results
+        unspecified, ProcessCommSlave.java:1390-1421; ``a2a`` = reduce-scatter + gather, the
+        reference's own composition), exact-probed at the root, MAX over ranks, fastest pinned
+        for this (dtype, op, size class).  Collective."""
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        op = self._op(operator, view)
+        nb = view.numel() * view.element_size()
+        cands = (["rccl"] if self.rccl_ok(op, view.dtype) else []) + ["a2a"]
+        if self.ipc_enabled and self._ipc_ok(op, view.dtype, nb):
+            cands.append("ipc")
+        n = view.numel()
+
+        def probe():
+            exp = self._fill_probe(view, op)
+            if exp is None:
+                return None
+
+            def check():
+                bad = int((view != exp).sum()) if self.rank == root else 0
+                view.zero_()
+                return bad
+            return check
+        return self._autotune_kind("reduce", view, op, cands, lambda: self.reduce(view, 0, n, op, None, root), iters,
+                                   probe, pin_rccl=True)
+
+    def _copy_probe(self, view: torch.Tensor, owners):
+        """Probe for the data-movement kinds: element i holds ``i % 97 + owner(i)`` where
+        ``owners`` = [(from, to, rank)] says which rank's data each range is; the caller fills
+        what this rank owns before the call."""
+        idt = torch.int32 if view.numel() < (1 << 31) else torch.int64
+        exp = torch.arange(view.numel(), device=view.device, dtype=idt).remainder_(97)
+        for f, t, j in owners:
+            exp[f:t] += j
+        return exp.to(view.dtype)
+
+    def autotune_broadcast(self, like: torch.Tensor, root: int = 0, iters: int = 3) -> Dict[str, float]:
+        """``broadcast``: RCCL ``ncclBroadcast`` vs the piecewise IPC copy plan (every receiver
+        pulls from the root over its own link) vs ``composite`` (scatter + all-gather, the
+        reference's van de Geijn schedule, ProcessCommSlave.java:750-775).  Collective."""
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        n = view.numel()
+        cands = ["rccl", "composite"] + (["ipc"] if self.ipc_enabled and view.is_cuda else [])
+
+        def probe():
+            exp = self._copy_probe(view, [(0, n, root)])
+            view.copy_(exp) if self.rank == root else view.fill_(-1)
+
+            def check():
+                bad = int((view != exp).sum())
+                view.zero_()
+                return bad
+            return check
+        return self._autotune_kind("broadcast", view, None, cands, lambda: self.broadcast(view, 0, n, root), iters,
+                                   probe, pin_rccl=True)
+
+    def _autotune_gs(self, kind: str, like: torch.Tensor, root: int, iters: int) -> Dict[str, float]:
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
+        cands = ["p2p"] + (["ipc"] if self.ipc_enabled and view.is_cuda else [])
+        r = self.rank
+
+        def probe():
+            exp = self._copy_probe(view, [(froms[j], tos[j], j) for j in range(self.p)])
+            view.fill_(-1)
+            if kind == "gather":
+                view[froms[r]:tos[r]] = exp[froms[r]:tos[r]]
+            elif r == root:
+                view.copy_(exp)
+
+            def check():
+                if kind == "gather":
+                    bad = int((view != exp).sum()) if r == root else 0
+                else:
+                    bad = int((view[froms[r]:tos[r]] != exp[froms[r]:tos[r]]).sum())
+                view.zero_()
+                return bad
+            return check
+        fn = (lambda: self.gather(view, froms, tos, root)) if kind == "gather" else \
+            (lambda: self.scatter(view, froms, tos, root))
+        return self._autotune_kind(kind, view, None, cands, fn, iters, probe, pin_rccl=True)
+
+    def autotune_gather(self, like: torch.Tensor, root: int = 0, iters: int = 3) -> Dict[str, float]:
+        """``gather`` (even split): grouped p2p (``ncclRecv`` x p-1 at the root) vs the
+        piecewise IPC copy plan (the root pulls every segment over its links).  Collective."""
+        return self._autotune_gs("gather", like, root, iters)
+
+    def autotune_scatter(self, like: torch.Tensor, root: int = 0, iters: int = 3) -> Dict[str, float]:
+        """``scatter`` (even split): grouped p2p vs the piecewise IPC copy plan.  Collective."""
+        return self._autotune_gs("scatter", like, root, iters)
 
     def _time_fn(self, run, uses_ipc: bool, iters: int, name: str, probe=None) -> float:
         """Seconds per call of ``run`` (inf when it failed or was wrong on ANY rank).  Collective.
@@ -929,7 +1032,9 @@ class DeviceEngine:
     # ------------------------------------------------------------------ persisted tuning table
     _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w", "a2a",
                                   "rhd"},
-                    "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"}}
+                    "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"},
+                    "reduce": {"rccl", "ipc", "a2a"}, "broadcast": {"rccl", "ipc", "composite"},
+                    "gather": {"p2p", "ipc"}, "scatter": {"p2p", "ipc"}}
 
     def _topology(self) -> dict:
         dev = torch.cuda.get_device_name(self.device) if self.device.type == "cuda" else "cpu"
@@ -1395,7 +1500,16 @@ class DeviceEngine:
     def broadcast(self, arr: torch.Tensor, frm: int, to: int, root: int):
         flat = self._flat(arr)
         if to > frm:
-            if self.algo == "composite" and to - frm >= self.p:
+            t = self._root_tuned("broadcast", flat[frm:to], None)
+            if t == "rccl":
+                self._count("broadcast")
+                self.coll.broadcast(flat[frm:to], root)
+                return arr
+            if t == "ipc" and self.ipc() is not None and self.ipc_large() is not None and \
+                    self.ipc_large().broadcast_large(flat, frm, to, root):
+                self._count("broadcast.ipc_large")
+                return arr
+            if (self.algo == "composite" or t == "composite") and to - frm >= self.p:
                 # van de Geijn, the reference's schedule (ProcessCommSlave.java:750-775): scatter
                 # from the root, then all-gather — kept for parity benchmarks (MP4X_DEVICE_ALGO)
                 self._count("broadcast.composite")
@@ -1446,6 +1560,28 @@ class DeviceEngine:
             return arr
         op = self._op(operator, view)
         nbytes = view.numel() * view.element_size()
+        t = self._root_tuned("reduce", view, op)
+        if t == "rccl" and self.rccl_ok(op, view.dtype):
+            self._count("reduce.rccl")
+            self.coll.reduce(view, root, op.code)
+            return arr
+        if t == "ipc" and self._ipc_ok(op, view.dtype, nbytes) and self.ipc() is not None:
+            from .ipc import TWOSHOT
+            peers = self._ipc_obj.registered(view) if self._zc else None
+            if peers is not None:
+                self._count("reduce.ipc_zc")
+                self._ipc_obj.allreduce_registered(view, op, peers)
+            else:
+                self._count("reduce.ipc2")
+                inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
+                inst.allreduce(view, op, algo=TWOSHOT)
+            return arr
+        if t == "a2a":
+            self._count("reduce.a2a")
+            froms, tos, _ = CommUtils.even_split(frm, to, self.p)
+            self._reduce_scatter_a2a(flat, froms, tos, op)
+            self.gather(flat, froms, tos, root)
+            return arr
         if self.algo in ("", "auto") and self._ipc_ok(op, view.dtype, nbytes) and self._ipc_small_ok(flat, nbytes):
             # latency tier: the IPC allreduce kernels (non-root results are unspecified by the
             # reduce contract, ProcessCommSlave.java:1390-1421, so every rank may receive the sum)
@@ -1473,11 +1609,16 @@ class DeviceEngine:
     def gather(self, arr: torch.Tensor, froms, tos, root: int):
         flat = self._flat(arr)
         r = self.rank
-        if self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
+        t = self._root_tuned("gather", flat[froms[0]:tos[-1]], None)
+        if t == "ipc" and self.ipc() is not None and self.ipc_large() is not None and \
+                self.ipc_large().gather_large(flat, froms, tos, root):
+            self._count("gather.ipc_large")
+            return arr
+        if t != "p2p" and self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
                 self._ipc_obj.gather(flat, froms, tos, root):
             self._count("gather.ipc")
             return arr
-        if self._dm_large_ok(flat) and self.ipc_large().gather_large(flat, froms, tos, root):
+        if t != "p2p" and self._dm_large_ok(flat) and self.ipc_large().gather_large(flat, froms, tos, root):
             self._count("gather.ipc_large")
             return arr
         self._count("gather")
@@ -1490,11 +1631,16 @@ class DeviceEngine:
     def scatter(self, arr: torch.Tensor, froms, tos, root: int):
         flat = self._flat(arr)
         r = self.rank
-        if self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
+        t = self._root_tuned("scatter", flat[froms[0]:tos[-1]], None)
+        if t == "ipc" and self.ipc() is not None and self.ipc_large() is not None and \
+                self.ipc_large().scatter_large(flat, froms, tos, root):
+            self._count("scatter.ipc_large")
+            return arr
+        if t != "p2p" and self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
                 self._ipc_obj.scatter(flat, froms, tos, root):
             self._count("scatter.ipc")
             return arr
-        if self._dm_large_ok(flat) and self.ipc_large().scatter_large(flat, froms, tos, root):
+        if t != "p2p" and self._dm_large_ok(flat) and self.ipc_large().scatter_large(flat, froms, tos, root):
             self._count("scatter.ipc_large")
             return arr
         self._count("scatter")
@@ -1585,7 +1731,8 @@ def _watched(name, fn):
     return wrapper
 
 
-_WATCHED = ["allreduce", "autotune_allreduce", "autotune_reduce_scatter", "autotune_allgather", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",
+_WATCHED = ["allreduce", "autotune_allreduce", "autotune_reduce_scatter", "autotune_allgather", "autotune_reduce",
+            "autotune_broadcast", "autotune_gather", "autotune_scatter", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",
             "scatter", "allreduce_map", "all_to_all_v", "reduce_map", "gather_map", "allgather_map",
             "reduce_scatter_map", "scatter_map", "broadcast_map", "barrier"]
 for _n in _WATCHED:

@@ -433,3 +433,39 @@ def first_op_is_a_map_with_an_empty_rank(comm):
 def test_first_device_op_is_a_map_with_an_empty_rank(p):
     res, code, _ = run_ranks(p, first_op_is_a_map_with_an_empty_rank, timeout=90)
     assert code == 0 and set(res.values()) == {"ok"}
+
+
+def rooted_autotune_job(comm):
+    """reduce / broadcast / gather / scatter autotuners: every candidate exact-probed, the
+    verdict agreed, the fastest pinned (RCCL pinned explicitly) and then used."""
+    eng = comm.device
+    p, r = comm.getSlaveNum(), comm.getRank()
+    t = torch.ones(6000, dtype=torch.float32)
+    root = p - 1
+    red = eng.autotune_reduce(t, Operators.Float.SUM, root=root, iters=2)
+    bc = eng.autotune_broadcast(t, root=root, iters=2)
+    ga = eng.autotune_gather(t, root=root, iters=2)
+    sc = eng.autotune_scatter(t, root=root, iters=2)
+    assert set(red) == {"rccl", "a2a"} and set(bc) == {"rccl", "composite"}   # no IPC on CPU tensors
+    assert set(ga) == {"p2p"} and set(sc) == {"p2p"}
+    assert all(v != float("inf") for d in (red, bc, ga, sc) for v in d.values()), (red, bc, ga, sc)
+    pinned = {k[0]: v for k, v in eng._tuned.items() if isinstance(k[0], str)}
+    eng.stats.clear()
+    x = torch.full((5000,), float(r + 1))                       # same size class as the probe
+    eng.reduce(x, 0, 5000, Operators.Float.SUM, None, root)
+    ok = r != root or bool(torch.all(x == p * (p + 1) / 2))
+    y = torch.arange(5000, dtype=torch.float32) if r == root else torch.zeros(5000)
+    eng.broadcast(y, 0, 5000, root)
+    ok = ok and bool(torch.equal(y, torch.arange(5000, dtype=torch.float32)))
+    return pinned, ok, dict(eng.stats)
+
+
+def test_rooted_autotuners_pin_and_apply():
+    res, code, _ = run_ranks(3, rooted_autotune_job, timeout=120)
+    assert code == 0
+    assert len({tuple(sorted(pin.items())) for pin, _, _ in res.values()}) == 1     # agreed
+    for pin, ok, st in res.values():
+        assert ok
+        assert set(pin) >= {"reduce", "broadcast", "gather", "scatter"}
+        assert st.get("reduce." + pin["reduce"]) == 1, st
+        assert st.get("broadcast" if pin["broadcast"] == "rccl" else "broadcast.composite") == 1, st
