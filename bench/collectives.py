@@ -116,6 +116,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--max-elems", type=float, default=1e9)
     ap.add_argument("--check", action="store_true", help="exact-value check of every row / config")
+    ap.add_argument("--ops", default=",".join(OPS), help="--sweep ref: comma list of collectives to run")
+    ap.add_argument("--alloc", choices=("memalloc", "plain"), default="memalloc",
+                    help="configs: the big tensor from comm.memAlloc (zero-copy at any size) or torch.empty")
+    ap.add_argument("--sizes", default=None, help="--sweep ref: comma list of element counts (default: ref sizes)")
     ap.add_argument("--codecs", default="none,fp8", help="fp8_8gb config: wire codecs to run")
     a = ap.parse_args()
     import torch
@@ -140,7 +144,10 @@ def main():
 
     if a.sweep == "ref":
         D = Operands.DOUBLE_OPERAND()
-        for n in (100000, 1000000, 10000000, 100000000, 1000000000):
+        sizes = [int(float(x)) for x in a.sizes.split(",")] if a.sizes else \
+            [100000, 1000000, 10000000, 100000000, 1000000000]
+        want = set(a.ops.split(","))
+        for n in sizes:
             if n > a.max_elems:
                 break
             buf = torch.randn(n, device="cuda", dtype=torch.float64)
@@ -157,6 +164,8 @@ def main():
                 "allreduce": lambda: comm.allreduceArray(buf, D, Operators.Double.SUM, 0, n),
             }
             for k, op in enumerate(OPS):
+                if op not in want:
+                    continue
                 st0 = dict(eng.stats) if eng is not None else {}
                 p50, p99 = timed(fns[op], a.iters, a.warmup, sync)
                 nb = n * 8
@@ -174,7 +183,13 @@ def main():
             del buf
     if a.config == "zero_bf16":   # BASELINE config 3: RS + AG of a 4 GB bf16 tensor
         n = 2_000_000_000 // p * p
-        x = torch.randn(n, device="cuda").to(torch.bfloat16)
+        # memAlloc (default for p > 1): mapped into every peer at any size, so RS and AG run the
+        # zero-copy kernels on it (a 4 GB caching-allocator tensor cannot be mapped: staged pieces)
+        x = comm.memAlloc(n, torch.bfloat16) if (p > 1 and a.alloc == "memalloc") else \
+            torch.empty(n, device="cuda", dtype=torch.bfloat16)
+        CH0 = 1 << 28
+        for s0 in range(0, n, CH0):
+            x[s0:s0 + CH0] = torch.randn(min(CH0, n - s0), device="cuda").to(torch.bfloat16)
         B = Operands.BF16_OPERAND()
         counts = [n // p] * p
         froms = CommUtils.getFromsFromCount(0, counts, p)
@@ -184,13 +199,16 @@ def main():
             comm.reduceScatterArray(x, B, Operators.BFloat16.SUM, 0, counts)
             comm.allgatherArray(x, B, froms, tos)
         tuned = None
-        if p > 1:   # untimed: RCCL vs piecewise IPC vs a2a / p2p, pinned per size class (MAX over ranks)
+        if p > 1 and a.alloc != "memalloc":
+            # untimed: RCCL vs piecewise IPC vs a2a / p2p, pinned per size class (MAX over ranks);
+            # a memAlloc tensor always takes the zero-copy kernels, so nothing to pin there
             tuned = {"reduce_scatter": eng.autotune_reduce_scatter(x, Operators.BFloat16.SUM, iters=2),
                      "allgather": eng.autotune_allgather(x, iters=2)}
             tuned = {k: {c: round(t * 1e3, 3) for c, t in v.items()} for k, v in tuned.items()}
         p50, p99 = timed(step, a.iters, a.warmup, sync)
         nb = n * 2
         rec = {"config": "reduceScatter + allgather of 4 GB bf16 (ZeRO)", "p": p, "p50_ms": p50, "p99_ms": p99,
+               "alloc": a.alloc if p > 1 else "plain", "path": sorted(k for k in eng.stats) if eng is not None else None,
                "busbw_GBps": round(nb / (p50 * 1e-3) / 1e9 * 2 * (p - 1) / p, 3) if p > 1 else None,
                "autotune_ms": tuned}
         if a.check:     # (i % 13 + rank) per rank: the RS + AG result is exact in bf16

@@ -779,6 +779,19 @@ extern "C" int mp4x_ipc_alloc(size_t bytes, void** ptr) {
 
 extern "C" int mp4x_ipc_free(void* ptr) { return (int)hipFree(ptr); }
 
+// Staging data buffer of an IPC instance, zeroed: ``coarse`` = 0 -> fine-grained uncached (the
+// default: peers' reads never meet a stale L2 line); 1 -> plain coarse-grained hipMalloc memory,
+// L2-cached on its home GPU, kept coherent by the kernels' system-scope release / acquire at
+// every barrier (the zero-copy protocol's argument).  MP4X_IPC_DATA_MEM selects it (A/B).
+extern "C" int mp4x_ipc_alloc_data(size_t bytes, int coarse, void** ptr) {
+  if (!coarse) return mp4x_ipc_alloc(bytes, ptr);
+  hipError_t e = hipMalloc(ptr, bytes);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemset(*ptr, 0, bytes);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipDeviceSynchronize();
+}
+
 // Plain (coarse-grained) device allocation, the kind the PyTorch caching allocator makes: the
 // self-test of the zero-copy protocol runs on memory like the caller tensors it will map.
 extern "C" int mp4x_dev_alloc(size_t bytes, void** ptr) { return (int)hipMalloc(ptr, bytes); }

@@ -28,6 +28,7 @@ from ..ops.native import check, capturing_now, ptr_array, stream_ptr, c_int, c_i
 native.register_signatures({
     "mp4x_ipc_signal_bytes": (c_size_t, []),
     "mp4x_ipc_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
+    "mp4x_ipc_alloc_data": (c_int, [c_size_t, c_int, ctypes.POINTER(c_void_p)]),
     "mp4x_ipc_free": (c_int, [c_void_p]),
     "mp4x_host_word_alloc": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
     "mp4x_host_word_free": (c_int, [c_void_p]),
@@ -72,6 +73,8 @@ ONESHOT, TWOSHOT = 0, 1
 ZC_TAG = 0x80000000      # epoch tag of the zero-copy protocol (csrc/runtime/ipc.hip kZcTag)
 PUSH_TAG = 0x40000000    # ... and of its push form (kPushTag); host epochs use the low 30 bits
 PUSH_ON = os.environ.get("MP4X_IPC_PUSH", "1") == "1"
+# staging buffers: fine-grained uncached (default) or coarse-grained (MP4X_IPC_DATA_MEM=coarse, A/B)
+DATA_COARSE = os.environ.get("MP4X_IPC_DATA_MEM", "uncached").lower() == "coarse"
 # hipIpcOpenMemHandle of an allocation of 2^31 bytes or more never returns on this ROCm
 # (measured: 2.0 GB opens in 0.1 ms, 2 GiB hangs — profiles/r2/ipc_open_probe.jsonl), so
 # registration refuses such allocations (every rank alike): the staged kernels run instead.
@@ -144,7 +147,8 @@ class IpcAllreduce:
         # below: raising before it would leave the peers waiting there for this rank
         local_err = None
         try:
-            check(self.lib.mp4x_ipc_alloc(self.nbytes, ctypes.byref(self._data)), "ipc_alloc(data)")
+            check(self.lib.mp4x_ipc_alloc_data(self.nbytes, int(DATA_COARSE), ctypes.byref(self._data)),
+                  "ipc_alloc(data)")
             check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)),
                   "ipc_alloc(sig)")
             herr_dev = c_void_p()
@@ -206,6 +210,7 @@ class IpcAllreduce:
         # every rank's push scratch or None)
         self._regs = {}
         self._peer_bases = {}       # (rank, handle bytes) -> [mapped base, registrations using it]
+        self._vmm_pool = {}         # memAlloc size -> [freed registrations] (see mem_free)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -538,6 +543,15 @@ class IpcAllreduce:
         the push scratch the same way.  Raises on every rank when any rank failed."""
         from . import vmm
         nb16 = -(-int(nbytes) // 16) * 16
+        es = torch.empty((), dtype=dtype).element_size()
+        pooled = self._vmm_pool.get(nb16)
+        if pooled:
+            # a freed allocation of this size (the same one on every rank: pool states agree)
+            reg = pooled.pop()
+            own_va = reg.vmm[0].va
+            self._regs[(own_va, nb16)] = reg
+            t = vmm.tensor_at(own_va, nb16, torch.uint8, torch.device("cuda", self.device))
+            return t[:nbytes // es * es].view(dtype)
         own = scr = None
         err = None
         plan = None
@@ -605,7 +619,6 @@ class IpcAllreduce:
         reg.scratch = scratch if push else None
         t = vmm.tensor_at(own.va, nb16, torch.uint8, torch.device("cuda", self.device))
         self._regs[(own.va, nb16)] = reg
-        es = torch.empty((), dtype=dtype).element_size()
         return t[:nbytes // es * es].view(dtype)
 
     def mem_free(self, t: torch.Tensor) -> None:
@@ -621,7 +634,13 @@ class IpcAllreduce:
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # no peer kernel still reads or writes it
         reg = self._regs.pop(key)
-        self._release(reg)
+        # Not released here: unmapping + releasing VMM chunks (own and imported) and then
+        # exporting / importing new ones made the NEXT allocation's peer mappings read zeros on
+        # this ROCm (gfx950, 3 ranks: tools/vmm_realloc_probe.py, profiles/r3/vmm_realloc.txt).
+        # The allocation is parked in a per-size pool instead and handed out again by the next
+        # memAlloc of the same size (every rank's pool state is identical: alloc / free are
+        # collective), so an alloc/free loop does not grow; everything is released at close().
+        self._vmm_pool.setdefault(key[1], []).append(reg)
 
     def allreduce_push(self, view: torch.Tensor, op, peers, scratch, scale: float = 1.0) -> torch.Tensor:
         """In place, on registered tensors, with every xGMI transfer a posted WRITE (see
@@ -1279,9 +1298,11 @@ class IpcAllreduce:
             self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
-        for reg in list(getattr(self, "_regs", {}).values()):
+        pooled = [r for lst in getattr(self, "_vmm_pool", {}).values() for r in lst]
+        for reg in list(getattr(self, "_regs", {}).values()) + pooled:
             try:
                 self._release(reg)
             except Exception:   # noqa: BLE001 — best effort at teardown
                 pass
         self._regs = {}
+        self._vmm_pool = {}

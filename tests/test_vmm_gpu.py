@@ -36,14 +36,25 @@ def _alloc_allreduce_fn(comm, n, reps):
     reg = eng._ipc_obj._find(t)[0]
     info = (t.numel(), t.is_contiguous(), len(reg.vmm) if reg else 0)
     comm.memFree(t)
-    # the communicator still works, and a new allocation maps again
+    # the communicator still works, and a new allocation maps again (at the freed addresses)
     t2 = comm.memAlloc(1 << 20, torch.float32)
-    t2.fill_(1.0)
+    i2 = torch.arange(1 << 20, device="cuda", dtype=torch.int32) % 11
+    t2.copy_(i2 + r)
     comm.allreduceArray(t2, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, 1 << 20)
     torch.cuda.synchronize()
-    ok2 = bool((t2 == p).all())
+    exp2 = (i2 * p + p * (p - 1) // 2).float()
+    wrong = (t2 != exp2).nonzero().view(-1)
+    ok2 = (int(wrong.numel()), [(int(j), float(t2[j]), float(exp2[j])) for j in wrong[:4].tolist()])
+    ptr2 = t2.data_ptr()
     comm.memFree(t2)
-    return bad, used, info, ok2
+    # same size again: the pooled allocation comes back (every rank alike), still exact
+    t3 = comm.memAlloc(1 << 20, torch.float32)
+    t3.copy_(i2 + r)
+    comm.allreduceArray(t3, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, 1 << 20)
+    torch.cuda.synchronize()
+    ok3 = (t3.data_ptr() == ptr2, int((t3 != exp2).sum()))
+    comm.memFree(t3)
+    return bad, used, info, ok2 + ok3
 
 
 def test_memalloc_above_2gib_zero_copy_exact():
@@ -53,7 +64,7 @@ def test_memalloc_above_2gib_zero_copy_exact():
         assert bad == [0, 0], (r, bad)
         assert used.get("allreduce.ipc2z", 0) == 2, used
         assert info[0] == n and info[1], info
-        assert ok2
+        assert ok2[0] == 0 and ok2[2] and ok2[3] == 0, (r, ok2)
 
 
 def test_memalloc_many_chunks():
@@ -63,7 +74,7 @@ def test_memalloc_many_chunks():
         assert bad == [0, 0], (r, bad)
         assert used.get("allreduce.ipc2z", 0) == 2, used
         assert info[2] >= 2 + 2 * 2, info       # own + scratch + two peers' tensor + scratch
-        assert ok2
+        assert ok2[0] == 0 and ok2[2] and ok2[3] == 0, (r, ok2)
 
 
 def _zero_fn(comm, n):
