@@ -147,6 +147,7 @@ class DeviceEngine:
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
+        self._tune_scratch: Dict[tuple, torch.Tensor] = {}   # autotune_allreduce scratch per (dtype, numel)
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
         self._select_tuned = False
         self._load_shared_tuning(shared=coll is None)
@@ -747,7 +748,14 @@ class DeviceEngine:
         the same shape; the decision uses the MAX time over ranks, so all ranks agree.
 
         Returns {algo: seconds per call} (inf for a schedule that failed on any rank)."""
-        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        # one scratch tensor per (dtype, size), kept: a re-tune of the same class registers the
+        # same allocation again, whose peer mappings are cached (ipc.IpcAllreduce._open_peer_base)
+        key = (like.dtype, like.numel())
+        view = self._tune_scratch.get(key)
+        if view is None:
+            view = self._tune_scratch[key] = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
+        else:
+            view.zero_()
         op = self._op(operator, view)
         nbytes = view.numel() * view.element_size()
         if candidates is None and os.environ.get("MP4X_AUTOTUNE_CANDIDATES"):

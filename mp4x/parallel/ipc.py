@@ -96,15 +96,13 @@ def _set_spin(lib) -> None:
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "opened", "peer_keys", "scratch_alloc", "vmm")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
         self.scratch = None
         self.keep = keep                 # the registered tensor: its memory stays allocated
-        self.opened: List[c_void_p] = []  # scratch mappings of the peers
-        self.peer_keys: list = []        # refcounted entries of IpcAllreduce._peer_bases
-        self.scratch_alloc = None        # own push scratch (hipExtMallocWithFlags)
+        self.scratch_alloc = None        # own push scratch: (allocation, IPC handle bytes)
         self.vmm: list = []              # memAlloc: own + imported VmmRegions
 
 
@@ -209,7 +207,9 @@ class IpcAllreduce:
         # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> (peer pointers,
         # every rank's push scratch or None)
         self._regs = {}
-        self._peer_bases = {}       # (rank, handle bytes) -> [mapped base, registrations using it]
+        self._peer_bases = {}       # (rank, handle bytes) -> mapped address (opened once)
+        self._scratch_pool = {}     # push-scratch bytes -> [(allocation, handle)] free for reuse
+        self._scratch_size = {}     # push-scratch address -> bytes
         self._vmm_pool = {}         # memAlloc size -> [freed registrations] (see mem_free)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
@@ -393,7 +393,8 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_get_handle(base, h), "ipc_get_handle(registered)")
             scr_h = None
             if PUSH_ON and not ok_local:
-                scr_alloc, scr_h = self._alloc_scratch(key[1], hs)
+                scr_alloc = self._alloc_scratch(key[1], hs)
+                scr_h = scr_alloc[1]
             blob = (h.raw, t.data_ptr() - base.value, key[1], ok_local, scr_h)
         except Exception as e:   # noqa: BLE001 — travels in the allgather: every rank decides together
             err = str(e)
@@ -416,17 +417,12 @@ class IpcAllreduce:
                 if r == self.rank:
                     reg.peers.append(t.data_ptr())
                     if push:
-                        scr.append(scr_alloc.value)
+                        scr.append(scr_alloc[0].value)
                     continue
                 hk = (r, bytes(b[0]))
                 reg.peers.append(self._open_peer_base(hk, hs) + int(b[1]))
-                reg.peer_keys.append(hk)
                 if push:
-                    q = c_void_p()
-                    check(self.lib.mp4x_ipc_open_handle(ctypes.create_string_buffer(bytes(b[4]), hs),
-                                                        ctypes.byref(q)), f"ipc_open_handle(scratch, rank {r})")
-                    reg.opened.append(q)
-                    scr.append(q.value)
+                    scr.append(self._open_peer_base((r, bytes(b[4])), hs))
         except Exception as e:   # noqa: BLE001
             err = str(e)
         reg.scratch = scr if push else None
@@ -439,23 +435,29 @@ class IpcAllreduce:
         return True
 
     def _open_peer_base(self, hk, hs: int) -> int:
-        """Mapped base of peer allocation ``hk`` = (rank, handle bytes): one open per allocation,
-        reference-counted over the registrations that use it."""
+        """Mapped address of peer allocation ``hk`` = (rank, handle bytes): opened once, cached
+        until close().  Mappings are never closed early: closing one and later opening a new
+        allocation handed out at recycled addresses made the new mapping read the wrong memory
+        on this ROCm (tests/test_ipc_zc_gpu.py push form at p = 4, tools/vmm_realloc_probe.py)."""
         ent = self._peer_bases.get(hk)
         if ent is None:
             hb = ctypes.create_string_buffer(hk[1], hs)
             ptr = c_void_p()
-            check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(registered, rank {hk[0]})")
-            ent = self._peer_bases[hk] = [ptr, 0]
-        ent[1] += 1
-        return ent[0].value
+            check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(rank {hk[0]})")
+            ent = self._peer_bases[hk] = ptr
+        return ent.value
 
     def _alloc_scratch(self, nbytes: int, hs: int):
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
         slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
-        (allocation, IPC handle), or (None, None): the registration then has no push form."""
+        (allocation, IPC handle), or (None, None): the registration then has no push form.
+        A scratch of the same size that an earlier deregistration returned is reused (the peers'
+        mappings of it are cached by handle, so nothing is re-opened)."""
         chunk = -(-(nbytes // 16) // self.p)
         size = max(16, (self.p - 1) * chunk * 16)
+        pooled = self._scratch_pool.get(size)
+        if pooled:
+            return pooled.pop()
         ptr = c_void_p()
         try:
             if size > IPC_OPEN_MAX:
@@ -467,26 +469,18 @@ class IpcAllreduce:
             if ptr:
                 self.lib.mp4x_ipc_free(ptr)
             return None, None
+        self._scratch_size[ptr.value] = size
         return ptr, h.raw
 
-    def _free_scratch(self, ptr) -> None:
-        if ptr:
-            self.lib.mp4x_ipc_free(ptr)
+    def _free_scratch(self, scr) -> None:
+        """Back to the per-size pool (freed at close())."""
+        if scr and scr[0]:
+            self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
     def _release(self, reg: "_Reg") -> None:
-        """Close every mapping ``reg`` opened and free its scratch (after the caller's stream
-        work on them is done)."""
-        for q in reg.opened:
-            self.lib.mp4x_ipc_close_handle(q)
-        reg.opened = []
-        for hk in reg.peer_keys:
-            ent = self._peer_bases.get(hk)
-            if ent is not None:
-                ent[1] -= 1
-                if ent[1] <= 0:
-                    self.lib.mp4x_ipc_close_handle(ent[0])
-                    del self._peer_bases[hk]
-        reg.peer_keys = []
+        """Return ``reg``'s scratch to the pool and drop its tensor reference (peer mappings stay
+        cached, see :meth:`_open_peer_base`); memAlloc regions are unmapped and released (only
+        at close(), see :meth:`mem_free`)."""
         self._free_scratch(reg.scratch_alloc)
         reg.scratch_alloc = None
         for region in reversed(reg.vmm):     # the peers' imported views first, own memory last
@@ -495,17 +489,15 @@ class IpcAllreduce:
         reg.keep = None
 
     def deregister(self, t: torch.Tensor) -> None:
-        """Forget ``t`` and release what its registration holds on THIS rank: the mappings of
-        the peers' allocations, the push scratch, the reference to ``t``.  Every peer
-        deregisters its tensor at the same point (the registration contract), so no peer
-        kernel uses them afterwards; the local stream is drained first."""
-        reg = self._regs.pop((t.data_ptr(), t.numel() * t.element_size()), None)
-        if reg is None:
+        """Forget ``t``: its push scratch goes back to a per-size pool for the next registration
+        and the reference to ``t`` is dropped.  Every peer deregisters its tensor at the same
+        point (the registration contract); the local stream is drained first.  A memAlloc tensor
+        stays registered until memFree."""
+        key = (t.data_ptr(), t.numel() * t.element_size())
+        reg = self._regs.get(key)
+        if reg is None or reg.vmm:
             return
-        if reg.vmm:
-            # memAlloc'ed: its memory is freed by mem_free (collective), not here
-            self._regs[(t.data_ptr(), t.numel() * t.element_size())] = reg
-            return
+        del self._regs[key]
         torch.cuda.synchronize(self.device)
         self._release(reg)
 
@@ -1298,6 +1290,9 @@ class IpcAllreduce:
             self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
+        for ptr in getattr(self, "_peer_bases", {}).values():
+            self.lib.mp4x_ipc_close_handle(ptr)
+        self._peer_bases = {}
         pooled = [r for lst in getattr(self, "_vmm_pool", {}).values() for r in lst]
         for reg in list(getattr(self, "_regs", {}).values()) + pooled:
             try:
@@ -1306,3 +1301,7 @@ class IpcAllreduce:
                 pass
         self._regs = {}
         self._vmm_pool = {}
+        for lst in getattr(self, "_scratch_pool", {}).values():
+            for ptr, _ in lst:
+                self.lib.mp4x_ipc_free(ptr)
+        self._scratch_pool = {}

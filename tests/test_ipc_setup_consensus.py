@@ -55,6 +55,9 @@ class _FakeLib:
         out._obj.value = 0x1000
         return 0
 
+    def mp4x_ipc_alloc_data(self, nbytes, coarse, out):
+        return self.mp4x_ipc_alloc(nbytes, out)
+
     def mp4x_ipc_get_handle(self, ptr, buf):
         return 0
 
