@@ -41,8 +41,20 @@ def body(comm, nkeys, dim, iters, fresh):
     base = torch.randn(nkeys, dim, device=dev, generator=torch.Generator(device=dev).manual_seed(r))
     keys = [f"f{i}" for i in range(nkeys // 2)] + [f"r{r}_{i}" for i in range(nkeys - nkeys // 2)]
     m = dict(zip(keys, base.unbind(0)))
-    out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)      # numbering round (first call)
+    comm.device                                                    # communicator bootstrap, untimed
+    comm.barrier()
+    t0 = time.perf_counter()
+    out = comm.allreduceMap(m, Operands.FLOAT_OPERAND(), op)      # first call: every key is new
+    torch.cuda.synchronize()
+    first_total = time.perf_counter() - t0
     assert len(out) == nkeys // 2 + p * (nkeys - nkeys // 2)
+    # the agreement round alone for a dict of ALL-new keys (the key-dictionary round of a first call)
+    m_new = dict(zip([f"n{r}_{i}" for i in range(nkeys)], base.unbind(0)))
+    comm.barrier()
+    t0 = time.perf_counter()
+    assert comm._map_on_device(m_new)
+    first_agree = time.perf_counter() - t0
+    comm.device._keys_presynced = False
     ph = {"total": [], "walk_only": [], "agree": [], "to_tensors": [], "exchange_and_kernels": [], "to_dict": []}
     rows_list = list(m.values())
     for _ in range(iters):
@@ -80,7 +92,10 @@ def body(comm, nkeys, dim, iters, fresh):
         for name, dt in (("total", t1 - t0), ("walk_only", walk), ("agree", b - a), ("to_tensors", c - b),
                          ("exchange_and_kernels", d - c), ("to_dict", e - d)):
             ph[name].append(dt)
-    return {k: sorted(v)[len(v) // 2] for k, v in ph.items()}
+    res = {k: sorted(v)[len(v) // 2] for k, v in ph.items()}
+    res["first_call_total"] = first_total
+    res["first_call_agree_new_keys"] = first_agree
+    return res
 
 
 def main():
@@ -97,7 +112,9 @@ def main():
     rec = {"config": f"allreduceMap Dict[str, float[{a.dim}]] {a.keys} keys/rank (50% shared)",
            "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)",
            "dict_per_call": "fresh" if a.fresh_dict else "same (walk cached by PEP 509 version tag)"}
-    for k in ("total", "walk_only", "agree", "to_tensors", "exchange_and_kernels", "to_dict"):
+    rec["keys_via"] = "master" if os.environ.get("MP4X_KEYS_VIA_MASTER") == "1" else "peer-to-peer host mesh"
+    for k in ("first_call_total", "first_call_agree_new_keys", "total", "walk_only", "agree", "to_tensors",
+              "exchange_and_kernels", "to_dict"):
         rec[f"{k}_ms_max_rank"] = round(max(v[k] for v in res.values()) * 1e3, 2)
     print(json.dumps(rec), flush=True)
 

@@ -721,8 +721,20 @@ class DeviceEngine:
             return not getattr(op, "is_custom", False)
         return algo == "a2a"
 
+    def _stand_in(self) -> bool:
+        """gloo standing in for RCCL on GPU tensors (the one-GPU rehearsals): its device paths stage
+        through host memory and, with 4-8 processes on one GPU, leave every later barrier kernel
+        time-sliced (~70-100 ms per call at any size, profiles/r3/round/rehearsal_np8.jsonl), so
+        the autotuners skip the transport candidates when IPC ones exist
+        (``MP4X_AUTOTUNE_GLOO=1`` keeps them).  Never true with RCCL underneath."""
+        return self.backend == "gloo" and self.device.type == "cuda" and self.ipc_enabled and \
+            os.environ.get("MP4X_AUTOTUNE_GLOO", "0") != "1"
+
     def allreduce_candidates(self, nbytes: int, op, dtype) -> List[str]:
         c = []
+        if self._stand_in() and self._ipc_ok(op, dtype, nbytes):
+            return (["ipc1"] if nbytes <= (4 << 20) else []) + ["ipc2"] + \
+                (["ipc2p"] if nbytes > self.ipc_twoshot_max else []) + (["ipc2z", "ipc2w"] if self._zc else [])
         if self.rccl_ok(op, dtype):
             c.append("rccl")
             if self.backend == "nccl" and nbytes >= (64 << 20):
@@ -799,6 +811,8 @@ class DeviceEngine:
         op = self._op(operator, view)
         froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
         cands = ["rccl", "a2a"] + (["ipc"] if self.ipc_enabled and self._ipc_ok(op, view.dtype, 16) else [])
+        if self._stand_in() and "ipc" in cands:
+            cands = ["ipc"]
         r = self.rank
 
         def probe():
@@ -820,6 +834,9 @@ class DeviceEngine:
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
         cands = ["rccl", "p2p"] + (["ipc"] if self.ipc_enabled else [])
+        if self._stand_in():
+            cands = ["ipc"]
+
         def probe():
             # owner j's segment holds i % 97 + j; after the call every rank holds every segment
             idt = torch.int32 if view.numel() < (1 << 31) else torch.int64
@@ -887,7 +904,7 @@ class DeviceEngine:
         nb = view.numel() * view.element_size()
         cands = (["rccl"] if self.rccl_ok(op, view.dtype) else []) + ["a2a"]
         if self.ipc_enabled and self._ipc_ok(op, view.dtype, nb):
-            cands.append("ipc")
+            cands = ["ipc"] if self._stand_in() else cands + ["ipc"]
         n = view.numel()
 
         def probe():
@@ -920,6 +937,8 @@ class DeviceEngine:
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         n = view.numel()
         cands = ["rccl", "composite"] + (["ipc"] if self.ipc_enabled and view.is_cuda else [])
+        if self._stand_in():
+            cands = ["ipc"]
 
         def probe():
             exp = self._copy_probe(view, [(0, n, root)])
@@ -937,6 +956,8 @@ class DeviceEngine:
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         froms, tos, _ = CommUtils.even_split(0, view.numel(), self.p)
         cands = ["p2p"] + (["ipc"] if self.ipc_enabled and view.is_cuda else [])
+        if self._stand_in():
+            cands = ["ipc"]
         r = self.rank
 
         def probe():

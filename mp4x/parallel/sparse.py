@@ -113,6 +113,8 @@ def allgather_keys(engine, new: List) -> List[List]:
     ranks, the control plane only when neither exists."""
     if hasattr(engine.coll, "_exchange"):
         return engine.coll._exchange(list(new))
+    if os.environ.get("MP4X_KEYS_VIA_MASTER") == "1":     # the round-2 path, kept for A/B records
+        return engine.all_gather_object(list(new))
     host = getattr(engine.comm, "engine", None)
     if host is not None and hasattr(host, "allgather_bytes"):
         return [decode_keys(b) for b in host.allgather_bytes(encode_keys(new))]
