@@ -68,11 +68,16 @@ class KeyDictionary:
 
     def learn_round(self, proposals) -> None:
         """Number the union of one sync round's proposals (every rank passes the same list)."""
-        for block in proposals:
-            for k in block or ():
-                if k not in self.key2id:
-                    self.key2id[k] = len(self.id2key)
-                    self.id2key.append(k)
+        # C-level passes only (a first call numbers ~1M keys): order-preserving union of the
+        # blocks, drop the known keys, number the rest in that order
+        union = dict.fromkeys(itertools.chain.from_iterable(b for b in proposals if b))
+        if self.key2id:
+            new = [k for k in union if k not in self.key2id]
+        else:
+            new = list(union)
+        base = len(self.id2key)
+        self.key2id.update(zip(new, range(base, base + len(new))))
+        self.id2key.extend(new)
 
     def ids(self, keys) -> List[int]:
         return [self.key2id[k] for k in keys]
