@@ -282,7 +282,13 @@ class ProcessCommSlave:
         dtype = dtype or torch.float32
         want_dev = device is None or str(device).startswith("cuda")
         if self.slaveNum > 1 and want_dev and torch.cuda.is_available():
-            t = self.device.mem_alloc(int(n), dtype)
+            try:
+                t = self.device.mem_alloc(int(n), dtype)
+            except Mp4jException as e:
+                # agreed on every rank inside mem_alloc (the failure travels in its collectives),
+                # so every rank falls back together: a plain tensor on the staged kernels / RCCL
+                LOG.warning("memAlloc(%d) fell back to a plain tensor: %s", int(n), e)
+                t = None
             if t is not None:
                 return t
         dev = device or ("cuda" if torch.cuda.is_available() else "cpu")

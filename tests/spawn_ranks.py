@@ -26,7 +26,14 @@ def device_plan(p, ndev, mode="shared"):
         raise ValueError(f"multi-GPU plan needs {p} GPUs, the box has {ndev}")
     if multi:
         return "multi", {"MP4X_DEVICE_BACKEND": "nccl", "MP4X_WATCHDOG": "0"}
-    return "shared", {"MP4X_DEVICE_BACKEND": "gloo", "MP4X_DEVICE_INDEX": "0", "MP4X_WATCHDOG": "0"}
+    env = {"MP4X_DEVICE_BACKEND": "gloo", "MP4X_DEVICE_INDEX": "0", "MP4X_WATCHDOG": "0"}
+    if p > 4:
+        # p processes x 4 hardware queues each oversubscribe one GPU's queue slots beyond 4
+        # ranks: the scheduler then time-slices the queues and every barrier kernel waits a
+        # slice (8 ranks: 32 ms per 256 MiB allreduce with 4 queues each, 1.4 ms with 2:
+        # profiles/r3/round/rehearsal_np8_queues.jsonl).  One process per GPU never needs this.
+        env["GPU_MAX_HW_QUEUES"] = "2"
+    return "shared", env
 
 
 def rank_device(plan, rank):

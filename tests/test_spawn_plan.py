@@ -9,6 +9,8 @@ def test_shared_plan_is_the_default():
     assert plan == "shared"
     assert env["MP4X_DEVICE_BACKEND"] == "gloo" and env["MP4X_DEVICE_INDEX"] == "0"
     assert [rank_device(plan, r) for r in range(4)] == [0, 0, 0, 0]
+    assert "GPU_MAX_HW_QUEUES" not in env                      # 4 ranks x 4 queues fit
+    assert device_plan(8, 1)[1]["GPU_MAX_HW_QUEUES"] == "2"     # 8 ranks share the queue slots
 
 
 @pytest.mark.parametrize("p,ndev,plan", [(2, 8, "multi"), (8, 8, "multi"), (8, 4, "shared"), (2, 1, "shared"),
