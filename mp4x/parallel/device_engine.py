@@ -144,6 +144,8 @@ class DeviceEngine:
         self._ipc_obj = None
         self._ipc_large = None
         self._ipc_large_failed = False   # set on every rank together (setup failure is collective)
+        self._ipc_fp8_big = None         # whole-tensor fp8 staging (see _ipc_fp8_whole)
+        self._ipc_fp8_big_failed = False
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = {}
@@ -212,7 +214,7 @@ class DeviceEngine:
         """Fail-stop teardown (``ncclCommAbort``): a rank blocked in a collective with a dead
         peer returns instead of hanging.  Called by ``ProcessCommSlave.close(code != 0)``."""
         self._stop_watchdog()
-        for name in ("_ipc_obj", "_ipc_large"):
+        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big"):
             setattr(self, name, None)          # peers may be gone: no synchronising close
         if self._owns_pg and dist.is_initialized():
             try:
@@ -235,7 +237,7 @@ class DeviceEngine:
 
     def shutdown(self):
         self._stop_watchdog()
-        for name in ("_ipc_obj", "_ipc_large"):
+        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big"):
             obj = getattr(self, name)
             if obj is not None:
                 try:
@@ -515,7 +517,7 @@ class DeviceEngine:
         pipelined pieces / sparse)."""
         if self.device.type != "cuda":
             raise Mp4jException("capture needs a GPU device engine")
-        for inst in (self.ipc(), self._ipc_large):
+        for inst in (self.ipc(), self._ipc_large, self._ipc_fp8_big):
             if inst is not None:
                 inst.prepare_graph()
         side = torch.cuda.Stream(device=self.device)
@@ -526,7 +528,7 @@ class DeviceEngine:
         torch.cuda.current_stream(self.device).wait_stream(side)
         self._sync()
         # the warm-up may have created the large-message instance: it needs device epochs too
-        for inst in (self._ipc_obj, self._ipc_large):
+        for inst in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big):
             if inst is not None:
                 inst.prepare_graph()
         self.barrier()
@@ -704,9 +706,41 @@ class DeviceEngine:
             return None
         if self.ipc() is None or not self._ipc_obj.fp8_ok(view):
             return None
-        inst = self._ipc_obj if view.numel() * 260 // 256 <= self._ipc_obj.nbytes else self.ipc_large()
-        if torch.cuda.is_current_stream_capturing() and (inst is None or inst._epoch_dev is None):
+        need = view.numel() * 260 // 256 + (64 << 10)          # e4m3 bytes + scales of the whole tensor
+        capturing = torch.cuda.is_current_stream_capturing()
+        if need <= self._ipc_obj.nbytes:
+            inst = self._ipc_obj
+        elif capturing or os.environ.get("MP4X_FP8_ONE_PIECE", "1") != "1":
+            inst = self.ipc_large()
+        else:
+            inst = self._ipc_fp8_whole(need)
+        if capturing and (inst is None or inst._epoch_dev is None):
             return None
+        return inst
+
+    def _ipc_fp8_whole(self, need: int):
+        """An IPC instance whose staging buffer holds a whole fp8-quantised tensor, so the fused
+        fp8 two-shot runs as ONE piece at any size (BASELINE config 5: 8 GB of f32 -> ~2 GB of
+        e4m3 + scales, above the IPC open limit: a VMM-built buffer, ``IpcAllreduce._vmm_data``).
+        Grown on demand (collective: every rank asks for the same size at the same call), kept."""
+        inst = self._ipc_fp8_big
+        if inst is not None and inst.nbytes >= need:
+            return inst
+        if self._ipc_fp8_big_failed:
+            return self.ipc_large()
+        try:
+            if inst is not None:
+                inst.close()
+            from .ipc import IpcAllreduce
+            inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8")
+            if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
+                inst.prepare_graph()
+        except Exception as e:   # noqa: BLE001 — setup failures are agreed inside IpcAllreduce
+            LOG.warning("whole-tensor fp8 IPC buffer disabled: %s", e)
+            self._ipc_fp8_big_failed = True
+            self._ipc_fp8_big = None
+            return self.ipc_large()
+        self._ipc_fp8_big = inst
         return inst
 
     # ------------------------------------------------------------------ autotuning
@@ -1155,7 +1189,7 @@ class DeviceEngine:
 
     def _ipc_error_local(self) -> int:
         mine = 0
-        for inst in (self._ipc_obj, self._ipc_large):
+        for inst in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big):
             # read-and-clear: a candidate that timed out must not poison the next one's check
             if inst is not None and inst.error_word(clear=True):
                 mine = 1

@@ -141,12 +141,27 @@ class IpcAllreduce:
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
+        # a staging buffer above the IPC open limit is built like a memAlloc tensor (VMM chunks,
+        # dmabuf fds to the peers): rank-independent (the size is the same on every rank)
+        self._vmm_data = self.nbytes > IPC_OPEN_MAX
+        self._data_regions: list = []     # VMM data buffer: own region + imported peer regions
         # a local failure here (out of memory, no IPC support) must still reach the allgather
         # below: raising before it would leave the peers waiting there for this rank
         local_err = None
         try:
-            check(self.lib.mp4x_ipc_alloc_data(self.nbytes, int(DATA_COARSE), ctypes.byref(self._data)),
-                  "ipc_alloc(data)")
+            if self._vmm_data:
+                from . import vmm
+                g = ctypes.c_size_t()
+                check(self.lib.mp4x_vmm_granularity(ctypes.byref(g)), "vmm_granularity")
+                chunk, nch = vmm.chunk_plan(self.nbytes, g.value)
+                own = vmm.VmmRegion.create(self.lib, chunk, nch)
+                self._data_regions.append(own)
+                self._data = c_void_p(own.va)
+                check(self.lib.mp4x_memset_async(own.va, 0, self.nbytes, None), "vmm data zero")
+                torch.cuda.synchronize()
+            else:
+                check(self.lib.mp4x_ipc_alloc_data(self.nbytes, int(DATA_COARSE), ctypes.byref(self._data)),
+                      "ipc_alloc(data)")
             check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)),
                   "ipc_alloc(sig)")
             herr_dev = c_void_p()
@@ -154,7 +169,8 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_set_host_error(self._sig, herr_dev), "ipc_set_host_error")
             hd = ctypes.create_string_buffer(hs)
             hsg = ctypes.create_string_buffer(hs)
-            check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
+            if not self._vmm_data:
+                check(self.lib.mp4x_ipc_get_handle(self._data, hd), "ipc_get_handle(data)")
             check(self.lib.mp4x_ipc_get_handle(self._sig, hsg), "ipc_get_handle(sig)")
             pci = ctypes.create_string_buffer(64)
             check(self.lib.mp4x_device_pci_id(pci, 64), "device_pci_id")
@@ -176,6 +192,15 @@ class IpcAllreduce:
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
         err = None
+        got = {}
+        if self._vmm_data:
+            from . import vmm
+            try:
+                got = vmm.exchange_fds(comm.server, self.rank, self.p, self._data_regions[0].fds)   # collective
+            except Exception:
+                self.close(sync=False)
+                raise
+            self._data_regions[0].close_fds()
         try:
             for r, blob in enumerate(allh):
                 if r == self.rank:
@@ -183,6 +208,16 @@ class IpcAllreduce:
                     self.sig_ptrs.append(self._sig.value)
                     continue
                 for i, lst in ((0, self.data_ptrs), (1, self.sig_ptrs)):
+                    if i == 0 and self._vmm_data:
+                        own = self._data_regions[0]
+                        try:
+                            pr = vmm.VmmRegion.import_fds(self.lib, got[r], own.chunk)
+                        finally:
+                            for fd in got[r]:
+                                os.close(fd)
+                        self._data_regions.append(pr)
+                        lst.append(pr.va)
+                        continue
                     h = ctypes.create_string_buffer(bytes(blob[i * hs:(i + 1) * hs]), hs)   # pci id follows
                     ptr = c_void_p()
                     check(self.lib.mp4x_ipc_open_handle(h, ctypes.byref(ptr)), f"ipc_open_handle(rank {r})")
@@ -1280,9 +1315,15 @@ class IpcAllreduce:
         for ptr in self._opened:
             self.lib.mp4x_ipc_close_handle(ptr)
         self._opened = []
-        if self._data:
+        if self._data and not getattr(self, "_vmm_data", False):
             self.lib.mp4x_ipc_free(self._data)
-            self._data = c_void_p()
+        self._data = c_void_p()
+        for region in reversed(getattr(self, "_data_regions", [])):   # imported views first
+            try:
+                region.free()
+            except Exception:   # noqa: BLE001 — best effort at teardown
+                pass
+        self._data_regions = []
         if self._sig:
             self.lib.mp4x_ipc_free(self._sig)
             self._sig = c_void_p()

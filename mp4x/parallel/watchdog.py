@@ -162,7 +162,7 @@ class CollectiveWatchdog:
         eng = self.engine
         if eng is None:
             return 0
-        for name in ("_ipc_obj", "_ipc_large"):
+        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big"):
             inst = getattr(eng, name, None)
             if inst is not None:
                 w = inst.error_word(clear=self.action == "log")

@@ -107,3 +107,33 @@ def test_memalloc_zero_rs_ag_bf16():
     for r, (bad_rs, bad_ag, used) in out.items():
         assert bad_rs == 0 and bad_ag == 0, (r, bad_rs, bad_ag, used)
         assert used.get("reduce_scatter.ipc_zc") == 1 and used.get("allgather.ipc_zc") == 1, used
+
+
+def _fp8_whole_fn(comm, n):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+
+    def gen(j):
+        return torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(7 + j))
+    x = gen(r)
+    comm.allreduceArray(x, Operands.FLOAT_OPERAND(codec="fp8"), Operators.Float.SUM, 0, n)
+    torch.cuda.synchronize()
+    idx = torch.arange(0, n, 997, device="cuda")          # strided sample vs the fp64 sum
+    ref = sum(gen(j)[idx].double() for j in range(p))
+    mag = sum(gen(j)[idx].double().abs() for j in range(p))
+    err = (x[idx].double() - ref).abs()
+    nbad = int((err > (mag + ref.abs()) / 8 + 1e-3).sum())
+    big = eng._ipc_fp8_big
+    return nbad, dict(eng.stats), (big is not None and big._vmm_data, big.nbytes if big else 0)
+
+
+def test_fp8_whole_tensor_staging_built_from_vmm():
+    # the open limit lowered to 64 MiB so a ~85 MB quantised tensor needs the VMM-built staging
+    # buffer (the path BASELINE config 5, 8 GB of f32 -> 2 GB of e4m3, takes at the real limit)
+    n = 80 << 20
+    out = run_spawn(2, _fp8_whole_fn, args=(n,), env={"MP4X_IPC_OPEN_MAX": str(64 << 20)})
+    for r, (nbad, stats, (is_vmm, nb)) in out.items():
+        assert nbad == 0, (r, nbad)
+        assert stats.get("allreduce.fp8.ipc", 0) == 1, stats
+        assert is_vmm and nb >= n * 260 // 256, (is_vmm, nb)
