@@ -143,3 +143,117 @@ def test_native_load_failure_before_first_collective_raises_on_every_rank(monkey
         t.join(20)
     assert not any(t.is_alive() for t in threads), "a rank is stuck waiting for its peers"
     assert all(e is not None and "setup failed on ranks [(2," in e for e in errors), errors
+
+
+class _CountingLib(_FakeLib):
+    """Fake native library that hands out distinct addresses and counts opens / closes / frees."""
+
+    def __init__(self):
+        super().__init__(lambda: False)
+        self.next = 0x10000
+        self.opens = 0
+        self.closes = 0
+        self.allocs = 0
+        self.lock = threading.Lock()
+
+    def _addr(self):
+        with self.lock:
+            self.next += 0x100000
+            return self.next
+
+    def mp4x_ipc_alloc(self, nbytes, out):
+        with self.lock:
+            self.allocs += 1
+        out._obj.value = self._addr()
+        return 0
+
+    def mp4x_ipc_get_handle(self, ptr, buf):
+        v = ptr.value if hasattr(ptr, "value") else int(ptr)
+        buf.raw = v.to_bytes(8, "little")
+        return 0
+
+    def mp4x_ipc_open_handle(self, h, out):
+        with self.lock:
+            self.opens += 1
+        out._obj.value = self._addr()
+        return 0
+
+    def mp4x_ipc_close_handle(self, ptr):
+        with self.lock:
+            self.closes += 1
+        return 0
+
+    def mp4x_mem_range(self, ptr, base, size):
+        base._obj.value = ptr.value
+        size._obj.value = 1 << 20
+        return 0
+
+
+class _FakeTensor:
+    is_cuda = True
+
+    def __init__(self, ptr, nbytes):
+        self.ptr, self.nbytes = ptr, nbytes
+
+    def is_contiguous(self):
+        return True
+
+    def data_ptr(self):
+        return self.ptr
+
+    def numel(self):
+        return self.nbytes // 4
+
+    def element_size(self):
+        return 4
+
+
+def test_registration_lifecycle_pools_scratch_and_keeps_mappings(monkeypatch):
+    """deregister() returns the push scratch to a per-size pool and keeps peer mappings cached
+    (closing + re-opening recycled addresses mapped the wrong memory on ROCm); a registration
+    holds its tensor; close() frees / closes everything."""
+    p = 2
+    lib = _CountingLib()
+    monkeypatch.setattr(ipc_mod.native, "hip", lambda: lib)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "synchronize", lambda *a, **k: None)
+    server = _Server(p)
+    res = [None] * p
+
+    def run(r):
+        inst = ipc_mod.IpcAllreduce(_Comm(server, r), nbytes=1 << 16)
+        base_allocs, base_opens = lib.allocs, lib.opens
+        server.call("barrier", r)
+        a = _FakeTensor(0x7000000 + r * 0x1000000, 1 << 16)
+        b = _FakeTensor(0x7100000 + r * 0x1000000, 1 << 16)
+        ok1 = inst.register(a)
+        keeps = inst._find(a)[0].keep is a
+        inst.deregister(a)
+        server.call("barrier", r)
+        allocs_after_first = lib.allocs
+        ok2 = inst.register(b)                       # same size: the pooled scratch comes back
+        server.call("barrier", r)
+        reused = lib.allocs == allocs_after_first
+        inst.deregister(b)
+        ok3 = inst.register(a)                       # a again: its peer mapping is cached
+        server.call("barrier", r)
+        closes_before = lib.closes
+        inst.deregister(a)
+        server.call("barrier", r)
+        res[r] = (ok1, ok2, ok3, keeps, reused, closes_before, lib.allocs - base_allocs, inst)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(p)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(20)
+    assert not any(t.is_alive() for t in threads)
+    for ok1, ok2, ok3, keeps, reused, closes_before, allocs, inst in res:
+        assert ok1 and ok2 and ok3 and keeps and reused
+        assert closes_before == 0                    # nothing closed while the job runs
+        assert allocs <= p                           # one push scratch per rank, reused
+        assert not inst._regs
+    opens = lib.opens
+    for *_, inst in res:
+        inst.close(sync=False)
+    assert lib.closes >= opens                      # every mapping closed at close()
