@@ -215,13 +215,138 @@ def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
     return x[idx]
 
 
+# ------------------------------------------------------------------ IPC data plane for the sparse path
+# The ragged exchanges of the map collectives as ONE copy-plan kernel each over the IPC mesh
+# (csrc/runtime/ipc.hip k_ipc_copy_plan): keys and rows travel together as fixed-width records
+# (row bytes | int64 key | 8 pad bytes, a 16-byte multiple).  All-to-all-v: every rank stages
+# its owner-sorted records into its own IPC buffer, one stage item per destination, and pulls
+# its block from every peer at once (every xGMI link busy; no RCCL all_to_all).  All-gather-v:
+# every rank stages its owned result and pulls every peer's.  The grid is sized from the full
+# count matrix, which every rank knows, so every rank launches the same grid.
+_SPARSE_IPC = os.environ.get("MP4X_SPARSE_IPC", "1") == "1"
+
+
+def _rec_width(vals: Optional[torch.Tensor]) -> int:
+    """Record bytes (row bytes + 16), or 0 when rows are not a whole number of 16-byte vectors."""
+    rb = 0 if vals is None else int(np.prod(vals.shape[1:], dtype=np.int64)) * vals.element_size()
+    return rb + 16 if rb % 16 == 0 else 0
+
+
+def _ipc_inst(engine, need_bytes: int):
+    """The IPC instance whose staging buffer fits ``need_bytes`` (rank-independent), or None."""
+    if need_bytes <= engine._ipc_obj.nbytes:
+        return engine._ipc_obj
+    big = engine.ipc_large()
+    return big if big is not None and need_bytes <= big.nbytes else None
+
+
+def _sparse_ipc_ok(engine, keys: torch.Tensor) -> bool:
+    """Rank-independent: environment, device kind, capture state and the mesh."""
+    from ..ops.native import capturing_now
+    return _SPARSE_IPC and keys.is_cuda and getattr(engine, "ipc_enabled", False) and \
+        engine.coll.__class__.__name__ == "TorchColl" and not capturing_now() and engine.ipc() is not None
+
+
+def _pack_records(keys: torch.Tensor, vals: Optional[torch.Tensor], wb: int) -> torch.Tensor:
+    n = keys.shape[0]
+    rec = torch.empty((n, wb), dtype=torch.uint8, device=keys.device)
+    rb = wb - 16
+    if n == 0:
+        return rec
+    if rb:
+        rec[:, :rb] = vals.contiguous().view(n, -1).view(torch.uint8).view(n, rb)
+    rec[:, rb:rb + 8] = keys.contiguous().view(torch.uint8).view(n, 8)
+    return rec
+
+
+def _unpack_records(rec: torch.Tensor, like_vals: Optional[torch.Tensor], wb: int):
+    m = rec.shape[0]
+    rb = wb - 16
+    keys = rec[:, rb:rb + 8].contiguous().view(torch.int64).view(-1)
+    vals = None
+    if like_vals is not None:
+        vals = rec[:, :rb].contiguous().view(like_vals.dtype).view((m,) + tuple(like_vals.shape[1:]))
+    return keys, vals
+
+
+def _ipc_alltoallv(engine, skeys, svals, mat: List[List[int]]):
+    """Owner exchange over the IPC mesh; ``mat[i][j]`` = rows rank i sends to rank j.  Returns
+    (keys, rows) received in source-rank order, or None when records are not 16-byte vectors
+    or the largest rank's payload exceeds the staging buffers (both rank-independent)."""
+    wb = _rec_width(svals)
+    p, r = engine.p, engine.rank
+    if not wb:
+        return None
+    inst = _ipc_inst(engine, max(sum(row) for row in mat) * wb)
+    if inst is None:
+        return None
+    v = wb // 16
+    rec = _pack_records(skeys, svals, wb)
+    sp = [0] * p                                   # this rank's block offsets (rows)
+    for j in range(1, p):
+        sp[j] = sp[j - 1] + mat[r][j - 1]
+    stage = [(sp[j] * v, sp[j] * v, mat[r][j] * v, 0) for j in range(p) if mat[r][j]]
+    pulls, off = [], 0
+    for j in range(p):
+        src = sum(mat[j][:r])                      # rank j's block for this rank
+        if mat[j][r]:
+            pulls.append((src * v, off * v, mat[j][r] * v, j))
+        off += mat[j][r]
+    out = torch.empty((off, wb), dtype=torch.uint8, device=skeys.device)
+    grid = max(max(row) for row in mat) * v
+    if grid:
+        inst._plan(stage, pulls, rec.data_ptr() if stage else None, out.data_ptr() if pulls else None, grid)
+    engine._count("sparse.a2a.ipc")
+    return _unpack_records(out, svals, wb)
+
+
+def _ipc_allgatherv(engine, keys, vals, sizes: List[int]):
+    """Every rank's (keys, rows), rank order, over the IPC mesh (see above), or None."""
+    wb = _rec_width(vals)
+    if not wb:
+        return None
+    inst = _ipc_inst(engine, max(sizes) * wb)
+    if inst is None:
+        return None
+    v = wb // 16
+    n = sizes[engine.rank]
+    rec = _pack_records(keys, vals, wb)
+    stage = [(0, 0, n * v, 0)] if n else []
+    pulls, off = [], 0
+    for j, sz in enumerate(sizes):
+        if sz:
+            pulls.append((0, off * v, sz * v, j))
+        off += sz
+    out = torch.empty((off, wb), dtype=torch.uint8, device=keys.device)
+    grid = max(sizes) * v
+    if grid:
+        inst._plan(stage, pulls, rec.data_ptr() if stage else None, out.data_ptr() if pulls else None, grid)
+    engine._count("sparse.allgatherv.ipc")
+    return _unpack_records(out, vals, wb)
+
+
+def _count_matrix(engine, hist: torch.Tensor) -> List[List[int]]:
+    """Every rank's per-destination row counts (one all-gather, one host sync)."""
+    ts = [torch.empty_like(hist) for _ in range(engine.p)]
+    engine.coll.all_gather(ts, hist)
+    return torch.stack(ts).tolist()
+
+
 # ------------------------------------------------------------------ tensor-level API
 def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor]):
     p = engine.p
     skeys, svals, hist = _pack_by_owner(keys, vals, p)
-    recv_counts = torch.empty_like(hist)
-    engine.coll.all_to_all_single(recv_counts, hist)
-    send, recv = torch.stack([hist, recv_counts]).tolist()      # one host sync for both
+    if _sparse_ipc_ok(engine, keys):
+        mat = _count_matrix(engine, hist)
+        got = _ipc_alltoallv(engine, skeys, svals, mat)
+        if got is not None:
+            return got
+        send = mat[engine.rank]
+        recv = [mat[j][engine.rank] for j in range(p)]
+    else:
+        recv_counts = torch.empty_like(hist)
+        engine.coll.all_to_all_single(recv_counts, hist)
+        send, recv = torch.stack([hist, recv_counts]).tolist()      # one host sync for both
     rkeys = torch.empty(sum(recv), dtype=keys.dtype, device=keys.device)
     engine.coll.all_to_all_single(rkeys, skeys, recv, send)
     rvals = None
@@ -286,8 +411,12 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, k
     rkeys, rvals = _exchange_by_owner(engine, keys, v2)
     uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
     sizes = _row_counts(engine, uk.shape[0], uk.device)     # one count round for keys AND rows
-    all_k = _allgather_v(engine, uk, sizes)
-    all_v = _allgather_v(engine, uv, sizes)
+    got = _ipc_allgatherv(engine, uk, uv, sizes) if _sparse_ipc_ok(engine, uk) else None
+    if got is not None:
+        all_k, all_v = got
+    else:
+        all_k = _allgather_v(engine, uk, sizes)
+        all_v = _allgather_v(engine, uv, sizes)
     return all_k, (all_v.view(-1) if squeeze else all_v)
 
 
@@ -309,6 +438,9 @@ def _dedupe_first(keys: torch.Tensor, vals: Optional[torch.Tensor], key_bits: Op
 def allgather_sparse(engine, keys: torch.Tensor, vals: torch.Tensor):
     """Every rank's (keys, rows) concatenated in rank order + the per-rank row counts."""
     sizes = _row_counts(engine, keys.shape[0], keys.device)
+    got = _ipc_allgatherv(engine, keys, vals, sizes) if _sparse_ipc_ok(engine, keys) else None
+    if got is not None:
+        return got[0], got[1], sizes
     return _allgather_v(engine, keys, sizes), _allgather_v(engine, vals, sizes), sizes
 
 

@@ -1,0 +1,58 @@
+"""The sparse map collectives' ragged exchanges over the IPC mesh (copy-plan kernel, keys + rows
+as 16-byte-vector records) with real processes on one GPU, against a reference built from every
+rank's seed: exact for integer-valued rows, f32 and bf16, p = 2 / 3 / 4, plus the fallback for
+rows that are not whole 16-byte vectors and empty ranks."""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from spawn_ranks import run_spawn  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(r, dim, dtype, n):
+    g = torch.Generator().manual_seed(100 + r)
+    keys = torch.randperm(3 * n, generator=g)[:n].to(torch.int64)          # overlapping id ranges
+    vals = torch.randint(-8, 8, (n, dim), generator=g).to(dtype)
+    return keys, vals
+
+
+def _sparse_fn(comm, dim, dtype_name, n, empty_rank):
+    from mp4x import Operators
+    dtype = getattr(torch, dtype_name)
+    r, p = comm.getRank(), comm.getSlaveNum()
+    k, v = _data(r, dim, dtype, 0 if r == empty_rank else n)
+    eng = comm.device
+    before = dict(eng.stats)
+    op = Operators.Float.SUM if dtype == torch.float32 else Operators.BFloat16.SUM
+    rk, rv = comm.allreduceSparse(k.cuda(), v.cuda(), op)
+    gk, gv, sizes = comm.allgatherSparse(k.cuda(), v.cuda())
+    torch.cuda.synchronize()
+    used = {x: c - before.get(x, 0) for x, c in eng.stats.items() if c != before.get(x, 0)}
+    return rk.cpu(), rv.float().cpu(), gk.cpu(), gv.float().cpu(), sizes, used
+
+
+@pytest.mark.parametrize("p,dim,dtype,empty", [(2, 64, "float32", -1), (3, 8, "bfloat16", -1), (4, 64, "float32", 2),
+                                               (3, 3, "float32", -1)])
+def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty):
+    n = 20000
+    out = run_spawn(p, _sparse_fn, args=(dim, dtype, n, empty))
+    dt = getattr(torch, dtype)
+    ins = [_data(j, dim, dt, 0 if j == empty else n) for j in range(p)]
+    ref = {}
+    for k, v in ins:
+        for kk, vv in zip(k.tolist(), v.float()):
+            ref[kk] = ref[kk] + vv if kk in ref else vv.clone()
+    allk = torch.cat([k for k, _ in ins])
+    allv = torch.cat([v.float() for _, v in ins])
+    ipc = dim * torch.empty((), dtype=dt).element_size() % 16 == 0
+    for r, (rk, rv, gk, gv, sizes, used) in out.items():
+        assert sorted(rk.tolist()) == sorted(ref)
+        got = dict(zip(rk.tolist(), rv))
+        assert all(torch.equal(got[kk], ref[kk]) for kk in ref), r
+        assert torch.equal(gk, allk) and torch.equal(gv, allv) and sizes == [k.numel() for k, _ in ins]
+        if ipc:
+            assert used.get("sparse.a2a.ipc") == 1 and used.get("sparse.allgatherv.ipc") == 2, used
+        else:
+            assert "sparse.a2a.ipc" not in used, used
