@@ -325,8 +325,19 @@ def _ipc_allgatherv(engine, keys, vals, sizes: List[int]):
     return _unpack_records(out, vals, wb)
 
 
+def _host_counts(engine) -> bool:
+    """Small count vectors of GPU-resident data go over the host mesh when no RCCL is underneath
+    (gloo standing in on device tensors stages even 8 integers through a device sync + host copy
+    + TCP round per call)."""
+    return engine.backend == "gloo" and engine.device.type == "cuda" and \
+        getattr(engine.comm, "engine", None) is not None and hasattr(engine.comm.engine, "allgather_bytes")
+
+
 def _count_matrix(engine, hist: torch.Tensor) -> List[List[int]]:
     """Every rank's per-destination row counts (one all-gather, one host sync)."""
+    if _host_counts(engine):
+        blobs = engine.comm.engine.allgather_bytes(hist.to(torch.int64).cpu().numpy().tobytes())
+        return [np.frombuffer(b, dtype=np.int64).tolist() for b in blobs]
     ts = [torch.empty_like(hist) for _ in range(engine.p)]
     engine.coll.all_gather(ts, hist)
     return torch.stack(ts).tolist()
@@ -357,6 +368,9 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
 
 
 def _row_counts(engine, n: int, device) -> List[int]:
+    if device.type == "cuda" and _host_counts(engine):
+        return [int(np.frombuffer(b, dtype=np.int64)[0])
+                for b in engine.comm.engine.allgather_bytes(np.array([n], dtype=np.int64).tobytes())]
     t = torch.tensor([n], dtype=torch.int64, device=device)
     ts = [torch.empty_like(t) for _ in range(engine.p)]
     engine.coll.all_gather(ts, t)

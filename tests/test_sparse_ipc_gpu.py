@@ -30,7 +30,9 @@ def _sparse_fn(comm, dim, dtype_name, n, empty_rank):
     gk, gv, sizes = comm.allgatherSparse(k.cuda(), v.cuda())
     torch.cuda.synchronize()
     used = {x: c - before.get(x, 0) for x, c in eng.stats.items() if c != before.get(x, 0)}
-    return rk.cpu(), rv.float().cpu(), gk.cpu(), gv.float().cpu(), sizes, used
+    # numpy, not tensors: a torch tensor crosses the result queue as a shared-memory fd that
+    # dies with the worker process
+    return rk.cpu().numpy(), rv.float().cpu().numpy(), gk.cpu().numpy(), gv.float().cpu().numpy(), sizes, used
 
 
 @pytest.mark.parametrize("p,dim,dtype,empty", [(2, 64, "float32", -1), (3, 8, "bfloat16", -1), (4, 64, "float32", 2),
@@ -48,6 +50,7 @@ def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty):
     allv = torch.cat([v.float() for _, v in ins])
     ipc = dim * torch.empty((), dtype=dt).element_size() % 16 == 0
     for r, (rk, rv, gk, gv, sizes, used) in out.items():
+        rk, rv, gk, gv = (torch.from_numpy(x) for x in (rk, rv, gk, gv))
         assert sorted(rk.tolist()) == sorted(ref)
         got = dict(zip(rk.tolist(), rv))
         assert all(torch.equal(got[kk], ref[kk]) for kk in ref), r
