@@ -110,7 +110,9 @@ def main():
     a = ap.parse_args()
     res = run_spawn(a.p, body, args=(a.keys, a.dim, a.iters, a.fresh_dict), timeout=600)
     rec = {"config": f"allreduceMap Dict[str, float[{a.dim}]] {a.keys} keys/rank (50% shared)",
-           "processes_on_one_gpu": a.p, "exchange_transport": "gloo (one GPU: not xGMI)",
+           "processes_on_one_gpu": a.p,
+           "exchange_transport": ("IPC copy-plan kernels (all ranks on one GPU: not xGMI); counts over the host mesh"
+                                  if os.environ.get("MP4X_SPARSE_IPC", "1") == "1" else "gloo (one GPU: not xGMI)"),
            "dict_per_call": "fresh" if a.fresh_dict else "same (walk cached by PEP 509 version tag)"}
     rec["keys_via"] = "master" if os.environ.get("MP4X_KEYS_VIA_MASTER") == "1" else "peer-to-peer host mesh"
     for k in ("first_call_total", "first_call_agree_new_keys", "total", "walk_only", "agree", "to_tensors",
