@@ -182,41 +182,6 @@ static int k1_variant() {
   return g_k1_variant;
 }
 
-// NIN = 1 (the out-of-place single-input form: out = in, a copy for every dtype — 16-bit floats
-// round-trip exactly through f32): a persistent grid-stride stream, 4 x 16 B per lane in flight,
-// nontemporal loads and stores.  Measured as the fastest plain 1 GB copy of the variants
-// (tools/exp/copy_variants.hip, profiles/r1/copy_variants.txt: 8192 blocks x 256 threads).
-constexpr int kCopyU = 4;
-constexpr int kCopyGrid = 8192;
-
-__global__ __launch_bounds__(kBlock) void k_copy_stream(u32x4* __restrict__ out, const u32x4* __restrict__ in,
-                                                        int64_t nvec) {
-  const int64_t step = (int64_t)gridDim.x * kBlock * kCopyU;
-  for (int64_t base = (int64_t)blockIdx.x * kBlock * kCopyU + threadIdx.x; base < nvec; base += step) {
-    if (base + (int64_t)(kCopyU - 1) * kBlock < nvec) {
-      u32x4 r[kCopyU];
-#pragma unroll
-      for (int u = 0; u < kCopyU; ++u) r[u] = __builtin_nontemporal_load(in + base + u * kBlock);
-#pragma unroll
-      for (int u = 0; u < kCopyU; ++u) __builtin_nontemporal_store(r[u], out + base + u * kBlock);
-    } else {
-      for (int u = 0; u < kCopyU; ++u) {
-        const int64_t v = base + (int64_t)u * kBlock;
-        if (v < nvec) out[v] = in[v];
-      }
-    }
-  }
-}
-
-static int g_k1_copy = -1;
-static bool k1_copy_on() {
-  if (g_k1_copy < 0) {
-    const char* e = getenv("MP4X_K1_COPY");
-    g_k1_copy = e ? atoi(e) : 1;
-  }
-  return g_k1_copy != 0;
-}
-
 template <int DT, int OP, int NIN>
 __global__ __launch_bounds__(kBlock) void k_reduce_scalar(void* __restrict__ out_, InPtrs<NIN> ins, int64_t n) {
   using E = Elem<DT>;
@@ -244,18 +209,6 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
   if (aligned) {
     int64_t nvec = n / W;
     const int var = k1_variant();
-    if (NIN == 1 && nvec > 0 && k1_copy_on()) {
-      const int64_t per = (int64_t)kBlock * kCopyU;
-      int64_t g = (nvec + per - 1) / per;
-      if (g > kCopyGrid) g = kCopyGrid;
-      hipLaunchKernelGGL(k_copy_stream, dim3((unsigned)g), dim3(kBlock), 0, st, (u32x4*)out, (const u32x4*)ins[0],
-                         nvec);
-      if (n > nvec * W) {        // < W trailing elements
-        hipLaunchKernelGGL((k_reduce_scalar<DT, OP, 1>), dim3(1), dim3(kBlock), 0, st,
-                           (void*)((S*)out + nvec * W), InPtrs<1>{{(const S*)ins[0] + nvec * W}}, n - nvec * W);
-      }
-      return (int)hipGetLastError();
-    }
     if (var == 0) {
       int g = grid_for(nvec > 0 ? nvec : 1, 2);
       hipLaunchKernelGGL((k_reduce_vec<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, nvec, n);
