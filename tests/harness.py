@@ -15,6 +15,12 @@ LAST = {}
 
 def _worker(fn, rank_hint, port, args, q, kind, threads):
     try:
+        import sys
+        if "torch" in sys.modules:
+            # a parent that already ran a parallel torch op (e.g. a single-process reference
+            # optimizer step) leaves an OpenMP team that does not survive fork: the child's
+            # first parallel op would wait on it forever.  One intra-op thread never enters it.
+            sys.modules["torch"].set_num_threads(1)
         from mp4x import ProcessCommSlave, ThreadCommSlave
         if kind == "thread":
             comm = ThreadCommSlave("test", threads, "127.0.0.1", port, heartbeat=False)
