@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--no-rccl-baseline", action="store_true", help="skip the equal-method RCCL baseline")
     ap.add_argument("--no-tier-sweep", action="store_true",
                     help="N>1: skip the untimed per-size schedule sweep (4 KiB .. 64 MiB) run after the timed steps")
+    ap.add_argument("--sweep-sizes", default="4096,65536,262144,1048576,4194304,16777216,67108864",
+                    help="N>1: comma-separated byte sizes of the allreduce schedule sweep, in order")
+    ap.add_argument("--no-rooted-sweep", action="store_true", help="N>1: skip the rooted collectives' sweep")
     args = ap.parse_args()
     if args.no_register:
         args.alloc = "plain"
@@ -249,7 +252,7 @@ def main():
     tiers = None
     if p > 1 and not args.cpu and not args.no_tier_sweep and not (args.algo or args.codec):
         tiers = {}
-        for nb in (4 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20, 16 << 20, 64 << 20):
+        for nb in [int(x) for x in args.sweep_sizes.split(",") if x.strip()]:
             failed = 0.0
             try:
                 res = comm.device.autotune_allreduce(torch.empty(nb // 4, device=dev), op, iters=3)
@@ -266,7 +269,7 @@ def main():
         # the rooted collectives' schedules (RCCL vs IPC copy plans / two-shot vs composites)
         # at sizes on both sides of the IPC direct tier, recorded the same way
         rooted = {}
-        for nb in (1 << 20, 16 << 20, 128 << 20):
+        for nb in () if args.no_rooted_sweep else (1 << 20, 16 << 20, 128 << 20):
             failed = 0.0
             like = torch.empty(nb // 4, device=dev)
             row = {}
