@@ -158,8 +158,14 @@ def main():
             comm.peer_barrier() if args.cpu else comm.device.barrier()
             torch.cuda.synchronize()
 
+    # host-side agreement tensors when gloo stands in for RCCL (the shared-GPU rehearsals): gloo
+    # runs a CUDA tensor's collective on a fresh pool stream each call, every new stream takes
+    # another hardware queue, and once the ranks' queues oversubscribe the GPU every barrier
+    # kernel waits a scheduler time slice (~24-35 ms per call, profiles/r3/sweep/)
+    agree_dev = "cpu" if args.cpu or (p > 1 and dist.get_backend() == "gloo") else dev
+
     def max_over_ranks(vals):
-        t = torch.tensor(vals, dtype=torch.float64, device=dev)
+        t = torch.tensor(vals, dtype=torch.float64, device=agree_dev)
         if p > 1:
             if args.cpu:
                 t = torch.from_numpy(comm.allreduceArray(t.numpy(), Operands.DOUBLE_OPERAND(),
@@ -262,7 +268,7 @@ def main():
                 failed = 1.0
             # every rank stops together (a rank-local failure must not leave the others waiting
             # in the next size's collectives)
-            flag = torch.tensor([failed], dtype=torch.float64, device=dev)
+            flag = torch.tensor([failed], dtype=torch.float64, device=agree_dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MAX)
             if flag.item() > 0:
                 break
@@ -283,7 +289,7 @@ def main():
                 row["error"] = str(e)[:200]
                 failed = 1.0
             rooted[str(nb)] = row
-            flag = torch.tensor([failed], dtype=torch.float64, device=dev)
+            flag = torch.tensor([failed], dtype=torch.float64, device=agree_dev)
             dist.all_reduce(flag, op=dist.ReduceOp.MAX)
             if flag.item() > 0:
                 break

@@ -9,16 +9,20 @@ torch = pytest.importorskip("torch")
 from harness import run_ranks  # noqa: E402
 
 
-def _zero(comm, clip):
+def _zero(comm, clip, kw):
     from mp4x.models.zero import train_zero
-    return train_zero(comm, steps=6, global_batch=48, max_grad_norm=clip)
+    return train_zero(comm, steps=6, global_batch=48, max_grad_norm=clip, **kw)
 
 
-@pytest.mark.parametrize("p,clip", [(2, None), (3, None), (2, 0.05)])
-def test_zero_matches_single_adamw(p, clip):
+# bucket_mb=0.01: the MLP's 10.4k parameters in 2 buckets; overlap: the reduce-scatters launch from
+# the backward hooks; micro=2: gradient accumulation with the first micro-batch under no_sync()
+@pytest.mark.parametrize("p,clip,kw", [(2, None, {}), (3, None, {}), (2, 0.05, {}),
+                                       (3, None, {"bucket_mb": 0.01, "overlap": True}),
+                                       (2, 0.05, {"bucket_mb": 0.01, "overlap": True, "micro": 2})])
+def test_zero_matches_single_adamw(p, clip, kw):
     from mp4x.models.zero import train_single_adamw
     ref = train_single_adamw(steps=6, global_batch=48, max_grad_norm=clip)
-    res, _, _ = run_ranks(p, _zero, (clip,), timeout=120)
+    res, _, _ = run_ranks(p, _zero, (clip, kw), timeout=120)
     assert len(res) == p
     for losses in res.values():
         np.testing.assert_allclose(losses, ref, rtol=2e-5, atol=1e-6)
@@ -31,9 +35,10 @@ def _layout(comm):
     m = MLP(5, 7, 3)                                    # 5*7+7+7*3+3 = 66 f32: padded to 16 * p / 4 multiples
     before = [q.detach().clone() for q in m.parameters()]
     opt = ZeroOptimizer(comm, m.parameters(), torch.optim.SGD, lr=0.0)
-    g = opt.groups[0]
+    assert len(opt.buckets) == 1
+    g = opt.buckets[0]
     same = all(torch.equal(a, q) for a, q in zip(before, m.parameters()))
-    views = all(q.data.data_ptr() >= g.param_arena.data_ptr() and q.grad.data_ptr() >= g.grad_arena.data_ptr()
+    views = all(q.data.data_ptr() >= g.param.data_ptr() and q.grad.data_ptr() >= g.grad.data_ptr()
                 for q in m.parameters())
     out = (g.n, g.shard, g.lo, g.hi, same, views, g.aliased)
     opt.close()
