@@ -94,6 +94,20 @@ def _tune_key(dtype, op, nbytes: int) -> tuple:
     return (dtype, int(op.code), max(0, int(nbytes) - 1).bit_length())   # ceil(log2(nbytes))
 
 
+# Grid variants of the zero-copy two-shot the allreduce autotuner tries on a GPU of its own
+# (``ipc2z_b<N>``: N blocks instead of up to one per CU).  How many concurrent readers keep 7
+# xGMI links busy without thrashing the remote request queues is a property of the topology,
+# so it is measured, not assumed.
+ZC_GRIDS = (64, 128)
+
+
+def zc_grid(algo: str):
+    """(base schedule, grid) of an allreduce schedule name: ``ipc2z_b64`` -> (``ipc2z``, 64)."""
+    if algo.startswith("ipc2z_b") and algo[7:].isdigit():
+        return "ipc2z", int(algo[7:])
+    return algo, 0
+
+
 class DeviceEngine:
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
@@ -475,7 +489,7 @@ class DeviceEngine:
         if kind == "allreduce" and op is not None and not getattr(op, "is_custom", False) and \
                 (codec == "zs" or (codec is None and getattr(operand, "compress", False))):
             return "zs"       # lossless wire compression (the reference's compress=true contract)
-        if forced in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and kind == "allreduce" and \
+        if zc_grid(forced)[0] in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and kind == "allreduce" and \
                 self._ipc_ok(op, dtype, nbytes):
             return forced
         if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
@@ -575,7 +589,7 @@ class DeviceEngine:
         nbytes = view.numel() * view.element_size()
         algo = self.select("allreduce", nbytes, op, view.dtype, operand)
         capturing = view.is_cuda and capturing_now()
-        if algo not in self._CAPTURABLE and capturing:
+        if zc_grid(algo)[0] not in self._CAPTURABLE and capturing:
             # host-synchronising schedule inside a hipGraph capture: use a capturable twin
             algo = "ipc2" if algo == "ipc2p" else ("rccl" if self.rccl_ok(op, view.dtype) else "a2a")
         if out is not None:
@@ -645,6 +659,7 @@ class DeviceEngine:
 
     def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
         """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
+        algo, grid = zc_grid(algo)
         if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo in ("ipc2z", "ipc2w"):
@@ -655,7 +670,7 @@ class DeviceEngine:
                 if scr is not None:     # posted remote writes only (push form)
                     self._ipc_obj.allreduce_push(view, op, peers, scr, scale=scale)
                 else:
-                    self._ipc_obj.allreduce_registered(view, op, peers, scale=scale)
+                    self._ipc_obj.allreduce_registered(view, op, peers, scale=scale, grid=grid)
                 return True
             algo = "ipc2"        # not registered (on this rank): the staged two-shot
         if algo in ("ipc1", "ipc2", "ipc2p") and torch.cuda.is_current_stream_capturing():
@@ -749,7 +764,7 @@ class DeviceEngine:
             return self.rccl_ok(op, dtype)
         if algo.startswith("rccl_c"):
             return self.backend == "nccl" and self.rccl_ok(op, dtype)
-        if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w"):
+        if zc_grid(algo)[0] in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w"):
             return self._ipc_ok(op, dtype, nbytes)
         if algo == "rhd":
             return not getattr(op, "is_custom", False)
@@ -782,6 +797,8 @@ class DeviceEngine:
             if self._zc:
                 c.append("ipc2z")     # zero-copy two-shot on a registered tensor (one kernel)
                 c.append("ipc2w")     # ... its push form: every xGMI transfer a posted write
+                if nbytes >= (64 << 20) and not getattr(self._ipc_obj, "shared_gpu", True):
+                    c += [f"ipc2z_b{g}" for g in ZC_GRIDS]     # ... with fewer, longer-lived blocks
         c.append("a2a")
         if nbytes <= (64 << 20):
             c.append("rhd")
@@ -813,14 +830,14 @@ class DeviceEngine:
             self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
         registered = False
         try:
-            if "ipc2z" in cands or "ipc2w" in cands:
+            if any(zc_grid(c)[0] in ("ipc2z", "ipc2w") for c in cands):
                 registered = self.register_buffer(view)     # collective; False on every rank alike
                 if not registered or (self._ipc_obj.scratch_of(view) is None and "ipc2w" in cands):
                     # (the push form needs every rank's scratch: agreed inside register)
                     cands[:] = [c for c in cands if c != "ipc2w" or registered and
                                 self._ipc_obj.scratch_of(view) is not None]
                 if not registered:
-                    cands[:] = [c for c in cands if c not in ("ipc2z", "ipc2w")]
+                    cands[:] = [c for c in cands if zc_grid(c)[0] not in ("ipc2z", "ipc2w")]
             for c in cands:
                 times.append(self._time_candidate(c, view, op, iters))
         finally:
@@ -1094,7 +1111,7 @@ class DeviceEngine:
 
     # ------------------------------------------------------------------ persisted tuning table
     _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w", "a2a",
-                                  "rhd"},
+                                  "rhd"} | {f"ipc2z_b{g}" for g in ZC_GRIDS},
                     "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"},
                     "reduce": {"rccl", "ipc", "a2a"}, "broadcast": {"rccl", "ipc", "composite"},
                     "gather": {"p2p", "ipc"}, "scatter": {"p2p", "ipc"}}

@@ -697,7 +697,7 @@ class IpcAllreduce:
                                                self.epoch | ZC_TAG | PUSH_TAG, blocks, edev, scale, st),
               "mp4x_ipc_allreduce_push")
 
-    def allreduce_registered(self, view: torch.Tensor, op, peers, scale: float = 1.0) -> torch.Tensor:
+    def allreduce_registered(self, view: torch.Tensor, op, peers, scale: float = 1.0, grid: int = 0) -> torch.Tensor:
         """In-place two-shot straight on the registered tensors (see :meth:`register`): ONE
         kernel, no staging and no pieces, whatever the size."""
         total = view.numel() * view.element_size()
@@ -705,7 +705,7 @@ class IpcAllreduce:
             raise Mp4jException("zero-copy IPC allreduce needs 16-byte aligned, 16-byte multiple views")
         if torch.cuda.is_current_stream_capturing() and self._epoch_dev is None:
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
-        self.allreduce_registered_ptrs(view.data_ptr(), total, op, peers, view.dtype, scale)
+        self.allreduce_registered_ptrs(view.data_ptr(), total, op, peers, view.dtype, scale, grid)
         return view
 
     def selftest_zero_copy(self, n: int) -> int:
@@ -783,9 +783,11 @@ class IpcAllreduce:
             self.lib.mp4x_ipc_free(scr)
         return bad
 
-    def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0) -> None:
+    def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0,
+                                  grid: int = 0) -> None:
         """The zero-copy two-shot on raw pointers (``dst`` = this rank's buffer, ``peers`` = every
-        rank's mapped buffer)."""
+        rank's mapped buffer).  ``grid``: block count (0 = the default, up to one per CU; the
+        autotuner's ``ipc2z_b<N>`` candidates try fewer — fewer, longer-lived readers per link)."""
         self.raise_if_failed()
         st = stream_ptr()
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
@@ -794,6 +796,8 @@ class IpcAllreduce:
         else:
             self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
         blocks = max(1, min(self.max_blocks, -(-total // 16 // 512))) if self.max_blocks else 0
+        if grid > 0:
+            blocks = min(grid, blocks) if blocks else grid
         pp = ptr_array(peers)
         check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
                                              self._pp_sig[0], self.rank, self.p, total, None, dst,

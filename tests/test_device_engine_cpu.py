@@ -469,3 +469,32 @@ def test_rooted_autotuners_pin_and_apply():
         assert set(pin) >= {"reduce", "broadcast", "gather", "scatter"}
         assert st.get("reduce." + pin["reduce"]) == 1, st
         assert st.get("broadcast" if pin["broadcast"] == "rccl" else "broadcast.composite") == 1, st
+
+
+def test_zero_copy_grid_variants_are_candidates_on_a_gpu_of_their_own():
+    """``ipc2z_b<N>`` (the zero-copy two-shot on N blocks) is tried for large messages when
+    every rank has a GPU of its own; never on a shared GPU (its grid is capped there anyway)
+    or under the gloo stand-in."""
+    from mp4x import Operators
+    from mp4x.parallel.device_engine import ZC_GRIDS, DeviceEngine, zc_grid
+    assert zc_grid("ipc2z_b64") == ("ipc2z", 64) and zc_grid("ipc2z") == ("ipc2z", 0)
+    assert zc_grid("ipc2z_bx") == ("ipc2z_bx", 0) and zc_grid("rccl_c64") == ("rccl_c64", 0)
+    e = object.__new__(DeviceEngine)
+    e.backend, e.device, e.ipc_enabled, e._zc = "nccl", torch.device("cuda", 0), True, True
+    e.ipc_twoshot_max = 16 << 20
+    e.rccl_ok = lambda op, dt: True
+    e._ipc_ok = lambda op, dt, nb: True
+
+    class _Ipc:
+        shared_gpu = False
+    e._ipc_obj = _Ipc()
+    op = Operators.Float.SUM
+    big = e.allreduce_candidates(256 << 20, op, torch.float32)
+    assert all(f"ipc2z_b{g}" in big for g in ZC_GRIDS) and "ipc2z" in big and "rccl" in big
+    assert not any(c.startswith("ipc2z_b") for c in e.allreduce_candidates(16 << 20, op, torch.float32))
+    assert all(e._algo_valid(f"ipc2z_b{g}", op, torch.float32, 256 << 20) for g in ZC_GRIDS)
+    assert all(f"ipc2z_b{g}" in DeviceEngine._KNOWN_ALGOS["allreduce"] for g in ZC_GRIDS)
+    e._ipc_obj.shared_gpu = True
+    assert not any(c.startswith("ipc2z_b") for c in e.allreduce_candidates(256 << 20, op, torch.float32))
+    e._ipc_obj.shared_gpu, e.backend = False, "gloo"
+    assert not any(c.startswith("ipc2z_b") for c in e.allreduce_candidates(256 << 20, op, torch.float32))

@@ -128,11 +128,11 @@ def _zc_fn(comm, sizes):
     return res, err, eng._ipc_obj.error_word()
 
 
-@pytest.mark.parametrize("algo", ["ipc2z", "ipc2w"])
+@pytest.mark.parametrize("algo", ["ipc2z", "ipc2w", "ipc2z_b64"])
 @pytest.mark.parametrize("p", [2, 4])
 def test_zero_copy_registered_two_shot_exact(p, algo):
-    """Pull (ipc2z) and push (ipc2w: every peer transfer a posted write) forms of the zero-copy
-    two-shot: 1 MiB (default two-shot tier) and 96 MiB (above the 64 MiB staging buffer: no
+    """Pull (ipc2z; ipc2z_b64 on a 64-block grid) and push (ipc2w: every peer transfer a posted
+    write) forms of the zero-copy two-shot: 1 MiB (default two-shot tier) and 96 MiB (above the 64 MiB staging buffer: no
     pieces), full range and an offset [from, to) view, exact; random data vs fp64."""
     out = run_spawn(p, _zc_fn, args=([1 << 18, 24 << 20],), env={"MP4X_DEVICE_ALGO": algo})
     for r, (res, err, ew) in out.items():
