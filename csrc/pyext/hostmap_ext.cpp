@@ -178,6 +178,58 @@ PyObject* stack_rows(PyObject*, PyObject* const* a, Py_ssize_t na) {
   Py_RETURN_FALSE;
 }
 
+// learn_keys(key2id: dict, id2key: list, proposals) -> int
+// One key-dictionary sync round (mp4x/parallel/sparse.py KeyDictionary.learn_round): walk every
+// rank's block of proposed keys in rank order and give each key not in ``key2id`` yet the next id
+// (= len(id2key)), appending it to ``id2key``.  ONE dict operation per key (PyDict_SetDefault:
+// a single probe that inserts or finds) instead of the union dict + membership test + insert of
+// the Python form.  Blocks may be None.  Returns the number of new keys.
+PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 3 || !PyDict_CheckExact(a[0]) || !PyList_CheckExact(a[1])) {
+    PyErr_SetString(PyExc_TypeError, "learn_keys(key2id: dict, id2key: list, proposals)");
+    return nullptr;
+  }
+  PyObject* d = a[0];
+  PyObject* ids = a[1];
+  const Py_ssize_t base = PyList_GET_SIZE(ids);
+  Py_ssize_t next = base;
+  PyObject* it = PyObject_GetIter(a[2]);
+  if (!it) return nullptr;
+  PyObject* blk;
+  while ((blk = PyIter_Next(it)) != nullptr) {
+    if (blk == Py_None) {
+      Py_DECREF(blk);
+      continue;
+    }
+    PyObject* seq = PySequence_Fast(blk, "learn_keys: every proposal block must be a sequence or None");
+    Py_DECREF(blk);
+    if (!seq) break;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    PyObject** items = PySequence_Fast_ITEMS(seq);
+    bool ok = true;
+    for (Py_ssize_t i = 0; i < n && ok; ++i) {
+      PyObject* id = PyLong_FromSsize_t(next);
+      if (!id) {
+        ok = false;
+        break;
+      }
+      PyObject* got = PyDict_SetDefault(d, items[i], id);     // borrowed
+      if (!got) {
+        ok = false;
+      } else if (got == id) {                                  // inserted: a new key
+        if (PyList_Append(ids, items[i]) != 0) ok = false;
+        ++next;
+      }
+      Py_DECREF(id);
+    }
+    Py_DECREF(seq);
+    if (!ok) break;
+  }
+  Py_DECREF(it);
+  if (PyErr_Occurred()) return nullptr;
+  return PyLong_FromSsize_t(next - base);
+}
+
 PyMethodDef kMethods[] = {
     {"partition", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(partition)), METH_FASTCALL,
      "partition(map, p) -> [p dicts] by Java String.hashCode % p, or None for non-str keys"},
@@ -185,6 +237,8 @@ PyMethodDef kMethods[] = {
      "owner_ids(keys, p, out) -> bool: out[i] = Java String.hashCode(keys[i]) % p (int32)"},
     {"stack_rows", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(stack_rows)), METH_FASTCALL,
      "stack_rows(values, out) -> bool: row i of out = bytes of values[i]"},
+    {"learn_keys", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(learn_keys)), METH_FASTCALL,
+     "learn_keys(key2id, id2key, proposals) -> int: number the keys not in key2id yet, in order"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_mp4x_hostmap", "native passes of the host map collectives", -1,

@@ -68,6 +68,11 @@ class KeyDictionary:
 
     def learn_round(self, proposals) -> None:
         """Number the union of one sync round's proposals (every rank passes the same list)."""
+        from ..ops import native
+        ext = native.hostmap_ext()
+        if ext is not None:       # one dict probe per key (csrc/pyext/hostmap_ext.cpp learn_keys)
+            ext.learn_keys(self.key2id, self.id2key, proposals)
+            return
         # C-level passes only (a first call numbers ~1M keys): order-preserving union of the
         # blocks, drop the known keys, number the rest in that order
         union = dict.fromkeys(itertools.chain.from_iterable(b for b in proposals if b))

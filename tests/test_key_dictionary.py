@@ -1,5 +1,7 @@
 """Dense, rank-consistent map-key ids (parallel/sparse.py KeyDictionary): every rank numbers a
 sync round's union in the same order, ids stay dense, and ``bits`` bounds the sort width."""
+import pytest
+
 from mp4x.parallel.sparse import KeyDictionary
 
 
@@ -295,3 +297,28 @@ def test_walk_cache_follows_the_dict_version():
     m2 = {"k0": base[0], "new": base[1]}                      # a miss is never cached
     _, nm, _, _ = sparse._pack_native(d, m2)
     assert nm == 1 and d._walk_cache is None
+
+
+def test_native_learn_round_matches_python_union():
+    """csrc/pyext/hostmap_ext.cpp ``learn_keys`` numbers exactly what the Python union does:
+    rank order, first occurrence, known keys skipped, None blocks, any hashable key."""
+    from mp4x.ops import native
+    from mp4x.parallel.sparse import KeyDictionary
+    ext = native.hostmap_ext()
+    if ext is None:
+        pytest.skip("native host-map extension not built")
+    props = [["a", "b", ("t", 1), "a"], None, [], ["c", "b", 7, "known"], ["d", ("t", 1)]]
+    nat = KeyDictionary()
+    nat.key2id, nat.id2key = {"known": 0}, ["known"]
+    assert ext.learn_keys(nat.key2id, nat.id2key, props) == 6
+    ref = KeyDictionary()
+    ref.key2id, ref.id2key = {"known": 0}, ["known"]
+    import itertools
+    union = dict.fromkeys(itertools.chain.from_iterable(b for b in props if b))
+    new = [k for k in union if k not in ref.key2id]
+    ref.key2id.update(zip(new, range(1, 1 + len(new))))
+    ref.id2key.extend(new)
+    assert nat.key2id == ref.key2id and nat.id2key == ref.id2key
+    assert nat.id2key == ["known", "a", "b", ("t", 1), "c", 7, "d"]
+    with pytest.raises(TypeError):
+        ext.learn_keys({}, [], [[["unhashable"]]])
