@@ -296,6 +296,19 @@ def main():
         tiers["rooted"] = rooted
 
     ref = REF_BUSBW_MBPS.get(p)
+    topo = None
+    if rank == 0 and not args.cpu:
+        # which of the ranks' devices are one xGMI hop apart (native probe; one process per GPU
+        # sees every device of the node, ranks 0..p-1 on devices 0..p-1)
+        from mp4x.utils.topology import local_summary
+        try:
+            topo = local_summary(list(range(p)) if torch.cuda.device_count() >= p else [local])
+            props = torch.cuda.get_device_properties(dev)
+            topo = dict(topo or {}, gpu=props.name, gcn_arch=getattr(props, "gcnArchName", None),
+                        cus=props.multi_processor_count, hbm_gib=round(props.total_memory / 2 ** 30, 1),
+                        ranks_share_one_gpu=torch.cuda.device_count() < p)
+        except Exception as e:   # noqa: BLE001 — evidence only
+            topo = {"error": str(e)[:200]}
     selftest = None if (p == 1 or args.cpu) else comm.device.ipc_selftest
     stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items() if k.startswith("allreduce")}
     if rank == 0:
@@ -317,7 +330,7 @@ def main():
                        "payload_bytes": nbytes, "algo": algo, "alloc": args.alloc, "registered": registered,
                        "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
                        "autotune_iters": args.autotune_iters, "ipc_selftest": selftest,
-                       "calls": stats, "tier_sweep_ms": tiers},
+                       "calls": stats, "tier_sweep_ms": tiers, "topology": topo},
             "verified": verified,
             "max_abs_err": max_err,
             "busbw_gbps_per_rank": round(busbw, 3),
