@@ -38,6 +38,7 @@ from ..exceptions import Mp4jException
 from ..operators import DType, OpCode, Operator, dtype_of_torch, for_dtype
 from ..ops.native import capturing_now
 from ..utils.commutils import CommUtils
+from .hier import NodeLayout
 
 LOG = logging.getLogger("mp4x.device")
 
@@ -109,6 +110,12 @@ def zc_grid(algo: str):
 
 
 class DeviceEngine:
+    # (class defaults: engines assembled without __init__ in unit tests see one node, no hier)
+    layout = NodeLayout([])
+    _hier = None
+    _hier_failed = False
+    hier_min_bytes = 1 << 20
+
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
         self.comm = comm
@@ -167,6 +174,16 @@ class DeviceEngine:
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
         self._select_tuned = False
         self._load_shared_tuning(shared=coll is None)
+        # which ranks share a node (parallel/hier.py): a job spanning nodes has no global IPC mesh;
+        # its allreduce can run node-aware (xGMI inside a node, RCCL across nodes)
+        from .hier import node_id
+        self.layout = NodeLayout(self.all_gather_object(node_id(self.rank)) if self.p > 1 and coll is None
+                                 else ["local"] * self.p)
+        if self.layout.multi_node:
+            self.ipc_enabled = False
+        self.hier_min_bytes = int(os.environ.get("MP4X_HIER_MIN_BYTES", 1 << 20))
+        self._hier = None
+        self._hier_failed = False
         # fail-stop detector for hung / failed collectives (parallel/watchdog.py)
         from . import watchdog
         self.watchdog = watchdog.CollectiveWatchdog(self) if coll is None and watchdog.enabled() else None
@@ -228,7 +245,7 @@ class DeviceEngine:
         """Fail-stop teardown (``ncclCommAbort``): a rank blocked in a collective with a dead
         peer returns instead of hanging.  Called by ``ProcessCommSlave.close(code != 0)``."""
         self._stop_watchdog()
-        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big"):
+        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big", "_hier"):
             setattr(self, name, None)          # peers may be gone: no synchronising close
         if self._owns_pg and dist.is_initialized():
             try:
@@ -251,7 +268,7 @@ class DeviceEngine:
 
     def shutdown(self):
         self._stop_watchdog()
-        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big"):
+        for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big", "_hier"):
             obj = getattr(self, name)
             if obj is not None:
                 try:
@@ -467,6 +484,32 @@ class DeviceEngine:
                 return self._ipc_obj
         return self._ipc_large or self._ipc_obj
 
+    def hier(self):
+        """The node-aware allreduce (parallel/hier.py) of a job spanning >= 2 nodes of equal size,
+        or None.  Collective, lazily created; a setup failure is agreed (every rank gets None)."""
+        if self._hier is None and not self._hier_failed and self.layout.hier_ok():
+            from .hier import HierAllreduce
+            try:
+                self._hier = HierAllreduce(self, self.layout)
+            except Exception as e:   # noqa: BLE001
+                LOG.warning("rank %d: hierarchical allreduce disabled: %s", self.rank, e)
+                self._hier_failed = True
+            ok = self.all_gather_object(self._hier is not None)
+            if not all(ok):
+                if self._hier is not None:
+                    self._hier.close()
+                self._hier, self._hier_failed = None, True
+        return self._hier
+
+    def _hier_ok(self, op, dtype, nbytes) -> bool:
+        """Rank-independent: a multi-node layout and an (op, dtype, size) the schedule serves."""
+        if not self.layout.hier_ok() or self._hier_failed or nbytes % 16 or getattr(op, "is_custom", False):
+            return False
+        from .ipc import SUPPORTED_DTYPES
+        if dtype not in SUPPORTED_DTYPES or not self.rccl_ok(op, dtype):
+            return False
+        return op.code == OpCode.SUM or (op.code in (OpCode.MAX, OpCode.MIN) and dtype.is_floating_point)
+
     def _ipc_ok(self, op, dtype, nbytes) -> bool:
         if not self.ipc_enabled or nbytes % 16 or getattr(op, "is_custom", False):
             return False
@@ -494,6 +537,8 @@ class DeviceEngine:
             return forced
         if forced == "rhd" and kind == "allreduce" and not getattr(op, "is_custom", False):
             return forced     # (custom operators may be non-commutative: rank-ordered a2a only)
+        if forced == "hier" and kind == "allreduce" and op is not None and self._hier_ok(op, dtype, nbytes):
+            return forced
         self._select_tuned = False
         if kind == "allreduce" and op is not None and forced in ("", "auto") and self._tuned:
             t = self._tuned.get(_tune_key(dtype, op, nbytes))
@@ -502,6 +547,9 @@ class DeviceEngine:
                 return t
         if op is not None and not self.rccl_ok(op, dtype):
             return "a2a"
+        if forced in ("", "auto") and kind == "allreduce" and nbytes >= self.hier_min_bytes and \
+                self._hier_ok(op, dtype, nbytes):
+            return "hier"     # several nodes: xGMI inside each, RCCL on 1/L of the bytes across
         if forced in ("rccl", "a2a"):
             return forced
         if forced.startswith("rccl_c") and kind == "allreduce" and op is not None \
@@ -678,6 +726,12 @@ class DeviceEngine:
             inst = self.ipc_large() if nb > self.ipc_twoshot_max else self._ipc_obj
             if inst is None or inst._epoch_dev is None:
                 algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
+        if algo == "hier":
+            h = self.hier()
+            if h is not None and h.supports(view, op):
+                h.allreduce(view, op, scale=scale)
+                return True
+            algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo == "rccl":
             avg = scale != 1.0 and abs(scale * self.p - 1.0) < 1e-9 and op.code == OpCode.SUM \
                 and self.backend == "nccl"
@@ -764,6 +818,8 @@ class DeviceEngine:
             return self.rccl_ok(op, dtype)
         if algo.startswith("rccl_c"):
             return self.backend == "nccl" and self.rccl_ok(op, dtype)
+        if algo == "hier":
+            return self._hier_ok(op, dtype, nbytes)
         if zc_grid(algo)[0] in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w"):
             return self._ipc_ok(op, dtype, nbytes)
         if algo == "rhd":
@@ -799,6 +855,8 @@ class DeviceEngine:
                 c.append("ipc2w")     # ... its push form: every xGMI transfer a posted write
                 if nbytes >= (64 << 20) and not getattr(self._ipc_obj, "shared_gpu", True):
                     c += [f"ipc2z_b{g}" for g in ZC_GRIDS]     # ... with fewer, longer-lived blocks
+        if self._hier_ok(op, dtype, nbytes):
+            c.append("hier")
         c.append("a2a")
         if nbytes <= (64 << 20):
             c.append("rhd")
@@ -1111,14 +1169,17 @@ class DeviceEngine:
 
     # ------------------------------------------------------------------ persisted tuning table
     _KNOWN_ALGOS = {"allreduce": {"rccl", "rccl_c64", "rccl_c112", "ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w", "a2a",
-                                  "rhd"} | {f"ipc2z_b{g}" for g in ZC_GRIDS},
+                                  "rhd", "hier"} | {f"ipc2z_b{g}" for g in ZC_GRIDS},
                     "reduce_scatter": {"ipc", "a2a"}, "allgather": {"ipc", "p2p"},
                     "reduce": {"rccl", "ipc", "a2a"}, "broadcast": {"rccl", "ipc", "composite"},
                     "gather": {"p2p", "ipc"}, "scatter": {"p2p", "ipc"}}
 
     def _topology(self) -> dict:
         dev = torch.cuda.get_device_name(self.device) if self.device.type == "cuda" else "cpu"
-        return {"p": self.p, "device": dev, "backend": self.backend}
+        top = {"p": self.p, "device": dev, "backend": self.backend}
+        if self.layout.multi_node:
+            top["nodes"] = len(self.layout.nodes)
+        return top
 
     def tuning_table(self) -> dict:
         """The schedules pinned by the autotuners, JSON-able, with the topology they were measured

@@ -132,7 +132,9 @@ class IpcAllreduce:
             local_err = f"{type(e).__name__}: {e}"
         # IPC handles only open on the same node: a job spanning hosts keeps RCCL (decided from
         # the exchanged host names, identically on every rank, before anything is allocated)
-        infos = comm.server.call("allgather_obj", self.rank, (socket.gethostname(), local_err))
+        from .hier import node_id
+        nid = comm.node_id() if hasattr(comm, "node_id") else node_id(self.rank)
+        infos = comm.server.call("allgather_obj", self.rank, (nid, local_err))
         errs = [(i, e) for i, (_, e) in enumerate(infos) if e]
         if errs:
             raise Mp4jException(f"IPC setup failed on ranks {errs}")
@@ -185,7 +187,7 @@ class IpcAllreduce:
             self.close(sync=False)
             raise Mp4jException(f"IPC buffer setup failed on ranks {failed}")
         ids = [bytes(b[2 * hs:]) for b in allh]
-        share = max(ids.count(i) for i in ids)
+        share = max(max(ids.count(i) for i in ids), int(getattr(comm, "gpu_share", 1)))
         # ranks on one device (rehearsal): cap the grid so all ranks' blocks fit at once
         self.max_blocks = 0 if share == 1 else max(8, _RESIDENT_BLOCKS // (2 * share))
         self.shared_gpu = share > 1

@@ -1,0 +1,106 @@
+"""Node-aware allreduce (mp4x/parallel/hier.py): layout / chunking units, and the schedule on CPU
+(gloo) with simulated nodes (``MP4X_SIM_NODE_SIZE``), several pieces, mixed ops and dtypes."""
+import os
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from harness import run_ranks  # noqa: E402
+from mp4x import Operators  # noqa: E402
+from mp4x.parallel.hier import NodeLayout, chunk_bounds  # noqa: E402
+
+
+def test_layout_groups_and_eligibility():
+    lay = NodeLayout(["a", "a", "b", "b", "c", "c"])
+    assert lay.nodes == [[0, 1], [2, 3], [4, 5]] and lay.local_index == [0, 1, 0, 1, 0, 1]
+    assert lay.hier_ok() and lay.cross_groups() == [[0, 2, 4], [1, 3, 5]]
+    # interleaved placement (ranks not contiguous per node)
+    lay = NodeLayout(["a", "b", "a", "b"])
+    assert lay.nodes == [[0, 2], [1, 3]] and lay.cross_groups() == [[0, 1], [2, 3]] and lay.node_of == [0, 1, 0, 1]
+    assert not NodeLayout(["a"] * 4).hier_ok()                  # one node: the flat mesh
+    assert not NodeLayout(["a", "a", "b"]).hier_ok()            # unequal nodes
+    assert not NodeLayout(["a", "b", "c"]).hier_ok()            # one rank per node
+
+
+@pytest.mark.parametrize("es", [1, 2, 4, 8])
+@pytest.mark.parametrize("L", [2, 3, 8])
+def test_chunk_bounds_aligned_and_covering(es, L):
+    for lo, n16 in ((0, 1), (32, 7), (1024, 1000)):
+        hi = lo + n16 * 16 // es
+        froms, tos = chunk_bounds(lo, hi, es, L)
+        assert froms[0] == lo and tos[-1] == hi and len(froms) == L
+        assert all(t == f2 for t, f2 in zip(tos, froms[1:]))
+        assert all(((f - lo) * es) % 16 == 0 for f in froms + tos)
+        assert all(t >= f for f, t in zip(froms, tos))
+
+
+def hier_body(comm, n):
+    eng = comm.device
+    p, r = comm.getSlaveNum(), comm.getRank()
+    assert eng.layout.hier_ok() and not eng.ipc_enabled
+    idx = torch.arange(n, dtype=torch.int64) % 7
+    # f32 SUM, a sub-range (the reference's [from, to) contract), fused 1/p average
+    t = (idx + r).to(torch.float32)
+    eng.allreduce(t, 0, n, Operators.Float.SUM)
+    assert torch.equal(t, (idx * p + p * (p - 1) // 2).to(torch.float32))
+    t = (idx + r).to(torch.float32)
+    eng.allreduce(t, 0, n, Operators.Float.SUM, scale=1.0 / p)
+    assert torch.allclose(t, (idx * p + p * (p - 1) / 2).to(torch.float32) / p)
+    # f64 MAX on an offset range; the elements outside it stay untouched
+    d = (idx * (r + 1)).to(torch.float64)
+    eng.allreduce(d, 8, n - 8, Operators.Double.MAX)
+    assert torch.equal(d[8:n - 8], (idx * p).to(torch.float64)[8:n - 8]) and d[0] == 0
+    # int64 SUM
+    q = torch.full((n,), r + 1, dtype=torch.int64)
+    eng.allreduce(q, 0, n, Operators.Long.SUM)
+    assert torch.all(q == p * (p + 1) // 2)
+    # a length that is not a 16-byte multiple: the flat schedule serves it
+    u = torch.full((n + 1,), float(r), dtype=torch.float32)
+    eng.allreduce(u, 0, n + 1, Operators.Float.SUM)
+    assert torch.all(u == p * (p - 1) / 2)
+    h = eng.hier()
+    return eng.stats.get("allreduce.hier", 0), h.stats["pieces"], eng.select(
+        "allreduce", n * 4 + 4, eng._op(Operators.Float.SUM, u), torch.float32)
+
+
+@pytest.mark.parametrize("p,size,piece", [(4, 2, 4096), (6, 3, 1 << 20), (6, 2, 160)])
+def test_hier_allreduce_simulated_nodes(p, size, piece):
+    n = 10_000
+    res, _, _ = run_ranks(p, hier_body, args=(n,), timeout=180,
+                          env={"MP4X_SIM_NODE_SIZE": str(size), "MP4X_HIER_MIN_BYTES": "0",
+                               "MP4X_HIER_PIECE_BYTES": str(piece), "MP4X_DEVICE_BACKEND": "gloo"})
+    for calls, pieces, odd_algo in res.values():
+        assert calls == 4
+        assert pieces >= 4 * -(-(n * 4) // piece) - 1
+        assert odd_algo != "hier"
+
+
+def unequal_body(comm):
+    eng = comm.device
+    p, r = comm.getSlaveNum(), comm.getRank()
+    t = torch.full((4096,), float(r + 1))
+    eng.allreduce(t, 0, 4096, Operators.Float.SUM)
+    assert torch.all(t == p * (p + 1) / 2)
+    return eng.layout.multi_node, eng.layout.hier_ok(), eng.stats
+
+
+def test_unequal_nodes_use_the_flat_schedule():
+    res, _, _ = run_ranks(3, unequal_body, timeout=120,
+                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_HIER_MIN_BYTES": "0", "MP4X_DEVICE_BACKEND": "gloo"})
+    for multi, ok, stats in res.values():
+        assert multi and not ok and "allreduce.hier" not in stats
+
+
+def autotune_body(comm):
+    eng = comm.device
+    res = eng.autotune_allreduce(torch.zeros(1 << 16), Operators.Float.SUM, iters=1)
+    return sorted(res), eng.select("allreduce", 1 << 18, eng._op(Operators.Float.SUM, torch.zeros(1)), torch.float32)
+
+
+def test_hier_is_an_autotune_candidate():
+    res, _, _ = run_ranks(4, autotune_body, timeout=180,
+                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_DEVICE_BACKEND": "gloo"})
+    names = {tuple(v[0]) for v in res.values()}
+    assert len(names) == 1 and "hier" in next(iter(names))
+    assert len({v[1] for v in res.values()}) == 1      # every rank pinned the same schedule
