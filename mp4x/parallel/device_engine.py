@@ -49,6 +49,55 @@ _RCCL_DTYPES = {torch.float64, torch.float32, torch.bfloat16, torch.float16, tor
                 torch.int8, torch.uint8}
 
 
+_IPC_DTYPES = None
+
+
+def _ipc_dtypes():
+    """``ipc.SUPPORTED_DTYPES`` without an import statement per call (the latency tier)."""
+    global _IPC_DTYPES
+    if _IPC_DTYPES is None:
+        from .ipc import SUPPORTED_DTYPES
+        _IPC_DTYPES = SUPPORTED_DTYPES
+    return _IPC_DTYPES
+
+
+class _TunedTable(dict):
+    """The pinned-schedule table; ``gen`` counts its mutations, so :meth:`DeviceEngine.select`
+    can memoise its decisions and still see every re-tune, table load or clear."""
+    gen = 0
+
+    def _bump(self):
+        self.gen += 1
+
+    def __setitem__(self, k, v):
+        self._bump()
+        super().__setitem__(k, v)
+
+    def __delitem__(self, k):
+        self._bump()
+        super().__delitem__(k)
+
+    def pop(self, *a):
+        self._bump()
+        return super().pop(*a)
+
+    def popitem(self):
+        self._bump()
+        return super().popitem()
+
+    def clear(self):
+        self._bump()
+        super().clear()
+
+    def update(self, *a, **k):
+        self._bump()
+        super().update(*a, **k)
+
+    def setdefault(self, k, d=None):
+        self._bump()
+        return super().setdefault(k, d)
+
+
 def _env_algo() -> str:
     return os.environ.get("MP4X_DEVICE_ALGO", "auto").lower()
 
@@ -112,6 +161,7 @@ def zc_grid(algo: str):
 class DeviceEngine:
     # (class defaults: engines assembled without __init__ in unit tests see one node, no hier)
     layout = NodeLayout([])
+    _dm_large = "auto"
     _hier = None
     _hier_failed = False
     hier_min_bytes = 1 << 20
@@ -169,7 +219,9 @@ class DeviceEngine:
         self._ipc_fp8_big_failed = False
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
-        self._tuned: Dict[tuple, str] = {}
+        self._tuned: Dict[tuple, str] = _TunedTable()
+        self._sel_memo: Dict[tuple, tuple] = {}       # select() decisions of repeated call shapes
+        self._dm_large = os.environ.get("MP4X_DM_LARGE", "auto")
         self._tune_scratch: Dict[tuple, torch.Tensor] = {}   # autotune_allreduce scratch per (dtype, numel)
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
         self._select_tuned = False
@@ -505,23 +557,49 @@ class DeviceEngine:
         """Rank-independent: a multi-node layout and an (op, dtype, size) the schedule serves."""
         if not self.layout.hier_ok() or self._hier_failed or nbytes % 16 or getattr(op, "is_custom", False):
             return False
-        from .ipc import SUPPORTED_DTYPES
-        if dtype not in SUPPORTED_DTYPES or not self.rccl_ok(op, dtype):
+        if dtype not in _ipc_dtypes() or not self.rccl_ok(op, dtype):
             return False
         return op.code == OpCode.SUM or (op.code in (OpCode.MAX, OpCode.MIN) and dtype.is_floating_point)
 
     def _ipc_ok(self, op, dtype, nbytes) -> bool:
         if not self.ipc_enabled or nbytes % 16 or getattr(op, "is_custom", False):
             return False
-        from .ipc import SUPPORTED_DTYPES
-        if dtype not in SUPPORTED_DTYPES:
+        if dtype not in _ipc_dtypes():
             return False
         if op.code == OpCode.SUM:
             return True
         return op.code in (OpCode.MAX, OpCode.MIN) and dtype in (torch.float32, torch.bfloat16, torch.float16)
 
+    _SEL_MEMO_MAX = 512
+
     def select(self, kind: str, nbytes: int, op, dtype, operand=None) -> str:
-        """Per-call algorithm choice (size tiers, dtype/op support, MP4X_DEVICE_ALGO override)."""
+        """Per-call algorithm choice (size tiers, dtype/op support, MP4X_DEVICE_ALGO override).
+
+        Memoised per call shape: the decision is a pure function of the key below (the forced
+        algorithm, the pinned table's mutation count, the IPC / hierarchical state and the tier
+        thresholds are part of it), so a repeated small collective skips the tier logic — on
+        the latency tier every microsecond of host time is a microsecond of latency."""
+        gen = getattr(self._tuned, "gen", None)
+        memo = getattr(self, "_sel_memo", None)
+        if gen is None or memo is None:
+            return self._select(kind, nbytes, op, dtype, operand)
+        key = (kind, nbytes, op, dtype, getattr(operand, "codec", None), getattr(operand, "compress", False),
+               self.algo, gen, self.ipc_enabled, self.ipc_oneshot_max, self.ipc_twoshot_max, self._hier_failed,
+               self.backend)
+        try:
+            hit = memo.get(key)
+        except TypeError:       # an unhashable custom operator: no memo
+            return self._select(kind, nbytes, op, dtype, operand)
+        if hit is not None:
+            self._select_tuned = hit[1]
+            return hit[0]
+        algo = self._select(kind, nbytes, op, dtype, operand)
+        if len(memo) >= self._SEL_MEMO_MAX:
+            memo.clear()
+        memo[key] = (algo, self._select_tuned)
+        return algo
+
+    def _select(self, kind: str, nbytes: int, op, dtype, operand=None) -> str:
         forced = self.algo
         codec = getattr(operand, "codec", None) if operand is not None else None
         if codec in ("fp8", "bf16") and kind == "allreduce" and \
@@ -559,7 +637,7 @@ class DeviceEngine:
             if nbytes <= self.ipc_oneshot_max:
                 return "ipc1"
             if nbytes <= self.ipc_twoshot_max or (self.backend != "nccl" and self.device.type == "cuda"
-                                                  and os.environ.get("MP4X_DM_LARGE", "auto") != "rccl"):
+                                                  and self._dm_large != "rccl"):
                 return "ipc2"     # (no RCCL underneath: the IPC two-shot takes every size)
         if self.a2a_bytes and nbytes >= self.a2a_bytes:
             return "a2a"
@@ -623,8 +701,10 @@ class DeviceEngine:
         ``scale`` (float dtypes): the result is multiplied by it — the 1/p average of a DP
         gradient sync fused into the collective's own final write (IPC kernels, fp8 requantise)
         or RCCL's ncclAvg, instead of a separate pass over the buffer."""
-        flat = self._flat(arr)
-        view = flat[frm:to]
+        if frm == 0 and arr.dim() == 1 and to == arr.shape[0] and arr.is_contiguous():
+            view = arr                    # the whole 1-D tensor: no view objects on the latency tier
+        else:
+            view = self._flat(arr)[frm:to]
         if scale != 1.0 and not view.is_floating_point():
             raise Mp4jException("allreduce scale= needs a floating-point tensor")
         if out is not None:
@@ -707,13 +787,19 @@ class DeviceEngine:
 
     def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
         """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
+        if algo == "ipc1" or algo == "ipc2":
+            # the latency tier first: a staged one-/two-shot on the default instance, not capturing
+            inst = self._ipc_obj
+            if inst is not None and view.numel() * view.element_size() <= self.ipc_twoshot_max \
+                    and not capturing_now():
+                inst.allreduce(view, op, algo=0 if algo == "ipc1" else 1, scale=scale)   # ipc.ONESHOT / TWOSHOT
+                return True
         algo, grid = zc_grid(algo)
         if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and self.ipc() is None:
             algo = "rccl" if self.rccl_ok(op, view.dtype) else "a2a"
         if algo in ("ipc2z", "ipc2w"):
             peers = self._ipc_obj.registered(view) if self._zc else None
-            if peers is not None and (not torch.cuda.is_current_stream_capturing()
-                                      or self._ipc_obj._epoch_dev is not None):
+            if peers is not None and (not capturing_now() or self._ipc_obj._epoch_dev is not None):
                 scr = self._ipc_obj.scratch_of(view) if algo == "ipc2w" else None
                 if scr is not None:     # posted remote writes only (push form)
                     self._ipc_obj.allreduce_push(view, op, peers, scr, scale=scale)
@@ -721,7 +807,7 @@ class DeviceEngine:
                     self._ipc_obj.allreduce_registered(view, op, peers, scale=scale, grid=grid)
                 return True
             algo = "ipc2"        # not registered (on this rank): the staged two-shot
-        if algo in ("ipc1", "ipc2", "ipc2p") and torch.cuda.is_current_stream_capturing():
+        if algo in ("ipc1", "ipc2", "ipc2p") and capturing_now():
             nb = view.numel() * view.element_size()
             inst = self.ipc_large() if nb > self.ipc_twoshot_max else self._ipc_obj
             if inst is None or inst._epoch_dev is None:
