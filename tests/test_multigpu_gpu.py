@@ -8,7 +8,9 @@ the cross-device paths with no edits:
   (the second call reads the first call's results on the peers: a stale L2 line from the cross-
   GPU coherence protocol would show here — the probe a shared GPU can never fail);
 * the fused fp8 two-shot against the fp64 sum (e4m3 error bound);
-* memAlloc above 2 GiB across GPUs, exact.
+* memAlloc above 2 GiB across GPUs, exact;
+* the node-aware allreduce with simulated nodes of real GPUs (IPC sub-meshes + RCCL
+  sub-communicators).
 """
 import pytest
 
@@ -160,3 +162,27 @@ def test_memalloc_above_2gib_cross_gpu(p):
     out = run_spawn(p, _memalloc_fn, args=(n,), mode="multi", timeout=300)
     for r, (bad, stats) in out.items():
         assert bad == [0, 0], (r, bad)
+
+
+def _hier_fn(comm):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    h = eng.hier()
+    n = (24 << 20) // 4 + 1024
+    x = _pattern(n, r)
+    comm.allreduceArray(x, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
+    torch.cuda.synchronize()
+    return bool(torch.equal(x, _expect(n, p))), h is not None and h.ipc is not None, h.selftest, \
+        eng.stats.get("allreduce.hier", 0)
+
+
+@pytest.mark.parametrize("p,node", [(4, 2), (8, 4)])
+def test_hier_allreduce_cross_gpu(p, node):
+    """Node-aware allreduce with simulated nodes of real GPUs: IPC sub-meshes over xGMI inside
+    each "node", RCCL sub-communicators across them, 8 MiB pipelined pieces."""
+    _need(p)
+    res = run_spawn(p, _hier_fn, timeout=240, mode="multi",
+                    env={"MP4X_SIM_NODE_SIZE": str(node), "MP4X_HIER_PIECE_BYTES": str(8 << 20)})
+    for r, (ok, has_ipc, st, calls) in res.items():
+        assert ok and has_ipc and st["ok"] and calls == 1, (r, ok, has_ipc, st, calls)
