@@ -208,8 +208,20 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
   }
   if (aligned) {
     int64_t nvec = n / W;
-    const int var = k1_variant();
-    if (var == 0) {
+    // the A/B variants (MP4X_K1_VARIANT, tools/bench_kernels.py --variants) are built for f32
+    // only: every other dtype runs the default tile + nontemporal kernel (a quarter of the
+    // template instantiations, which dominated the library's build time)
+    const int var = DT == MP4X_F32 ? k1_variant() : 2;
+    if constexpr (DT != MP4X_F32) {
+      constexpr int U = NIN >= 4 ? 1 : (NIN == 3 ? 2 : 4);
+      int64_t per_block = (int64_t)kBlock * U;
+      int64_t g = (nvec + per_block - 1) / per_block;
+      if (g < 1) g = 1;
+      const int64_t cap = k1_grid_cap();
+      if (cap > 0 && g > cap) g = cap;
+      hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, true>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
+      (void)var;
+    } else if (var == 0) {
       int g = grid_for(nvec > 0 ? nvec : 1, 2);
       hipLaunchKernelGGL((k_reduce_vec<DT, OP, NIN>), dim3(g), dim3(kBlock), 0, st, out, p, nvec, n);
     } else {
