@@ -176,9 +176,9 @@ class HierAllreduce:
 
     # ------------------------------------------------------------------ setup check
     def _self_test(self) -> None:
-        """One exact-pattern hierarchical allreduce (f32 SUM, 4 MiB, two pieces when the piece
-        size allows) through the IPC sub-meshes; any wrong element on any rank drops IPC on every
-        node (agreed through the control plane)."""
+        """One exact-pattern hierarchical allreduce (f32 SUM, 4 MiB) through the IPC sub-meshes;
+        any wrong element or error on any rank drops IPC on every node (agreed through the
+        control plane)."""
         from ..operators import Operators, for_dtype, DType
         eng = self.engine
         bad = None
