@@ -498,3 +498,33 @@ def test_zero_copy_grid_variants_are_candidates_on_a_gpu_of_their_own():
     assert not any(c.startswith("ipc2z_b") for c in e.allreduce_candidates(256 << 20, op, torch.float32))
     e._ipc_obj.shared_gpu, e.backend = False, "gloo"
     assert not any(c.startswith("ipc2z_b") for c in e.allreduce_candidates(256 << 20, op, torch.float32))
+
+
+def test_select_memo_sees_every_state_change():
+    """select() memoises per call shape; a re-tune, a cleared table, a forced algorithm, IPC being
+    switched off or a moved tier threshold must each change the decision at once."""
+    from mp4x import Operands, Operators
+    from mp4x.parallel.device_engine import DeviceEngine, _TunedTable, _tune_key
+    e = object.__new__(DeviceEngine)
+    e.backend, e.device, e.ipc_enabled, e._zc = "nccl", torch.device("cuda", 0), True, True
+    e.ipc_twoshot_max, e.ipc_oneshot_max, e.algo, e.a2a_bytes, e.p = 16 << 20, 256 << 10, "auto", 0, 2
+    e._tuned, e._sel_memo, e._select_tuned = _TunedTable(), {}, False
+    op, opnd = Operators.Float.SUM, Operands.FLOAT_OPERAND()
+    sel = lambda nb=4096: e.select("allreduce", nb, op, torch.float32, opnd)   # noqa: E731
+    assert sel() == "ipc1" and sel() == "ipc1" and len(e._sel_memo) == 1
+    e._tuned[_tune_key(torch.float32, op, 4096)] = "rccl"
+    assert sel() == "rccl" and e._select_tuned
+    e._tuned.clear()
+    assert sel() == "ipc1" and not e._select_tuned
+    e.algo = "a2a"
+    assert sel() == "a2a"
+    e.algo = "auto"
+    e.ipc_oneshot_max = 1024
+    assert sel() == "ipc2"
+    e.ipc_enabled = False
+    assert sel() == "rccl"
+    assert e.select("allreduce", 4096, op, torch.float32, Operands.FLOAT_OPERAND(compress=True)) == "zs"
+    before = e._tuned.gen
+    e._tuned.update({"x": 1})
+    e._tuned.pop("x")
+    assert e._tuned.gen == before + 2
