@@ -52,6 +52,8 @@ class KeyDictionary:
         self.key2id: Dict = {}
         # (dict version, dict, base, ids, rows, {device copies}) of the last complete walk
         self._walk_cache = None
+        # (key objects, ids) of the last complete walk: the native walk's position hint
+        self._hint = None
 
     def unknown(self, keys) -> List:
         """Keys this rank has never numbered (first-seen order, de-duplicated)."""
@@ -701,7 +703,13 @@ def _pack_native(d: "KeyDictionary", mapData):
     n = len(mapData)
     ids = np.empty(n, dtype=np.int64)
     rows = np.empty(n, dtype=np.int64)
-    nmiss, rows_ok = ext.pack(mapData, d.key2id, base, ids, rows)
+    # position hint: a fresh dict built from the same key objects as the last complete walk
+    # takes those ids by pointer compare instead of a dictionary probe per key
+    hint = d._hint if _KEY_HINT else None
+    nmiss, rows_ok, _, keys_t = ext.pack(mapData, d.key2id, base, ids, rows, hint[0] if hint else None,
+                                         hint[1] if hint else None, _KEY_HINT)
+    if _KEY_HINT and not nmiss:
+        d._hint = (keys_t, ids.copy())
     rows = rows if rows_ok else None
     # cache only complete walks (every key numbered; ids never change once given)
     d._walk_cache = (ver, mapData, base, ids.copy(), rows.copy() if rows is not None else None, {}) \
@@ -710,6 +718,7 @@ def _pack_native(d: "KeyDictionary", mapData):
 
 
 _WALK_CACHE = os.environ.get("MP4X_MAP_WALK_CACHE", "1") == "1"
+_KEY_HINT = os.environ.get("MP4X_MAP_KEY_HINT", "1") == "1"
 
 
 def _take_rows(table: torch.Tensor, rows: np.ndarray) -> torch.Tensor:

@@ -322,3 +322,43 @@ def test_native_learn_round_matches_python_union():
     assert nat.id2key == ["known", "a", "b", ("t", 1), "c", 7, "d"]
     with pytest.raises(TypeError):
         ext.learn_keys({}, [], [[["unhashable"]]])
+
+
+def test_native_walk_position_hint():
+    """The native walk's position hint (same key objects, same order as the last complete walk):
+    pointer compares replace dictionary probes; any other key — a new object with an equal value,
+    a moved key, an unknown key — still takes the probe, so ids are always those of key2id."""
+    import numpy as np
+    import torch
+    from mp4x.ops import native
+    from mp4x.parallel.sparse import KeyDictionary, _pack_native
+    ext = native.map_ext()
+    if ext is None:
+        pytest.skip("_mp4x_map not built")
+    d = KeyDictionary()
+    keys = [f"k{i}" for i in range(1000)]
+    d.learn_round([keys])
+    base = torch.randn(1000, 4)
+    rows = base.unbind(0)
+
+    def walk(ks, vals):
+        return _pack_native(d, dict(zip(ks, vals)))
+
+    ids, nmiss, rr, _ = walk(keys, rows)
+    assert nmiss == 0 and np.array_equal(ids, np.arange(1000)) and np.array_equal(rr, np.arange(1000))
+    assert d._hint is not None and len(d._hint[0]) == 1000
+    m = dict(zip(keys, rows))
+    out = np.empty(1000, dtype=np.int64)
+    r2 = np.empty(1000, dtype=np.int64)
+    _, _, hits, _ = ext.pack(m, d.key2id, base, out, r2, d._hint[0], d._hint[1], False)
+    assert hits == 1000 and np.array_equal(out, np.arange(1000))
+    # equal-valued new objects, a reversed order, and a key the dictionary has never seen
+    fresh = ["%s" % k for k in keys[:10]] + keys[10:]
+    ids, nmiss, _, _ = walk(fresh, rows)
+    assert nmiss == 0 and np.array_equal(ids, np.arange(1000))
+    ids, nmiss, _, _ = walk(list(reversed(keys)), rows)
+    assert nmiss == 0 and np.array_equal(ids, np.arange(999, -1, -1))
+    ids, nmiss, _, _ = walk(keys[:500] + ["new"] + keys[501:], rows)
+    assert nmiss == 1 and ids[500] == -1 and np.array_equal(np.delete(ids, 500), np.delete(np.arange(1000), 500))
+    # a walk with a miss keeps the previous hint
+    assert len(d._hint[0]) == 1000 and d._hint[0][0] == "k999"
