@@ -115,6 +115,7 @@ def main():
                                   if os.environ.get("MP4X_SPARSE_IPC", "1") == "1" else "gloo (one GPU: not xGMI)"),
            "dict_per_call": "fresh" if a.fresh_dict else "same (walk cached by PEP 509 version tag)"}
     rec["keys_via"] = "master" if os.environ.get("MP4X_KEYS_VIA_MASTER") == "1" else "peer-to-peer host mesh"
+    rec["key_hint"] = os.environ.get("MP4X_MAP_KEY_HINT", "1") == "1"
     for k in ("first_call_total", "first_call_agree_new_keys", "total", "walk_only", "agree", "to_tensors",
               "exchange_and_kernels", "to_dict"):
         rec[f"{k}_ms_max_rank"] = round(max(v[k] for v in res.values()) * 1e3, 2)
