@@ -1196,6 +1196,9 @@ class DeviceEngine(AutotuneMixin):
                 self.scatter(flat, froms, tos, root)
                 self.allgather(flat, froms, tos)
                 return arr
+            if self.algo in ("", "auto") and self._zc_ok(flat) and self._zc_broadcast(flat, frm, to, root):
+                self._count("broadcast.ipc_zc")
+                return arr
             if self._ipc_small_ok(flat, (to - frm) * flat.element_size()) and \
                     self._ipc_obj.broadcast(flat, frm, to, root):
                 self._count("broadcast.ipc")
@@ -1206,6 +1209,17 @@ class DeviceEngine(AutotuneMixin):
             self._count("broadcast")
             self.coll.broadcast(flat[frm:to], root)
         return arr
+
+    def _zc_broadcast(self, flat: torch.Tensor, frm: int, to: int, root: int) -> bool:
+        """Broadcast on a registered tensor as the zero-copy all-gather whose only non-empty
+        segment is the root's: every other rank pulls ``[frm, to)`` straight from the root's
+        tensor over xGMI, one kernel at any size (no staging, no pieces).  False (nothing done,
+        on every rank alike: ranges and registration are collective facts) otherwise."""
+        if (to - frm) * flat.element_size() <= self.ipc_oneshot_max:
+            return False                      # the latency tier keeps the one-kernel copy plan
+        froms = [frm if j <= root else to for j in range(self.p)]
+        tos = [frm if j < root else to for j in range(self.p)]
+        return self._ipc_obj.allgather_registered(flat, froms, tos)
 
     def _dm_large_ok(self, flat: torch.Tensor) -> bool:
         """Piecewise IPC copy plans for broadcast / scatter / gather / all-gather above the
@@ -1261,6 +1275,15 @@ class DeviceEngine(AutotuneMixin):
             self._reduce_scatter_a2a(flat, froms, tos, op)
             self.gather(flat, froms, tos, root)
             return arr
+        if self.algo in ("", "auto") and nbytes > self.ipc_oneshot_max and self._zc_ok(flat) and \
+                self._ipc_ok(op, view.dtype, nbytes) and not capturing_now():
+            peers = self._ipc_obj.registered(view)
+            if peers is not None:
+                # a registered tensor (collective fact): the zero-copy two-shot, one kernel at any
+                # size; non-root results are unspecified by the reduce contract
+                self._count("reduce.ipc_zc")
+                self._ipc_obj.allreduce_registered(view, op, peers)
+                return arr
         if self.algo in ("", "auto") and self._ipc_ok(op, view.dtype, nbytes) and self._ipc_small_ok(flat, nbytes):
             # latency tier: the IPC allreduce kernels (non-root results are unspecified by the
             # reduce contract, ProcessCommSlave.java:1390-1421, so every rank may receive the sum)

@@ -367,3 +367,36 @@ def test_zero_copy_reduce_scatter_allgather_registered(p):
     for r, (ok_rs, ok_out, ok_ag, stats) in out.items():
         assert ok_rs and ok_out and ok_ag, (r, ok_rs, ok_out, ok_ag)
         assert stats.get("reduce_scatter.ipc_zc") == 1 and stats.get("allgather.ipc_zc") == 1, stats
+
+
+def _zc_rooted_fn(comm, root):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    F = Operands.FLOAT_OPERAND()
+    n = (24 << 20) // 4                            # 24 MiB: above the staging buffer
+    x = comm.memAlloc(n, torch.float32)            # registered from the start
+    i = torch.arange(n, device="cuda")
+    frm, to = 64, n - 128
+    x.copy_((i % 7 + r).float())
+    comm.reduceArray(x, F, Operators.Float.SUM, frm, to, root)
+    exp = (p * (i % 7) + p * (p - 1) // 2).float()
+    ok_red = r != root or bool(torch.equal(x[frm:to], exp[frm:to]))
+    ok_edge = bool(torch.equal(x[:frm], (i[:frm] % 7 + r).float()))
+    x.copy_((i % 5).float() if r == root else torch.full_like(x, -1.0))
+    comm.broadcastArray(x, F, frm, to, root)
+    ok_bc = bool(torch.equal(x[frm:to], (i[frm:to] % 5).float()))
+    ok_bc_edge = r == root or bool((x[:frm] == -1).all()) and bool((x[to:] == -1).all())
+    torch.cuda.synchronize()
+    st = dict(comm.device.stats)
+    comm.memFree(x)
+    return ok_red, ok_edge, ok_bc, ok_bc_edge, st
+
+
+@pytest.mark.parametrize("p,root", [(2, 1), (3, 0), (4, 2)])
+def test_zero_copy_reduce_broadcast_registered(p, root):
+    """reduce / broadcast on a registered (memAlloc) tensor: one zero-copy kernel each (the
+    two-shot; an all-gather whose only segment is the root's), any root, [from, to) ranges."""
+    out = run_spawn(p, _zc_rooted_fn, args=(root,))
+    for r, (ok_red, ok_edge, ok_bc, ok_bc_edge, st) in out.items():
+        assert ok_red and ok_edge and ok_bc and ok_bc_edge, (r, ok_red, ok_edge, ok_bc, ok_bc_edge)
+        assert st.get("reduce.ipc_zc") == 1 and st.get("broadcast.ipc_zc") == 1, st
