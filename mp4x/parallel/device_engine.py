@@ -1312,6 +1312,11 @@ class DeviceEngine(AutotuneMixin):
         flat = self._flat(arr)
         r = self.rank
         t = self._root_tuned("gather", flat[froms[0]:tos[-1]], None)
+        if self.algo in ("", "auto") and t != "p2p" and self._zc_ok(flat) and \
+                (tos[-1] - froms[0]) * flat.element_size() > self.ipc_oneshot_max and \
+                self._ipc_obj.gather_registered(flat, froms, tos, root):
+            self._count("gather.ipc_zc")        # registered tensors: the root pulls from the peers' own
+            return arr
         if t == "ipc" and self.ipc() is not None and self.ipc_large() is not None and \
                 self.ipc_large().gather_large(flat, froms, tos, root):
             self._count("gather.ipc_large")
@@ -1334,6 +1339,11 @@ class DeviceEngine(AutotuneMixin):
         flat = self._flat(arr)
         r = self.rank
         t = self._root_tuned("scatter", flat[froms[0]:tos[-1]], None)
+        if self.algo in ("", "auto") and t != "p2p" and self._zc_ok(flat) and \
+                (tos[-1] - froms[0]) * flat.element_size() > self.ipc_oneshot_max and \
+                self._ipc_obj.scatter_registered(flat, froms, tos, root):
+            self._count("scatter.ipc_zc")       # registered tensors: every rank pulls from the root's
+            return arr
         if t == "ipc" and self.ipc() is not None and self.ipc_large() is not None and \
                 self.ipc_large().scatter_large(flat, froms, tos, root):
             self._count("scatter.ipc_large")

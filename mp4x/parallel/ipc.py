@@ -864,6 +864,51 @@ class IpcAllreduce:
               "mp4x_ipc_allgather(zero-copy)")
         return True
 
+    # ---------------------------------------------------------------- zero-copy gather / scatter
+    # The copy-plan kernel on the registered tensors themselves: pulls read the peers' tensors
+    # (not their staging buffers) and land in this rank's tensor; nothing is staged.  The start
+    # barrier orders the pulls after every owner's earlier writes, the end barrier keeps the
+    # sources unmodified until every pull is done (as for the staged plans).  Epoch tag as the
+    # other zero-copy forms: a rank running the staged plan against these fails at once.
+    def _plan_registered(self, peers, pull, out_ptr, grid_len: int, buf_vecs: int) -> None:
+        self.raise_if_failed()
+        st = stream_ptr()
+        edev = self._next_epoch(st)
+        pp = ptr_array(peers)
+        sa = (c_int64 * 4)()
+        pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
+        check(self.lib.mp4x_ipc_copy_plan(pp[0], self._pp_sig[0], self.rank, self.p, sa, 0, pa, len(pull), None,
+                                          out_ptr if pull else None, grid_len, buf_vecs, self.epoch | ZC_TAG,
+                                          self._grid(grid_len), edev, st), "mp4x_ipc_copy_plan(zero-copy)")
+
+    def gather_registered(self, flat: torch.Tensor, froms, tos, root: int) -> bool:
+        """Root pulls every rank's ``[froms[j], tos[j])`` straight from the peers' registered
+        tensors (16-byte ranges).  False (nothing done, on every rank alike) otherwise."""
+        z = self._zc_segs(flat, froms, tos)
+        if z is None:
+            return False
+        rng, peers, lo, hi = z
+        ln = [h - l_ for l_, h in zip(lo, hi)]
+        if max(ln) == 0:
+            return True
+        pull = [(lo[j], lo[j], ln[j], j) for j in range(self.p) if j != root and ln[j]] if self.rank == root else []
+        self._plan_registered(peers, pull, rng.data_ptr(), max(ln), rng.numel() * rng.element_size() // 16)
+        return True
+
+    def scatter_registered(self, flat: torch.Tensor, froms, tos, root: int) -> bool:
+        """Every rank pulls its ``[froms[r], tos[r])`` straight from the root's registered tensor."""
+        z = self._zc_segs(flat, froms, tos)
+        if z is None:
+            return False
+        rng, peers, lo, hi = z
+        ln = [h - l_ for l_, h in zip(lo, hi)]
+        if max(ln) == 0:
+            return True
+        r = self.rank
+        pull = [(lo[r], lo[r], ln[r], root)] if r != root and ln[r] else []
+        self._plan_registered(peers, pull, rng.data_ptr(), max(ln), rng.numel() * rng.element_size() // 16)
+        return True
+
     # ---------------------------------------------------------------- RS / AG over ragged ranges
     # Results are produced inside the staging buffer (always 16-byte aligned) and copied out, so
     # whether a call qualifies depends only on the (rank-independent) ranges: every rank takes

@@ -386,17 +386,34 @@ def _zc_rooted_fn(comm, root):
     comm.broadcastArray(x, F, frm, to, root)
     ok_bc = bool(torch.equal(x[frm:to], (i[frm:to] % 5).float()))
     ok_bc_edge = r == root or bool((x[:frm] == -1).all()) and bool((x[to:] == -1).all())
+    # gather / scatter over ragged 16-byte ranges of the same registered tensor
+    from mp4x import CommUtils
+    counts = [(n // p) // 4 * 4 - 4 * j for j in range(p)]
+    froms = CommUtils.getFromsFromCount(frm, counts, p)
+    tos = CommUtils.getTosFromCount(frm, counts, p)
+    x.fill_(-1.0)
+    x[froms[r]:tos[r]] = r + 1.0
+    comm.gatherArray(x, F, froms, tos, root)
+    ok_ga = r != root or all(bool((x[froms[j]:tos[j]] == j + 1).all()) for j in range(p))
+    x.fill_(-1.0)
+    if r == root:
+        for j in range(p):
+            x[froms[j]:tos[j]] = 10.0 + j
+    comm.scatterArray(x, F, froms, tos, root)
+    ok_sc = bool((x[froms[r]:tos[r]] == 10.0 + r).all()) and (r == root or bool((x[:froms[0]] == -1).all()))
     torch.cuda.synchronize()
     st = dict(comm.device.stats)
     comm.memFree(x)
-    return ok_red, ok_edge, ok_bc, ok_bc_edge, st
+    return ok_red and ok_ga and ok_sc, ok_edge, ok_bc, ok_bc_edge, st
 
 
 @pytest.mark.parametrize("p,root", [(2, 1), (3, 0), (4, 2)])
 def test_zero_copy_reduce_broadcast_registered(p, root):
-    """reduce / broadcast on a registered (memAlloc) tensor: one zero-copy kernel each (the
-    two-shot; an all-gather whose only segment is the root's), any root, [from, to) ranges."""
+    """reduce / broadcast / gather / scatter on a registered (memAlloc) tensor: one zero-copy kernel
+    each (the two-shot; an all-gather whose only segment is the root's; copy plans that pull
+    straight from the peers' tensors), any root, [from, to) and ragged ranges."""
     out = run_spawn(p, _zc_rooted_fn, args=(root,))
     for r, (ok_red, ok_edge, ok_bc, ok_bc_edge, st) in out.items():
         assert ok_red and ok_edge and ok_bc and ok_bc_edge, (r, ok_red, ok_edge, ok_bc, ok_bc_edge)
         assert st.get("reduce.ipc_zc") == 1 and st.get("broadcast.ipc_zc") == 1, st
+        assert st.get("gather.ipc_zc") == 1 and st.get("scatter.ipc_zc") == 1, st
