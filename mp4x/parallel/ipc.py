@@ -814,6 +814,8 @@ class IpcAllreduce:
     def _zc_segs(self, flat: torch.Tensor, froms, tos):
         es = flat.element_size()
         base = froms[0]
+        if base < 0 or tos[-1] > flat.numel():      # (same-shaped tensors: rank-independent)
+            return None
         rng = flat[base:tos[-1]]
         if not self._zc_regs_ok(rng):
             return None

@@ -388,7 +388,7 @@ def _zc_rooted_fn(comm, root):
     ok_bc_edge = r == root or bool((x[:frm] == -1).all()) and bool((x[to:] == -1).all())
     # gather / scatter over ragged 16-byte ranges of the same registered tensor
     from mp4x import CommUtils
-    counts = [(n // p) // 4 * 4 - 4 * j for j in range(p)]
+    counts = [((n - frm - 64) // p) // 4 * 4 - 4 * j for j in range(p)]
     froms = CommUtils.getFromsFromCount(frm, counts, p)
     tos = CommUtils.getTosFromCount(frm, counts, p)
     x.fill_(-1.0)
