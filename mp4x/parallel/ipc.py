@@ -939,9 +939,14 @@ class IpcAllreduce:
     def _grid(self, nvec: int) -> int:
         """Explicit grid for a per-block-barrier kernel.  ``nvec`` must be RANK-INDEPENDENT (the
         largest segment of any rank): block b of every rank has to exist to meet block b of the
-        peers, so ragged segments may not size the grid per rank."""
+        peers, so ragged segments may not size the grid per rank.
+
+        At least 8 blocks: workgroups are dealt round-robin over the 8 XCDs, so every XCD runs
+        the barriers' system-scope release / acquire (each XCD has its own L2) even when the
+        data would fit fewer blocks — the zero-copy forms read and write the peers' cached
+        tensors."""
         cap = self.max_blocks or 256                   # kIpcMaxBlocks
-        return max(1, min(cap, -(-nvec // 512)))
+        return max(min(8, cap), min(cap, -(-nvec // 512)))
 
     def reduce_scatter(self, view: torch.Tensor, froms, tos, op) -> bool:
         """In place: ``view[froms[r]:tos[r]]`` <- op over all ranks of that range (ragged ranges
