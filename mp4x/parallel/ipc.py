@@ -797,9 +797,9 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
             self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
-        blocks = max(1, min(self.max_blocks, -(-total // 16 // 512))) if self.max_blocks else 0
+        blocks = self._grid(total // 16)               # >= 8: every XCD passes the barriers
         if grid > 0:
-            blocks = min(grid, blocks) if blocks else grid
+            blocks = min(grid, self.max_blocks) if self.max_blocks else grid
         pp = ptr_array(peers)
         check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
                                              self._pp_sig[0], self.rank, self.p, total, None, dst,
