@@ -19,6 +19,16 @@ Algorithm families (selected per call, see :meth:`DeviceEngine.select`):
            all-gather(q, scales) → dequant.  4x fewer bytes than f32 on every link.
 ``p2p``    grouped ncclSend/ncclRecv (batch_isend_irecv) for gather / scatter /
            ragged allgather: the root talks to all peers concurrently.
+``ipc*``   mp4x's own xGMI kernels over IPC-mapped peer memory (parallel/ipc.py,
+           csrc/runtime/ipc.hip): one-shot / two-shot allreduce through staging buffers, and
+           on registered / memAlloc tensors one zero-copy kernel per call for every collective
+           (two-shot pull or push, direct RS / AG, copy plans for the rooted ones).
+``rhd``    recursive halving / doubling over grouped send/recv, K1 per round.
+``hier``   jobs spanning nodes: IPC RS inside each node, RCCL on 1/L of the bytes across
+           nodes, IPC AG (parallel/hier.py).
+
+Autotuning (RCCL vs the IPC forms vs a2a / rhd / hier, exact-probed, agreed, pinned per size
+class) lives in parallel/autotune.py.
 
 Semantics mirror ProcessCommSlave (in place on ``[from, to)`` views, last rank takes the
 remainder in allreduce/reduce splits, rank-order reductions) — see process_comm.py.
