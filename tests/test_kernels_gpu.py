@@ -341,3 +341,26 @@ def test_device_map_pass_is_native_and_exact():
     assert np.array_equal(ids, d.lookup(list(m.keys())))
     got = base.reshape(-1, 32).index_select(0, torch.from_numpy(rows).to(DEV))
     assert torch.equal(got, torch.stack(list(m.values())))
+
+
+def test_reduce_by_key_is_deterministic_in_input_order():
+    """SURVEY §5.2 deterministic mode: the sort-based K5 reduce-by-key sums every key's rows in
+    INPUT order (stable radix sort + sequential segment reduce), so repeated runs are bitwise
+    equal and equal to a float64-free sequential reference in that order."""
+    K = _native()
+    n, dim = 50_000, 8
+    g = torch.Generator(device=DEV).manual_seed(7)
+    keys = torch.randint(0, 500, (n,), device=DEV, dtype=torch.int64, generator=g)
+    vals = (torch.randn(n, dim, device=DEV, generator=g) * 1e3).float()
+    runs = [K.reduce_by_key(keys, vals, int(OpCode.SUM)) for _ in range(3)]
+    for uk, uv, _ in runs[1:]:
+        assert torch.equal(uk, runs[0][0]) and torch.equal(uv, runs[0][1])
+    # sequential f32 sums in input order for a few keys
+    kc, vc = keys.cpu(), vals.cpu()
+    for k in runs[0][0][:5].cpu().tolist():
+        rows = vc[kc == k]
+        acc = rows[0].clone()
+        for r in rows[1:]:
+            acc = acc + r
+        j = int((runs[0][0].cpu() == k).nonzero()[0])
+        assert torch.equal(runs[0][1][j].cpu(), acc), k
