@@ -186,3 +186,47 @@ def test_hier_allreduce_cross_gpu(p, node):
                     env={"MP4X_SIM_NODE_SIZE": str(node), "MP4X_HIER_PIECE_BYTES": str(8 << 20)})
     for r, (ok, has_ipc, st, calls) in res.items():
         assert ok and has_ipc and st["ok"] and calls == 1, (r, ok, has_ipc, st, calls)
+
+
+def _zc_rooted_cross_fn(comm):
+    from mp4x import CommUtils, Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    F = Operands.FLOAT_OPERAND()
+    n = (96 << 20) // 4
+    x = comm.memAlloc(n, torch.float32)
+    root = p - 1
+    x.copy_(_pattern(n, r))
+    comm.reduceArray(x, F, Operators.Float.SUM, 0, n, root)
+    ok = [r != root or bool(torch.equal(x, _expect(n, p)))]
+    base = torch.arange(n, device="cuda", dtype=torch.int32).remainder_(11).float()
+    x.copy_(base if r == root else torch.zeros_like(base))
+    comm.broadcastArray(x, F, 0, n, root)
+    ok.append(bool(torch.equal(x, base)))
+    counts = [n // p] * p
+    counts[-1] += n - sum(counts)
+    fr, to = CommUtils.getFromsFromCount(0, counts, p), CommUtils.getTosFromCount(0, counts, p)
+    x.fill_(-1.0)
+    x[fr[r]:to[r]] = r + 1.0
+    comm.gatherArray(x, F, fr, to, root)
+    ok.append(r != root or all(bool((x[fr[j]:to[j]] == j + 1).all()) for j in range(p)))
+    x.fill_(-1.0)
+    if r == root:
+        for j in range(p):
+            x[fr[j]:to[j]] = 10.0 + j
+    comm.scatterArray(x, F, fr, to, root)
+    ok.append(bool((x[fr[r]:to[r]] == 10.0 + r).all()))
+    torch.cuda.synchronize()
+    st = {k: v for k, v in comm.device.stats.items() if k.endswith("ipc_zc")}
+    comm.memFree(x)
+    return ok, st
+
+
+@pytest.mark.parametrize("p", [2, 8])
+def test_zero_copy_rooted_cross_gpu(p):
+    """reduce / broadcast / gather / scatter on a memAlloc tensor across real GPUs: one zero-copy
+    kernel each, pulling over xGMI from the peers' tensors."""
+    _need(p)
+    res = run_spawn(p, _zc_rooted_cross_fn, timeout=240, mode="multi")
+    for r, (ok, st) in res.items():
+        assert all(ok), (r, ok)
+        assert all(st.get(f"{k}.ipc_zc") == 1 for k in ("reduce", "broadcast", "gather", "scatter")), st
