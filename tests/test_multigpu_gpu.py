@@ -10,7 +10,8 @@ the cross-device paths with no edits:
 * the fused fp8 two-shot against the fp64 sum (e4m3 error bound);
 * memAlloc above 2 GiB across GPUs, exact;
 * the node-aware allreduce with simulated nodes of real GPUs (IPC sub-meshes + RCCL
-  sub-communicators).
+  sub-communicators);
+* the zero-copy reduce / broadcast / gather / scatter on memAlloc tensors across GPUs.
 """
 import pytest
 
