@@ -553,7 +553,13 @@ class IpcAllreduce:
         return None, 0
 
     def registered(self, view: torch.Tensor):
-        """Peer pointers of ``view`` when it lies inside a registered tensor, else None."""
+        """Peer pointers of ``view`` when it lies inside a registered tensor and is a whole number
+        of 16-byte vectors at a 16-byte aligned address (what the zero-copy kernels move), else
+        None — a [from, to) view off that grid takes the staged kernels.  The alignment of a
+        view is rank-independent: every rank's registered allocation is 16-byte aligned and
+        the range is the same on every rank."""
+        if view.data_ptr() % 16 or (view.numel() * view.element_size()) % 16:
+            return None
         reg, d = self._find(view)
         if reg is None:
             return None

@@ -417,3 +417,29 @@ def test_zero_copy_reduce_broadcast_registered(p, root):
         assert ok_red and ok_edge and ok_bc and ok_bc_edge, (r, ok_red, ok_edge, ok_bc, ok_bc_edge)
         assert st.get("reduce.ipc_zc") == 1 and st.get("broadcast.ipc_zc") == 1, st
         assert st.get("gather.ipc_zc") == 1 and st.get("scatter.ipc_zc") == 1, st
+
+
+def _zc_offgrid_fn(comm):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    F = Operands.FLOAT_OPERAND()
+    n = (4 << 20) // 4
+    x = torch.empty(n, device="cuda")
+    assert comm.registerBuffer(x)
+    x.copy_(_pattern(n, r))
+    comm.allreduceArray(x, F, Operators.Float.SUM, 3, n - 1)          # off the 16-byte grid
+    ok_ar = bool(torch.equal(x[3:n - 1], _expect(n, p)[3:n - 1])) and bool(torch.equal(x[:3], _pattern(n, r)[:3]))
+    x.copy_(_pattern(n, r))
+    comm.reduceArray(x, F, Operators.Float.SUM, 1, n - 2, 0)
+    ok_red = r != 0 or bool(torch.equal(x[1:n - 2], _expect(n, p)[1:n - 2]))
+    torch.cuda.synchronize()
+    return ok_ar, ok_red, dict(comm.device.stats)
+
+
+def test_registered_tensor_views_off_the_16_byte_grid():
+    """[from, to) views of a registered tensor that are not whole 16-byte vectors at 16-byte
+    aligned addresses take the staged kernels (same decision on every rank), exactly."""
+    out = run_spawn(2, _zc_offgrid_fn)
+    for r, (ok_ar, ok_red, st) in out.items():
+        assert ok_ar and ok_red, (r, ok_ar, ok_red, st)
+        assert not any(k.endswith("ipc2z") or k.endswith("ipc_zc") for k in st), st
