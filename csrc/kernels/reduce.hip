@@ -168,9 +168,17 @@ static int64_t g_k1_grid = -1;
 static int64_t k1_grid_cap() {
   if (g_k1_grid < 0) {
     const char* e = getenv("MP4X_K1_GRID");
-    g_k1_grid = e ? atoll(e) : 0;      // 0: one tile per block (no cap)
+    g_k1_grid = e ? atoll(e) : -2;     // unset: per fan-in default (k1_grid_for)
   }
   return g_k1_grid;
+}
+// Grid cap of a launch with NIN inputs: MP4X_K1_GRID when set (0 = one tile per block), else
+// 8192 grid-strided blocks for the single-input copy (in-situ N=1 bench A/B, interleaved rounds:
+// 2992 vs 2957 GB/s mean, profiles/r3/k1/n1_grid_cap_ab.txt) and one tile per block from two
+// inputs up (a capped grid measured 20% slower at NIN >= 4, profiles/r1/k1_grid_cap.txt).
+static int64_t k1_grid_for(int nin) {
+  const int64_t c = k1_grid_cap();
+  return c >= 0 ? c : (nin == 1 ? 8192 : 0);
 }
 
 static int g_k1_variant = -1;
@@ -217,7 +225,7 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
       int64_t per_block = (int64_t)kBlock * U;
       int64_t g = (nvec + per_block - 1) / per_block;
       if (g < 1) g = 1;
-      const int64_t cap = k1_grid_cap();
+      const int64_t cap = k1_grid_for(NIN);
       if (cap > 0 && g > cap) g = cap;
       hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, true>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
       (void)var;
@@ -234,7 +242,7 @@ static int launch_nin(void* out, const void* const* ins, int64_t n, hipStream_t 
       int64_t per_block = (int64_t)kBlock * u;
       int64_t g = (nvec + per_block - 1) / per_block;
       if (g < 1) g = 1;
-      const int64_t cap = k1_grid_cap();
+      const int64_t cap = k1_grid_for(NIN);
       if (cap > 0 && g > cap) g = cap;
       if (var == 1)
         hipLaunchKernelGGL((k_reduce_tile<DT, OP, NIN, U, false>), dim3((unsigned)g), dim3(kBlock), 0, st, out, p, nvec, n);
