@@ -6,13 +6,15 @@ timeout -k 10 120 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/n1prof/s
   > gpurun_out/n1prof/stats.log 2>&1 || exit 1
 grep '^{' gpurun_out/n1prof/stats.log | cut -c1-200
 find gpurun_out/n1prof/stats -name '*kernel_stats.csv' -exec cp {} gpurun_out/n1prof/n1_kernel_stats.csv \;
-cut -d, -f1-6 gpurun_out/n1prof/n1_kernel_stats.csv | head -4
-timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE WRITE_SIZE -f csv -d gpurun_out/n1prof/pmc -o n1 -- python3 bench.py --steps 3 --warmup 1 \
-  > gpurun_out/n1prof/pmc.log 2>&1 || exit 1
-find gpurun_out/n1prof/pmc -name '*counter_collection.csv' -exec cp {} gpurun_out/n1prof/n1_pmc.csv \;
+python3 -c "import csv; [print(r['Name'][:60], r['Calls'], r['AverageNs']) for r in list(csv.DictReader(open('gpurun_out/n1prof/n1_kernel_stats.csv')))[:3]]"
+for c in FETCH_SIZE WRITE_SIZE; do   # one counter set per run (FETCH_SIZE takes 3 TCC counters)
+  timeout -s KILL 90 rocprofv3 --pmc $c -f csv -d gpurun_out/n1prof/pmc_$c -o n1 -- python3 bench.py --steps 3 --warmup 1 \
+    > gpurun_out/n1prof/pmc_$c.log 2>&1 || exit 1
+  find gpurun_out/n1prof/pmc_$c -name '*counter_collection.csv' -exec cp {} gpurun_out/n1prof/n1_pmc_$c.csv \;
+done
 python3 - <<'PY'
 import csv, collections
-rows = list(csv.DictReader(open("gpurun_out/n1prof/n1_pmc.csv")))
+rows = [r for c in ("FETCH_SIZE", "WRITE_SIZE") for r in csv.DictReader(open(f"gpurun_out/n1prof/n1_pmc_{c}.csv"))]
 agg = collections.defaultdict(list)
 for r in rows:
     if "k_reduce_tile" in r["Kernel_Name"]:
