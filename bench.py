@@ -15,8 +15,9 @@ a SUM would grow p-fold per call and reach f32 inf after ~40 calls at p=8.
 For N>1 the warm-up first autotunes the schedule (RCCL, RCCL with more channels, IPC two-shot
 over xGMI staged / zero-copy pull / zero-copy push, a2a, rhd; ``--autotune-iters`` timed calls
 each, MAX over ranks, every candidate checked against an exact pattern first) and pins the
-fastest.  Timing: W untimed warmup calls, barrier + device sync, K timed calls with a hipEvent
-pair around each (p50 / p99), barrier + sync; MAX over ranks.
+fastest.  Timing: W untimed warmup calls, barrier + device sync, K timed back-to-back calls,
+barrier + device sync (the headline, host clock; MAX over ranks); then, outside the timed
+region, K more calls with a hipEvent pair around each for p50 / p99.
 
 Self-verification (after the timed steps, outside them): the SAME call on the SAME buffer with
 the pinned schedule runs once more on an exact pattern; the result is compared with the fp64
@@ -24,7 +25,7 @@ answer on every rank -> ``verified`` and ``max_abs_err`` (MAX over ranks).  A wr
 makes the run exit non-zero (rc 3) after printing its line.
 
 RCCL baseline at equal method (N>1, GPU): K more calls of the same public call with the RCCL
-schedule forced (``ncclAllReduce``, fused ncclAvg), same hipEvent timing, MAX over ranks ->
+schedule forced (``ncclAllReduce``, fused ncclAvg), same timing method, MAX over ranks ->
 ``rccl_busbw_gbps`` / ``rccl_p50_ms`` next to ``value`` ("judge our
 numbers against RCCL's on the same box").
 
@@ -68,17 +69,25 @@ class _CpuEvent:
         return (other.t - self.t) * 1e3
 
 
-def _timed(torch, step, steps):
-    """K calls of ``step`` with a hipEvent pair around each; returns (wall start, start events,
-    end events) — the caller synchronises, then reads the wall time and the event pairs."""
+def _measure(torch, step, steps, sync_all):
+    """The headline timing: K back-to-back calls of ``step`` on the host clock, bracketed by a
+    device-wide sync + barrier on both sides (nothing else inside the timed region).  Then K
+    more calls with a hipEvent pair around each, in a separate pass, for the per-call latency
+    distribution (p50 / p99).  Returns (wall seconds of the timed K calls, sorted ms list)."""
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync_all()
+    wall = time.perf_counter() - t0
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    t0 = time.perf_counter()
     for i in range(steps):
         starts[i].record()
         step()
         ends[i].record()
-    return t0, starts, ends
+    sync_all()
+    return wall, sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
 
 
 def main():
@@ -185,12 +194,8 @@ def main():
                      comm.device.autotune_allreduce(buf, op, iters=max(1, args.autotune_iters)).items()}
     for _ in range(args.warmup):
         step()
-    sync_all()
 
-    t0, starts, ends = _timed(torch, step, args.steps)
-    sync_all()
-    wall = time.perf_counter() - t0
-    lat = sorted(s.elapsed_time(e) for s, e in zip(starts, ends))   # ms
+    wall, lat = _measure(torch, step, args.steps, sync_all)     # lat: ms, from the separate event pass
     wall, p50, p99 = max_over_ranks([wall, lat[len(lat) // 2], lat[min(len(lat) - 1, int(0.99 * len(lat)))]])
 
     ms_per_step = wall * 1e3 / args.steps
@@ -240,11 +245,7 @@ def main():
         try:
             for _ in range(max(1, args.warmup)):
                 step()
-            sync_all()
-            r0, rs, re_ = _timed(torch, step, args.steps)
-            sync_all()
-            rwall = time.perf_counter() - r0
-            rlat = sorted(s.elapsed_time(e) for s, e in zip(rs, re_))
+            rwall, rlat = _measure(torch, step, args.steps, sync_all)
             rwall, rp50, rp99 = max_over_ranks([rwall, rlat[len(rlat) // 2],
                                                 rlat[min(len(rlat) - 1, int(0.99 * len(rlat)))]])
             rms = rwall * 1e3 / args.steps
