@@ -1383,6 +1383,9 @@ class DeviceEngine(AutotuneMixin):
         self._count("all_to_all_v")
         if sum(send_counts) != send.shape[0]:
             raise Mp4jException(f"sendCounts sum {sum(send_counts)} != rows {send.shape[0]}")
+        got = self._all_to_all_v_ipc(send, send_counts, recv)
+        if got is not None:
+            return got
         sc = torch.tensor(send_counts, dtype=torch.int64, device=self.device if self.backend == "nccl" else "cpu")
         rc = torch.empty_like(sc)
         self.coll.all_to_all_single(rc, sc)
@@ -1394,6 +1397,34 @@ class DeviceEngine(AutotuneMixin):
             raise Mp4jException(f"recvData shape {tuple(recv.shape)} != {shape}")
         self.coll.all_to_all_single(recv, send.contiguous(), recv_counts, list(send_counts))
         return recv, recv_counts
+
+    def _all_to_all_v_ipc(self, send: torch.Tensor, send_counts: List[int], recv: Optional[torch.Tensor]):
+        """The all-to-all-v as one IPC copy-plan kernel (sparse._ipc_rows_alltoallv) when the rows
+        are whole 16-byte vectors and the largest rank's payload fits a staging buffer; the count
+        matrix comes from one small all-gather.  Every condition is rank-independent (shape,
+        dtype, environment, the gathered counts), so every rank takes the same path; None when
+        the call does not qualify."""
+        from . import sparse
+        width = 1
+        for d in send.shape[1:]:
+            width *= int(d)
+        rb = width * send.element_size()          # bytes per row
+        if rb == 0 or rb % 16 or self.algo not in ("", "auto", "ipc") or not send.is_cuda or \
+                not sparse._sparse_ipc_ok(self, send):
+            return None
+        mat = sparse._count_matrix(self, torch.tensor(list(send_counts), dtype=torch.int64, device=send.device))
+        recv_counts = [mat[j][self.rank] for j in range(self.p)]
+        shape = (sum(recv_counts),) + tuple(send.shape[1:])
+        if recv is not None and tuple(recv.shape) != shape:
+            raise Mp4jException(f"recvData shape {tuple(recv.shape)} != {shape}")
+        out = sparse._ipc_rows_alltoallv(self, send.contiguous().view(torch.uint8).view(send.shape[0], rb), mat)
+        if out is None:
+            return None
+        res = out.view(send.dtype).view(shape)
+        if recv is not None:
+            recv.copy_(res)
+            res = recv
+        return res, recv_counts
 
     def reduce_map(self, mapData: Dict, operator, root: int):
         from .sparse import reduce_map_device

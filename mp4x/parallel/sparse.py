@@ -307,6 +307,36 @@ def _ipc_alltoallv(engine, skeys, svals, mat: List[List[int]]):
     return _unpack_records(out, svals, wb)
 
 
+def _ipc_rows_alltoallv(engine, rows: torch.Tensor, mat: List[List[int]]):
+    """Dense all-to-all-v of ``rows`` (uint8 [n, rb], rb a 16-byte multiple, grouped by
+    destination) over the IPC mesh — ``alltoallArray``'s expert-parallel style routing as ONE
+    copy-plan kernel: this rank stages its whole send buffer, every rank pulls its block from
+    every peer at once.  ``mat[i][j]`` = rows rank i sends to rank j (every rank knows it).
+    Returns the received rows in source-rank order, or None when the largest rank's payload
+    does not fit the staging buffers (rank-independent)."""
+    p, r = engine.p, engine.rank
+    rb = rows.shape[1]
+    v = rb // 16
+    inst = _ipc_inst(engine, max(sum(row) for row in mat) * rb)
+    if inst is None:
+        return None
+    n = sum(mat[r])
+    src = rows if rows.data_ptr() % 16 == 0 else rows.clone()
+    stage = [(0, 0, n * v, 0)] if n else []
+    pulls, off = [], 0
+    for j in range(p):
+        s0 = sum(mat[j][:r])                      # rank j's block for this rank, in its buffer
+        if mat[j][r]:
+            pulls.append((s0 * v, off * v, mat[j][r] * v, j))
+        off += mat[j][r]
+    out = torch.empty((off, rb), dtype=torch.uint8, device=rows.device)
+    glen = max(sum(row) for row in mat) * v       # sizes the grid: rank-independent
+    if glen:
+        inst._plan(stage, pulls, src.data_ptr() if stage else None, out.data_ptr() if pulls else None, glen)
+    engine._count("all_to_all_v.ipc")
+    return out
+
+
 def _ipc_allgatherv(engine, keys, vals, sizes: List[int]):
     """Every rank's (keys, rows), rank order, over the IPC mesh (see above), or None."""
     wb = _rec_width(vals)

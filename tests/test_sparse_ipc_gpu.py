@@ -59,3 +59,38 @@ def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty):
             assert used.get("sparse.a2a.ipc") == 1 and used.get("sparse.allgatherv.ipc") == 2, used
         else:
             assert "sparse.a2a.ipc" not in used, used
+
+
+def _a2a_fn(comm, dim, dtype_name):
+    import torch
+    from mp4x import Mp4jException  # noqa: F401
+    r, p = comm.getRank(), comm.getSlaveNum()
+    dt = getattr(torch, dtype_name)
+    counts = [(r + 1) * 37 + 11 * j for j in range(p)]
+    rows = []
+    for j in range(p):
+        blk = torch.arange(counts[j] * dim, device="cuda").view(counts[j], dim).to(dt) + 1000 * r + 100 * j
+        rows.append(blk)
+    send = torch.cat(rows)
+    recv, rc = comm.alltoallArray(send, counts)
+    exp_counts = [(j + 1) * 37 + 11 * r for j in range(p)]
+    ok = rc == exp_counts
+    off = 0
+    for j in range(p):
+        exp = torch.arange(exp_counts[j] * dim, device="cuda").view(exp_counts[j], dim).to(dt) + 1000 * j + 100 * r
+        ok = ok and bool(torch.equal(recv[off:off + exp_counts[j]], exp))
+        off += exp_counts[j]
+    torch.cuda.synchronize()
+    return ok, dict(comm.device.stats)
+
+
+@pytest.mark.parametrize("p,dim,dtype_name,ipc", [(2, 16, "float32", True), (4, 8, "bfloat16", True),
+                                                   (3, 3, "float32", False)])
+def test_alltoallv_rows_over_ipc(p, dim, dtype_name, ipc):
+    """alltoallArray (expert-parallel routing): rows of whole 16-byte vectors go through ONE IPC
+    copy-plan kernel (every rank pulls its block from every peer at once); other row widths take
+    the transport's all-to-all.  Ragged counts, exact."""
+    out = run_spawn(p, _a2a_fn, args=(dim, dtype_name))
+    for r, (ok, st) in out.items():
+        assert ok, r
+        assert (st.get("all_to_all_v.ipc", 0) == 1) == ipc, st
