@@ -1346,7 +1346,8 @@ class IpcAllreduce:
     def _blocks_for_waves(self, waves: int) -> int:
         if not self.max_blocks:
             return 0
-        return max(1, min(self.max_blocks, -(-waves // 8)))
+        cap = max(1, self.max_blocks // max(1, int(os.environ.get("MP4X_FP8_BLOCK_DIV", "1"))))
+        return max(1, min(cap, -(-waves // 8)))
 
     def prepare_graph(self):
         """Move the epoch counter to device memory so hipGraph replays get fresh epochs.
