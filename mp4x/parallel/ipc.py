@@ -1344,9 +1344,15 @@ class IpcAllreduce:
         return view
 
     def _blocks_for_waves(self, waves: int) -> int:
+        """Grid of the fused fp8 two-shot.  On a GPU shared by the ranks (rehearsals) every rank's
+        blocks must be resident at once for the per-block barriers; this kernel (512 threads, a
+        40 KB LDS tile and a heavy register load per block) fits about half as many blocks per
+        CU as the generic budget assumes, so it takes half the shared grid
+        (``MP4X_FP8_BLOCK_DIV``, default 2): with the full budget, 8 ranks stalled at the start
+        barrier; with half, config 5 at 8 ranks runs exact (profiles/r3/configs_s2/)."""
         if not self.max_blocks:
             return 0
-        cap = max(1, self.max_blocks // max(1, int(os.environ.get("MP4X_FP8_BLOCK_DIV", "1"))))
+        cap = max(1, self.max_blocks // max(1, int(os.environ.get("MP4X_FP8_BLOCK_DIV", "2"))))
         return max(1, min(cap, -(-waves // 8)))
 
     def prepare_graph(self):
