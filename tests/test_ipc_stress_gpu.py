@@ -90,3 +90,72 @@ def test_ipc_protocol_random_soak(p, seed):
             if pr.is_alive():
                 pr.kill()
         m.stop(timeout=5)
+
+
+def _zc_soak_fn(comm, seed, iters):
+    import random
+
+    import torch
+    from mp4x import CommUtils, Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    F = Operands.FLOAT_OPERAND()
+    n = (48 << 20) // 4
+    x = comm.memAlloc(n, torch.float32)
+    rng = random.Random(seed)
+    bad = []
+    for it in range(iters):
+        op = rng.choice(["allreduce", "reduce", "broadcast", "gather", "scatter", "reduce_scatter", "allgather"])
+        root = rng.randrange(p)
+        a = rng.randrange(0, n // 2) // 4 * 4                      # 16-byte grid
+        b = min(n, a + rng.choice([1 << 16, 1 << 20, 3 << 20, 10 << 20]) // 4 * 4)
+        idx = torch.arange(a, b, device="cuda", dtype=torch.int64)
+        base = ((idx % 13) + it).float()
+        if op in ("allreduce", "reduce"):
+            x[a:b] = base + r
+            (comm.allreduceArray(x, F, Operators.Float.SUM, a, b) if op == "allreduce"
+             else comm.reduceArray(x, F, Operators.Float.SUM, a, b, root))
+            exp = base * p + p * (p - 1) // 2
+            ok = (op == "reduce" and r != root) or bool(torch.equal(x[a:b], exp))
+        elif op == "broadcast":
+            x[a:b] = base if r == root else -1.0
+            comm.broadcastArray(x, F, a, b, root)
+            ok = bool(torch.equal(x[a:b], base))
+        else:
+            m = b - a
+            counts = [(m // p) // 4 * 4] * p
+            counts[-1] = m - sum(counts[:-1])
+            fr, to = CommUtils.getFromsFromCount(a, counts, p), CommUtils.getTosFromCount(a, counts, p)
+            if op == "reduce_scatter":
+                x[a:b] = base + r
+                comm.reduceScatterArray(x, F, Operators.Float.SUM, a, counts)
+                exp = base * p + p * (p - 1) // 2
+                ok = bool(torch.equal(x[fr[r]:to[r]], exp[fr[r] - a:to[r] - a]))
+            else:
+                x[a:b] = -1.0
+                if op == "scatter":
+                    if r == root:
+                        x[a:b] = base
+                    comm.scatterArray(x, F, fr, to, root)
+                    ok = bool(torch.equal(x[fr[r]:to[r]], base[fr[r] - a:to[r] - a]))
+                else:
+                    x[fr[r]:to[r]] = base[fr[r] - a:to[r] - a]
+                    (comm.gatherArray(x, F, fr, to, root) if op == "gather" else comm.allgatherArray(x, F, fr, to))
+                    ok = (op == "gather" and r != root) or bool(torch.equal(x[a:b], base))
+        if not ok:
+            bad.append((it, op, root, a, b))
+    torch.cuda.synchronize()
+    zc = sum(v for k, v in comm.device.stats.items() if k.endswith("ipc_zc") or k.endswith("ipc2z"))
+    comm.memFree(x)
+    return bad, zc
+
+
+@pytest.mark.parametrize("p,seed", [(3, 5), (4, 6)])
+def test_zero_copy_random_soak(p, seed):
+    """The zero-copy forms of all 7 collectives on one memAlloc arena, a seeded random sequence of
+    ops, roots and 16-byte-grid ranges (overlapping from call to call), every result exact."""
+    from spawn_ranks import run_spawn
+    iters = 60
+    out = run_spawn(p, _zc_soak_fn, args=(seed, iters), timeout=300)
+    for r, (bad, zc) in out.items():
+        assert not bad, (r, bad[:5])
+        assert zc >= iters // 2, zc
