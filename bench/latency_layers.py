@@ -39,7 +39,7 @@ def worker(port, q, nbytes, iters):
     def raw():
         inst.epoch = (inst.epoch + 1) & 0x3FFFFFFF or 1
         lib.mp4x_ipc_allreduce_ex(ipcm.ONESHOT, dt, int(fop.code), inst._pp_data[0], inst._pp_sig[0], inst.rank,
-                                  inst.p, nbytes, x.data_ptr(), x.data_ptr(), inst.epoch, inst.max_blocks and 8,
+                                  inst.p, nbytes, x.data_ptr(), x.data_ptr(), inst.epoch, 8 if inst.shared_gpu else 0,
                                   None, 1.0, st)
     layers = {"api": lambda: comm.allreduceArray(x, opnd, op, 0, n),
               "engine": lambda: eng.allreduce(x, 0, n, op, opnd),

@@ -1,0 +1,168 @@
+// One-shot / two-shot allreduce over IPC-mapped peer buffers (see ipc_common.hpp for the
+// protocol).  Every (dtype, op) pair of the reference's operator table runs here; the hot pairs
+// with a compile-time combine, the others through the runtime-op kernel (kOpRt).
+#include "ipc_common.hpp"
+
+namespace mp4x {
+
+// src != nullptr: the kernel stages its own input (fused copy-in, one launch instead of a
+// memcpy + kernel): block b copies exactly the vectors block b of every peer will read, then
+// meets them at the start barrier (whose release fence publishes the copies).
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
+                                                              u32x4* __restrict__ out, uint32_t epoch,
+                                                              const uint32_t* epoch_dev,
+                                                              const u32x4* __restrict__ src, float scale, int op) {
+  constexpr int p = NR;
+  epoch = resolve_epoch(epoch, epoch_dev);
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  if (src) {
+    u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+    for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride) mine[v] = src[v];
+  }
+  if (!block_barrier(P, 0, rank, p, epoch, self)) return;
+  for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
+    out[v] = reduce_vec<DT, OP, NR>(P, v, scale, op);
+  block_barrier(P, 2, rank, p, epoch, self);
+}
+
+// two-shot: direct reduce-scatter into own buffer chunk `rank`, then direct all-gather.
+template <int DT, int OP, int NR>
+__global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
+                                                              u32x4* __restrict__ out, uint32_t epoch,
+                                                              const uint32_t* epoch_dev,
+                                                              const u32x4* __restrict__ src, float scale, int op) {
+  constexpr int p = NR;
+  MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
+  epoch = resolve_epoch(epoch, epoch_dev);
+  const int64_t chunk = (nvec + p - 1) / p;
+  const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
+  const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
+  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  if (src) {   // fused copy-in: block b stages the chunk offsets block b of every peer reads
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t b = (int64_t)k * chunk;
+      const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+      for (int64_t v = b + off0; v < e; v += stride) mine[v] = src[v];
+    }
+  }
+  if (!block_barrier(P, 0, rank, p, epoch, self)) return;
+  {
+    const int64_t b = (int64_t)rank * chunk;
+    const int64_t e = b + chunk < nvec ? b + chunk : nvec;
+    // zero-copy form: `out` IS this rank's registered buffer (== mine), one store per vector
+    const bool zc = out == mine;
+    for (int64_t v = b + off0; v < e; v += stride) {
+      u32x4 o = reduce_vec<DT, OP, NR>(P, v, scale, op);
+      mine[v] = o;
+      if (!zc) out[v] = o;
+    }
+  }
+  if (!block_barrier(P, 1, rank, p, epoch, self)) return;
+  // all-gather: every thread pulls the same chunk offset from ALL p-1 peers at once, so all
+  // xGMI links stream concurrently (peer after peer would leave one link busy at a time).
+  // k is a compile-time index: no dynamic indexing of the kernarg pointer table.
+  for (int64_t v = off0; v < chunk; v += stride) {
+    u32x4 x[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec) x[k] = reinterpret_cast<const u32x4*>(P.data[k])[idx];
+    }
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int64_t idx = (int64_t)k * chunk + v;
+      if (k != rank && idx < nvec) out[idx] = x[k];
+    }
+  }
+  block_barrier(P, 2, rank, p, epoch, self);
+}
+
+}  // namespace mp4x
+
+using namespace mp4x;
+
+// algo 0 = one-shot, 1 = two-shot.  data_ptrs / signal_ptrs: p entries (own rank included,
+// peers as mapped by mp4x_ipc_open_handle).  nbytes must be a multiple of 16.
+// epoch_dev == NULL: `epoch` (host counter) is used.  epoch_dev != NULL: graph-capturable form,
+// the kernel reads the epoch from device memory (bump it with mp4x_ipc_bump_epoch first).
+// src != NULL: this rank's input (16-byte aligned) is copied into its own buffer INSIDE the
+// kernel (fused copy-in: one launch per call); NULL: already staged, or zero-copy (the data
+// pointers are the registered caller tensors and out == data_ptrs[rank]).  scale != 1: the
+// reduced value is multiplied by it before it is stored (fused average; float dtypes only).
+// op: any operator of the reference table valid for dtype (MP4X_E_UNSUPPORTED otherwise).
+extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                     int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
+                                     int blocks, const uint32_t* epoch_dev, float scale, void* stream) {
+  if ((nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
+  if (((uintptr_t)out & 15) || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
+  if (scale != 1.0f && !float_dtype(dtype)) return MP4X_E_BADARG;
+  IpcPtrs P;
+  if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
+  const int64_t nvec = nbytes / 16;
+  if (blocks <= 0) {
+    int64_t b = (nvec + kIpcThreads - 1) / kIpcThreads;
+    // one-shot (latency tier): up to 128 blocks; two-shot: up to one block per CU so large
+    // messages keep enough remote requests in flight on every link
+    const int64_t cap = algo == 0 ? 128 : kIpcMaxBlocks;
+    blocks = (int)(b < 1 ? 1 : (b > cap ? cap : b));
+  }
+  if (blocks > kIpcMaxBlocks) blocks = kIpcMaxBlocks;
+  Signal* self = (Signal*)signal_ptrs[rank];
+  hipStream_t st = (hipStream_t)stream;
+  const u32x4* srcv = (const u32x4*)src;
+  u32x4* outv = (u32x4*)out;
+  return with_dtype(dtype, [&](auto dtc) {
+    constexpr int DT = decltype(dtc)::value;
+    return with_op<DT>(op, [&](auto opc) {
+      constexpr int OP = decltype(opc)::value;
+      return with_nr(p, [&](auto nrc) {
+        constexpr int NR = decltype(nrc)::value;
+        if (algo == 0)
+          hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,
+                             nvec, outv, epoch, epoch_dev, srcv, scale, op);
+        else
+          hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,
+                             nvec, outv, epoch, epoch_dev, srcv, scale, op);
+        return (int)hipGetLastError();
+      });
+    });
+  });
+}
+
+// The pre-staged form (no fused copy-in, no scale).
+extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                  int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream) {
+  return mp4x_ipc_allreduce_ex(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, nullptr, out, epoch, blocks,
+                               epoch_dev, 1.0f, stream);
+}
+
+// Does the IPC allreduce have a kernel for (dtype, op)?  1 / 0.
+extern "C" int mp4x_ipc_op_supported(int dtype, int op) {
+  return with_dtype(dtype, [&](auto dtc) {
+    constexpr int DT = decltype(dtc)::value;
+    return with_op<DT>(op, [&](auto) { return 1; }) == 1 ? 1 : 0;
+  }) == 1 ? 1 : 0;
+}
+
+// Blocks per CU the occupancy API admits for the kernel a call of (algo, dtype, op, p) launches
+// (the shared-GPU co-residency budget, mp4x/parallel/occupancy.py).
+extern "C" int mp4x_ipc_occupancy_ar(int algo, int dtype, int op, int p, int* blocks_per_cu) {
+  int m = 1 << 30;
+  int e = with_dtype(dtype, [&](auto dtc) {
+    constexpr int DT = decltype(dtc)::value;
+    return with_op<DT>(op, [&](auto opc) {
+      constexpr int OP = decltype(opc)::value;
+      return with_nr(p, [&](auto nrc) {
+        constexpr int NR = decltype(nrc)::value;
+        if (algo == 0) occ_min(k_ipc_oneshot<DT, OP, NR>, &m);
+        else occ_min(k_ipc_twoshot<DT, OP, NR>, &m);
+        return 0;
+      });
+    });
+  });
+  *blocks_per_cu = m == (1 << 30) ? 0 : m;
+  return e;
+}

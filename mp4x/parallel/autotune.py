@@ -159,6 +159,8 @@ class AutotuneMixin:
         if self.watchdog is not None:
             self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
         registered = False
+        probe = self.probing()
+        probe.__enter__()
         try:
             if any(zc_grid(c)[0] in ("ipc2z", "ipc2w") for c in cands):
                 registered = self.register_buffer(view)     # collective; False on every rank alike
@@ -173,6 +175,7 @@ class AutotuneMixin:
         finally:
             if registered:
                 self.deregister_buffer(view)
+            probe.__exit__(None, None, None)
             if self.watchdog is not None:
                 self.watchdog.paused -= 1
         tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
@@ -246,13 +249,8 @@ class AutotuneMixin:
         if self.watchdog is not None:
             self.watchdog.paused += 1
         try:
-            for c in cands:
-                if c == "rccl" and not pin_rccl:
-                    self._tuned.pop(key, None)
-                else:
-                    self._tuned[key] = c
-                times.append(self._time_fn(run, uses_ipc=c not in ("rccl", "p2p"), iters=iters,
-                                           name=f"{kind}:{c}", probe=probe))
+            with self.probing():
+                self._autotune_loop(kind, view, cands, run, iters, probe, pin_rccl, key, times)
         finally:
             self._tuned.pop(key, None)
             if self.watchdog is not None:
@@ -265,6 +263,15 @@ class AutotuneMixin:
             self._tuned[key] = best
         self._autosave()
         return res
+
+    def _autotune_loop(self, kind, view, cands, run, iters, probe, pin_rccl, key, times) -> None:
+        for c in cands:
+            if c == "rccl" and not pin_rccl:
+                self._tuned.pop(key, None)
+            else:
+                self._tuned[key] = c
+            times.append(self._time_fn(run, uses_ipc=c not in ("rccl", "p2p"), iters=iters,
+                                       name=f"{kind}:{c}", probe=probe))
 
     # ------------------------------------------------------------------ reduce / broadcast / gather / scatter
     def _root_tuned(self, kind: str, view: torch.Tensor, op) -> Optional[str]:

@@ -35,6 +35,7 @@ remainder in allreduce/reduce splits, rank-order reductions) — see process_com
 """
 from __future__ import annotations
 
+import contextlib
 import datetime
 import logging
 import os
@@ -61,6 +62,7 @@ _RCCL_DTYPES = {torch.float64, torch.float32, torch.bfloat16, torch.float16, tor
 
 
 _IPC_DTYPES = None
+_IPC_OP_OK = None
 
 
 def _ipc_dtypes():
@@ -70,6 +72,15 @@ def _ipc_dtypes():
         from .ipc import SUPPORTED_DTYPES
         _IPC_DTYPES = SUPPORTED_DTYPES
     return _IPC_DTYPES
+
+
+def _ipc_op_ok(dtype, op) -> bool:
+    """``ipc.ipc_op_ok`` without an import statement per call."""
+    global _IPC_OP_OK
+    if _IPC_OP_OK is None:
+        from .ipc import ipc_op_ok
+        _IPC_OP_OK = ipc_op_ok
+    return _IPC_OP_OK(dtype, op)
 
 
 def _env_algo() -> str:
@@ -121,6 +132,8 @@ class DeviceEngine(AutotuneMixin):
     _hier = None
     _hier_failed = False
     hier_min_bytes = 1 << 20
+    _probe_depth = 0
+    _ipc_obj = _ipc_large = _ipc_fp8_big = None
 
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
@@ -339,9 +352,56 @@ class DeviceEngine(AutotuneMixin):
                 self.ipc_selftest = {"ok": False, "failures": bad}
                 return None
             self._ipc_obj = inst
+            self._probe_spin(inst)
         return self._ipc_obj
 
     ipc_selftest: Optional[dict] = None
+
+    # ------------------------------------------------------------------ fail-stop at the call boundary
+    def _ipc_all(self):
+        """Every IPC instance of this engine (None entries skipped)."""
+        h = self._hier
+        return [i for i in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big,
+                            h.ipc if h is not None else None) if i is not None]
+
+    def check_failed(self) -> None:
+        """Raise :class:`Mp4jException` if an IPC collective of this rank gave up waiting for a
+        peer (its spin bound expired: a peer died, diverged or was later than the fail-stop
+        budget).  Reads pinned host words only — no device synchronisation — so it runs at the
+        entry of EVERY device collective, in ``barrier()`` and in ``close()``: a result that
+        followed a timeout is never consumed silently, whether or not the watchdog runs."""
+        for inst in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big):
+            if inst is not None:
+                inst.raise_if_failed()
+        h = self._hier
+        if h is not None and h.ipc is not None:
+            h.ipc.raise_if_failed()
+
+    def _probe_spin(self, inst) -> None:
+        if self._probe_depth and inst is not None:
+            from .ipc import probe_spin
+            inst.set_spin(probe_spin())
+
+    @contextlib.contextmanager
+    def probing(self):
+        """Autotune / probe scope: every IPC instance (also ones created inside) uses the short
+        probe spin bound (``MP4X_IPC_PROBE_SPIN_S``), so a candidate that cannot complete on this
+        topology is ruled out in seconds; the fail-stop bound is restored afterwards."""
+        from .ipc import probe_spin, spin_default
+        self._probe_depth += 1
+        try:
+            if self._probe_depth == 1:
+                for inst in self._ipc_all():
+                    inst.set_spin(probe_spin())
+            yield
+        finally:
+            self._probe_depth -= 1
+            if self._probe_depth == 0:
+                for inst in self._ipc_all():
+                    try:
+                        inst.set_spin(spin_default())
+                    except Exception as e:   # noqa: BLE001 — a dead mesh is reported by the next call
+                        LOG.warning("rank %d: could not restore the IPC spin bound: %s", self.rank, e)
 
     def _ipc_self_test(self, inst) -> Optional[list]:
         """Collective exact-pattern test of every IPC kernel family on the fresh mesh (f32 SUM):
@@ -355,10 +415,9 @@ class DeviceEngine(AutotuneMixin):
         from . import ipc as ipcm
         from ..operators import Operators
         t0 = time.perf_counter()
-        lib = inst.lib
         fails = []
         try:
-            ipcm.check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2"))), "set_spin")
+            inst.set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2")))
         except Exception as e:   # noqa: BLE001
             fails.append(f"set_spin: {e}")
         dev = self.device
@@ -446,7 +505,7 @@ class DeviceEngine(AutotuneMixin):
             except Exception as e:   # noqa: BLE001
                 fails.append(f"zero_copy_twoshot_4MiB: {type(e).__name__}: {e}")
         try:
-            ipcm.check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SPIN_S", "10"))), "set_spin")
+            inst.set_spin(ipcm.spin_default())     # normal operation: the fail-stop budget
         except Exception as e:   # noqa: BLE001
             fails.append(f"set_spin: {e}")
         if os.environ.get("MP4X_IPC_SELFTEST_INJECT", "").strip() == str(r):   # failure-path tests
@@ -484,6 +543,7 @@ class DeviceEngine(AutotuneMixin):
                 from .ipc import IpcAllreduce
                 self._ipc_large = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
                                                tag="large")
+                self._probe_spin(self._ipc_large)
                 if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
                     self._ipc_large.prepare_graph()   # a capture is being prepared: same epoch mode
             except Exception as e:
@@ -518,13 +578,11 @@ class DeviceEngine(AutotuneMixin):
         return op.code == OpCode.SUM or (op.code in (OpCode.MAX, OpCode.MIN) and dtype.is_floating_point)
 
     def _ipc_ok(self, op, dtype, nbytes) -> bool:
-        if not self.ipc_enabled or nbytes % 16 or getattr(op, "is_custom", False):
+        """The IPC kernels reduce (op, dtype): every operator of the reference's table (see
+        ``ipc.ipc_op_ok``), on 16-byte multiples, with IPC enabled."""
+        if not self.ipc_enabled or nbytes % 16 or op is None:
             return False
-        if dtype not in _ipc_dtypes():
-            return False
-        if op.code == OpCode.SUM:
-            return True
-        return op.code in (OpCode.MAX, OpCode.MIN) and dtype in (torch.float32, torch.bfloat16, torch.float16)
+        return _ipc_op_ok(dtype, op)
 
     _SEL_MEMO_MAX = 512
 
@@ -541,7 +599,8 @@ class DeviceEngine(AutotuneMixin):
             return self._select(kind, nbytes, op, dtype, operand)
         key = (kind, nbytes, op, dtype, getattr(operand, "codec", None), getattr(operand, "compress", False),
                self.algo, gen, self.ipc_enabled, self.ipc_oneshot_max, self.ipc_twoshot_max, self._hier_failed,
-               self.backend)
+               self.backend, self.a2a_bytes, self.hier_min_bytes, self._dm_large, self.layout.multi_node,
+               self.device.type)
         try:
             hit = memo.get(key)
         except TypeError:       # an unhashable custom operator: no memo
@@ -580,6 +639,11 @@ class DeviceEngine(AutotuneMixin):
                 self._select_tuned = True
                 return t
         if op is not None and not self.rccl_ok(op, dtype):
+            # RCCL cannot reduce it (bitwise, *_LOC, int16, ...): the IPC kernels run every
+            # operator of the table in one fused kernel per call; a2a only without a mesh
+            if kind in ("allreduce", "reduce") and forced in ("", "auto") and self._ipc_ok(op, dtype, nbytes) \
+                    and self.device.type == "cuda":
+                return "ipc1" if kind == "allreduce" and nbytes <= self.ipc_oneshot_max else "ipc2"
             return "a2a"
         if forced in ("", "auto") and kind == "allreduce" and nbytes >= self.hier_min_bytes and \
                 self._hier_ok(op, dtype, nbytes):
@@ -844,6 +908,7 @@ class DeviceEngine(AutotuneMixin):
                 inst.close()
             from .ipc import IpcAllreduce
             inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8")
+            self._probe_spin(inst)
             if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
                 inst.prepare_graph()
         except Exception as e:   # noqa: BLE001 — setup failures are agreed inside IpcAllreduce
@@ -1158,6 +1223,9 @@ class DeviceEngine(AutotuneMixin):
         t = self._tuned.get(self._rsag_key(kind, whole, op)) if self._tuned else None
         if t is None and self._dm_large_ok(whole) and (op is None or self._ipc_ok(op, whole.dtype, 16)):
             return "ipc"     # no RCCL underneath (see _dm_large_ok): the piecewise IPC kernels
+        if t is None and op is not None and not self.rccl_ok(op, whole.dtype) and whole.is_cuda and \
+                self._ipc_ok(op, whole.dtype, 16):
+            return "ipc"     # an op RCCL cannot reduce: the piecewise IPC reduce-scatter, not a2a
         return t
 
     @staticmethod
@@ -1274,11 +1342,12 @@ class DeviceEngine(AutotuneMixin):
             if peers is not None:
                 self._count("reduce.ipc_zc")
                 self._ipc_obj.allreduce_registered(view, op, peers)
-            else:
+                return arr
+            inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
+            if inst is not None:
                 self._count("reduce.ipc2")
-                inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
                 inst.allreduce(view, op, algo=TWOSHOT)
-            return arr
+                return arr
         if t == "a2a":
             self._count("reduce.a2a")
             froms, tos, _ = CommUtils.even_split(frm, to, self.p)
@@ -1307,7 +1376,16 @@ class DeviceEngine(AutotuneMixin):
             self._count("reduce.ipc2")
             self.ipc_large().allreduce(view, op, algo=TWOSHOT)
             return arr
-        if self.algo != "composite" and self.select("reduce", nbytes, op, view.dtype) == "rccl":
+        sel = self.select("reduce", nbytes, op, view.dtype) if self.algo != "composite" else "a2a"
+        if sel == "ipc2" and not capturing_now() and self.ipc() is not None:
+            # an op RCCL cannot reduce, above the direct tier: the piecewise IPC two-shot
+            inst = self.ipc_large() if nbytes > self.ipc_twoshot_max else self._ipc_obj
+            if inst is not None:
+                from .ipc import TWOSHOT
+                self._count("reduce.ipc2")
+                inst.allreduce(view, op, algo=TWOSHOT)
+                return arr
+        if sel == "rccl":
             self._count("reduce.rccl")
             self.coll.reduce(view, root, op.code)
         else:   # reduce-scatter + gather (reference reduceArray composition, ProcessCommSlave.java:1390-1421)
@@ -1467,9 +1545,13 @@ class DeviceEngine(AutotuneMixin):
 
 
 def _watched(name, fn):
-    """Bracket a device collective for the watchdog (host time inside the call; a HIP event on
-    the stream when the outermost collective returns)."""
+    """Bracket a device collective: first the fail-stop check of the IPC error words (an earlier
+    call that timed out fails this one, :meth:`DeviceEngine.check_failed`), then the watchdog
+    (host time inside the call; a HIP event on the stream when the outermost collective returns)."""
     def wrapper(self, *args, **kwargs):
+        if self._ipc_obj is not None or self._ipc_large is not None or self._ipc_fp8_big is not None or \
+                self._hier is not None:
+            self.check_failed()
         wd = self.watchdog
         if wd is None:
             return fn(self, *args, **kwargs)

@@ -97,6 +97,13 @@ class _GroupServer:
         self._g = global_rank
         self._members = members
 
+    def allgather_both(self, rank, obj):
+        """(the members' values, every rank's values) of one global allgather: the IPC mesh setup
+        agrees failures job-wide, so a node whose mesh fails raises at the same agreement point as
+        every other node and the global calls that follow stay paired."""
+        allv = self._srv.call("allgather_obj", self._g, obj)
+        return [allv[m] for m in self._members], allv
+
     def call(self, method, rank, *args):
         if method == "allgather_obj":
             allv = self._srv.call("allgather_obj", self._g, *args)

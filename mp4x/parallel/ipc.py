@@ -13,7 +13,9 @@ processes sharing one GPU — which is how it is tested on a single-GPU box.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import logging
 import os
 import socket
 from typing import List, Optional
@@ -21,9 +23,10 @@ from typing import List, Optional
 import torch
 
 from ..exceptions import Mp4jException
-from ..operators import OpCode, dtype_of_torch
+from ..operators import DType, OpCode, dtype_of_torch
 from ..ops import native
 from ..ops.native import check, capturing_now, ptr_array, stream_ptr, c_int, c_int64, c_void_p, c_size_t, PP
+from . import occupancy
 
 native.register_signatures({
     "mp4x_ipc_signal_bytes": (c_size_t, []),
@@ -33,7 +36,12 @@ native.register_signatures({
     "mp4x_host_word_alloc": (c_int, [ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
     "mp4x_host_word_free": (c_int, [c_void_p]),
     "mp4x_ipc_set_host_error": (c_int, [c_void_p, c_void_p]),
-    "mp4x_ipc_set_spin": (c_int, [ctypes.c_double]),
+    "mp4x_ipc_set_spin": (c_int, [c_void_p, ctypes.c_double, c_void_p]),
+    "mp4x_ipc_op_supported": (c_int, [c_int, c_int]),
+    "mp4x_ipc_occupancy_ar": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "mp4x_ipc_occupancy_push": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "mp4x_ipc_occupancy_rs": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
+    "mp4x_ipc_occupancy_misc": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int)]),
     "mp4x_mem_range": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t)]),
     "mp4x_dev_alloc": (c_int, [c_size_t, ctypes.POINTER(c_void_p)]),
     "mp4x_ipc_allreduce_push": (c_int, [c_int, c_int, PP, PP, PP, c_int, c_int, c_int64, ctypes.c_uint32, c_int,
@@ -65,9 +73,7 @@ native.register_signatures({
                                    c_void_p, ctypes.c_uint32, c_int, c_void_p, c_void_p]),
 })
 
-# Resident 512-thread blocks per MI355X: 256 CUs x 4 (2048 threads / CU).  Per-block barriers
-# need block b of EVERY rank resident at once, so ranks sharing one GPU split this budget.
-_RESIDENT_BLOCKS = 1024
+LOG = logging.getLogger("mp4x.ipc")
 
 ONESHOT, TWOSHOT = 0, 1
 ZC_TAG = 0x80000000      # epoch tag of the zero-copy protocol (csrc/runtime/ipc.hip kZcTag)
@@ -79,18 +85,63 @@ DATA_COARSE = os.environ.get("MP4X_IPC_DATA_MEM", "uncached").lower() == "coarse
 # (measured: 2.0 GB opens in 0.1 ms, 2 GiB hangs — profiles/r2/ipc_open_probe.jsonl), so
 # registration refuses such allocations (every rank alike): the staged kernels run instead.
 IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
-SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64}
+SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64,
+                    torch.int16, torch.int8, torch.uint8}
+_FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
 
-
-_SPIN_SET = [False]
 _FP8_NARROW = os.environ.get("MP4X_FP8_NARROW") == "1"    # the r1 4-byte-lane fp8 kernel (A/B)
 
 
-def _set_spin(lib) -> None:
-    """Barrier spin bound (``MP4X_IPC_SPIN_S`` seconds, default 10), once per process."""
-    if not _SPIN_SET[0]:
-        check(lib.mp4x_ipc_set_spin(float(os.environ.get("MP4X_IPC_SPIN_S", "10"))), "ipc_set_spin")
-        _SPIN_SET[0] = True
+def ipc_op_ok(dtype, op) -> bool:
+    """Does the IPC tier reduce ``op`` over ``dtype``?  Every operator of the reference's table
+    (Operators.java:29-353) for every primitive dtype, plus 16-bit floats and uint8: SUM / MAX /
+    MIN / PROD everywhere, BITS_AND / OR / XOR on integers, FLOAT_*_LOC on the packed f64 words,
+    INT_*_LOC on the packed i64 words (csrc/runtime/ipc_common.hpp rt_op_ok).  Custom operators
+    (possibly non-commutative host callables) never run here."""
+    if getattr(op, "is_custom", False) or dtype not in SUPPORTED_DTYPES:
+        return False
+    c = op.code
+    if c in (OpCode.SUM, OpCode.MAX, OpCode.MIN, OpCode.PROD):
+        return True
+    if c in (OpCode.BAND, OpCode.BOR, OpCode.BXOR):
+        return dtype not in _FLOAT_DTYPES
+    if c in (OpCode.FMAXLOC, OpCode.FMINLOC):
+        return dtype == torch.float64
+    if c in (OpCode.IMAXLOC, OpCode.IMINLOC):
+        return dtype == torch.int64
+    return False
+
+
+def spin_default() -> float:
+    """Barrier spin bound (seconds) of the IPC kernels in normal operation: ``MP4X_IPC_SPIN_S``,
+    else the collective watchdog's fail-stop budget ``MP4X_WATCHDOG_TIMEOUT`` (600 s, the
+    reference's heartbeat gap, Server.java:82-83).  A collective waits for a straggling peer as
+    long as the job's failure detector would, like the reference's ring step that blocks on
+    ``recvResultQueue.take()`` (ProcessCommSlave.java:1355); only the mesh self-test and the
+    autotune probes use a short bound (:meth:`IpcAllreduce.spin_bound`)."""
+    v = os.environ.get("MP4X_IPC_SPIN_S")
+    if v:
+        return float(v)
+    return float(os.environ.get("MP4X_WATCHDOG_TIMEOUT", 600.0))
+
+
+def probe_spin() -> float:
+    """Spin bound of the autotune probes (``MP4X_IPC_PROBE_SPIN_S``, 10 s): a candidate whose
+    barrier cannot complete on this topology is ruled out in seconds, not after the watchdog."""
+    return float(os.environ.get("MP4X_IPC_PROBE_SPIN_S", 10.0))
+
+
+def _agree(comm, rank, obj, is_bad):
+    """``allgather_obj`` of ``obj`` over the mesh's ranks and whether ``is_bad`` holds for ANY rank
+    of the JOB.  A sub-mesh (parallel/hier.py) answers for the whole job, so a failure on one node
+    makes every node raise at the same agreement point and their control-plane calls stay paired
+    (a node raising alone would pair its next global call with the others' setup)."""
+    both = getattr(comm.server, "allgather_both", None)
+    if both is not None:
+        mine, every = both(rank, obj)
+        return mine, any(is_bad(x) for x in every)
+    allv = comm.server.call("allgather_obj", rank, obj)
+    return allv, any(is_bad(x) for x in allv)
 
 
 class _Reg:
@@ -114,6 +165,8 @@ class IpcAllreduce:
         if not (2 <= self.p <= 8):
             raise Mp4jException("IPC allreduce supports 2..8 ranks")
         self.lib = None
+        self.spin_s = None
+        self.cus = None                  # CUs of this GPU (grid caps), read lazily
         self._data = c_void_p()
         self._sig = c_void_p()
         self._herr = c_void_p()          # pinned host error word (CPU address)
@@ -127,17 +180,16 @@ class IpcAllreduce:
             self.lib = native.hip()
             self.device = torch.cuda.current_device()
             hs = self.lib.mp4x_ipc_handle_size()
-            _set_spin(self.lib)
         except Exception as e:   # noqa: BLE001
             local_err = f"{type(e).__name__}: {e}"
         # IPC handles only open on the same node: a job spanning hosts keeps RCCL (decided from
         # the exchanged host names, identically on every rank, before anything is allocated)
         from .hier import node_id
         nid = comm.node_id() if hasattr(comm, "node_id") else node_id(self.rank)
-        infos = comm.server.call("allgather_obj", self.rank, (nid, local_err))
+        infos, bad = _agree(comm, self.rank, (nid, local_err), lambda x: bool(x[1]))
         errs = [(i, e) for i, (_, e) in enumerate(infos) if e]
-        if errs:
-            raise Mp4jException(f"IPC setup failed on ranks {errs}")
+        if bad:
+            raise Mp4jException(f"IPC setup failed on ranks {errs or 'of another node'}")
         hosts = [h for h, _ in infos]
         if len(set(hosts)) != 1:
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
@@ -169,6 +221,7 @@ class IpcAllreduce:
             herr_dev = c_void_p()
             check(self.lib.mp4x_host_word_alloc(ctypes.byref(self._herr), ctypes.byref(herr_dev)), "host_word_alloc")
             check(self.lib.mp4x_ipc_set_host_error(self._sig, herr_dev), "ipc_set_host_error")
+            self.set_spin(spin_default(), on_current_stream=False)     # nothing queued yet
             hd = ctypes.create_string_buffer(hs)
             hsg = ctypes.create_string_buffer(hs)
             if not self._vmm_data:
@@ -180,17 +233,19 @@ class IpcAllreduce:
         except Exception as e:
             local_err = str(e)
             blob = b"ERR:" + local_err.encode()
-        allh = comm.server.call("allgather_obj", self.rank, blob)
+        allh, bad = _agree(comm, self.rank, blob, lambda b: bytes(b).startswith(b"ERR:"))
         failed = [(i, bytes(b)[4:].decode(errors="replace")) for i, b in enumerate(allh)
                   if bytes(b).startswith(b"ERR:")]
-        if failed:
+        if bad:
             self.close(sync=False)
-            raise Mp4jException(f"IPC buffer setup failed on ranks {failed}")
+            raise Mp4jException(f"IPC buffer setup failed on ranks {failed or 'of another node'}")
         ids = [bytes(b[2 * hs:]) for b in allh]
         share = max(max(ids.count(i) for i in ids), int(getattr(comm, "gpu_share", 1)))
-        # ranks on one device (rehearsal): cap the grid so all ranks' blocks fit at once
-        self.max_blocks = 0 if share == 1 else max(8, _RESIDENT_BLOCKS // (2 * share))
+        # ranks on one device (rehearsal): every launch's grid is capped so all ranks' blocks fit
+        # at once, per kernel instantiation from its occupancy (grid_cap, parallel/occupancy.py)
+        self.share = share
         self.shared_gpu = share > 1
+        self.grid_caps = {}
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
         err = None
@@ -227,11 +282,11 @@ class IpcAllreduce:
                     lst.append(ptr.value)
         except Exception as e:   # decide collectively: every rank enables IPC or none does
             err = str(e)
-        oks = comm.server.call("allgather_obj", self.rank, b"" if err is None else err.encode())
-        if any(oks):
+        oks, anybad = _agree(comm, self.rank, b"" if err is None else err.encode(), bool)
+        if anybad:
             self.close(sync=False)
             bad = [(i, bytes(o).decode()) for i, o in enumerate(oks) if o]
-            raise Mp4jException(f"IPC peer mapping failed on ranks {bad}")
+            raise Mp4jException(f"IPC peer mapping failed on ranks {bad or 'of another node'}")
         self._pp_data = ptr_array(self.data_ptrs)
         self._pp_sig = ptr_array(self.sig_ptrs)
         self.epoch = 0
@@ -280,12 +335,71 @@ class IpcAllreduce:
             raise Mp4jException(f"rank {self.rank}: an earlier IPC collective timed out at its {where} barrier "
                                 f"(a peer skipped, failed or died in that call); its result is invalid")
 
+    def set_spin(self, seconds: float, on_current_stream: bool = True) -> None:
+        """Barrier spin bound of this instance's kernels (stream-ordered on the current stream:
+        kernels queued before keep the previous bound)."""
+        st = stream_ptr() if on_current_stream else None
+        check(self.lib.mp4x_ipc_set_spin(self._sig, float(seconds), st), "ipc_set_spin")
+        self.spin_s = float(seconds)
+
+    @contextlib.contextmanager
+    def spin_bound(self, seconds: float):
+        """A short spin bound while the block runs (self-test, autotune probes), then the previous one."""
+        old = self.spin_s if self.spin_s is not None else spin_default()
+        self.set_spin(seconds)
+        try:
+            yield self
+        finally:
+            self.set_spin(old)
+
+    # ---------------------------------------------------------------- co-residency grid caps
+    _OCC_FAMILY = {"gather": 0, "plan": 1, "fp8": 2, "fp8n": 3}
+
+    def grid_cap(self, family: str, dtype=None, op=None) -> int:
+        """Largest grid a launch of ``family`` ((dtype, op) kernel; see parallel/occupancy.py)
+        may use: 256 with a GPU of its own; on a GPU shared by ``share`` ranks, the budget derived
+        from the kernel instantiation's occupancy (API and compiler resources, the smaller) so
+        every rank's blocks are resident at once.  Rank-independent (every rank of a shared GPU
+        computes the same value), memoised and logged once per kernel."""
+        if not self.shared_gpu:
+            return occupancy.MAX_BLOCKS
+        code = int(op.code) if op is not None else 0
+        key = (family, dtype, code)
+        cap = self.grid_caps.get(key)
+        if cap is not None:
+            return cap
+        dt = int(dtype_of_torch(dtype)) if dtype is not None else int(DType.F32)
+        n = ctypes.c_int(0)
+        try:
+            if family in ("oneshot", "twoshot"):
+                rc = self.lib.mp4x_ipc_occupancy_ar(0 if family == "oneshot" else 1, dt, code, self.p, ctypes.byref(n))
+            elif family == "push":
+                rc = self.lib.mp4x_ipc_occupancy_push(dt, code, self.p, ctypes.byref(n))
+            elif family == "rs":
+                rc = self.lib.mp4x_ipc_occupancy_rs(dt, code, self.p, ctypes.byref(n))
+            else:
+                rc = self.lib.mp4x_ipc_occupancy_misc(self._OCC_FAMILY[family], dt, self.p, ctypes.byref(n))
+            api = n.value if rc == 0 else 0
+        except Exception:   # noqa: BLE001 — the compiler table still bounds it
+            api = 0
+        if self.cus is None:
+            self.cus = int(torch.cuda.get_device_properties(self.device).multi_processor_count)
+        tbl = occupancy.table_bpc(family, dt, DType(dt).name, code, self.p)
+        known = [x for x in (api, tbl) if x]
+        bpc = min(known) if known else 1
+        cap = occupancy.shared_grid_cap(self.cus, bpc, self.share)
+        self.grid_caps[key] = cap
+        LOG.info("rank %d: grid cap %s %s op=%d p=%d share=%d: %d blocks (blocks/CU: api %s, compiler %s)",
+                 self.rank, family, DType(dt).name, code, self.p, self.share, cap, api, tbl)
+        return cap
+
+    def grid_caps_summary(self) -> dict:
+        """The caps computed so far, JSON-able (rehearsal / bench records)."""
+        return {f"{f}:{str(d).replace('torch.', '') if d is not None else '-'}:{c}": v
+                for (f, d, c), v in sorted(self.grid_caps.items(), key=str)}
+
     def supports(self, t: torch.Tensor, op) -> bool:
-        if getattr(op, "is_custom", False) or t.dtype not in SUPPORTED_DTYPES:
-            return False
-        if op.code == OpCode.SUM:
-            return True
-        return op.code in (OpCode.MAX, OpCode.MIN) and t.dtype in (torch.float32, torch.bfloat16, torch.float16)
+        return ipc_op_ok(t.dtype, op)
 
     def allreduce(self, view: torch.Tensor, op, algo: int = ONESHOT, out: Optional[torch.Tensor] = None,
                   blocks: int = 0, overlap: Optional[bool] = None, scale: float = 1.0) -> torch.Tensor:
@@ -312,9 +426,10 @@ class IpcAllreduce:
             out.copy_(tmp)
             return out
         dt = int(dtype_of_torch(view.dtype))
-        if not blocks and self.max_blocks:
+        if not blocks and self.shared_gpu:
             vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
-            blocks = max(1, min(self.max_blocks, -(-min(total, self.nbytes) // 16 // vec_per_block)))
+            cap = self.grid_cap("oneshot" if algo == ONESHOT else "twoshot", view.dtype, op)
+            blocks = max(1, min(cap, -(-min(total, self.nbytes) // 16 // vec_per_block)))
         if overlap is None:
             overlap = self._overlap_default
         capturing = capturing_now()
@@ -468,6 +583,10 @@ class IpcAllreduce:
         if any(oks):
             self._release(reg)
             return False
+        old = self._regs.get(key)
+        if old is not None:
+            # registered on this rank already but not on every rank: the new entry replaces it
+            self._release(old)
         self._regs[key] = reg
         return True
 
@@ -697,7 +816,7 @@ class IpcAllreduce:
         else:
             self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
         chunk = -(-(total // 16) // self.p)
-        blocks = max(1, min(self.max_blocks, -(-chunk // 512))) if self.max_blocks else 0
+        blocks = max(1, min(self.grid_cap("push", dtype, op), -(-chunk // 512))) if self.shared_gpu else 0
         pp = ptr_array(peers)
         sp = ptr_array(scratch)
         check(self.lib.mp4x_ipc_allreduce_push(int(dtype_of_torch(dtype)), int(op.code), pp[0], sp[0],
@@ -803,9 +922,9 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
             self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
-        blocks = self._grid(total // 16)               # >= 8: every XCD passes the barriers
+        blocks = self._grid(total // 16, "twoshot", dtype, op)   # >= 8: every XCD passes the barriers
         if grid > 0:
-            blocks = min(grid, self.max_blocks) if self.max_blocks else grid
+            blocks = min(grid, self.grid_cap("twoshot", dtype, op))
         pp = ptr_array(peers)
         check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
                                              self._pp_sig[0], self.rank, self.p, total, None, dst,
@@ -851,7 +970,7 @@ class IpcAllreduce:
         maxv = max(h - l_ for l_, h in zip(lo, hi))
         check(self.lib.mp4x_ipc_reduce_scatter(int(dtype_of_torch(flat.dtype)), int(op.code), pp[0], self._pp_sig[0],
                                                r, self.p, lo[r], hi[r], rng.data_ptr() + lo[r] * 16,
-                                               self.epoch | ZC_TAG, self._grid(maxv), edev, st),
+                                               self.epoch | ZC_TAG, self._grid(maxv, "rs", flat.dtype, op), edev, st),
               "mp4x_ipc_reduce_scatter(zero-copy)")
         return True
 
@@ -868,7 +987,7 @@ class IpcAllreduce:
         hi_a = (c_int64 * self.p)(*hi)
         maxv = max(h - l_ for l_, h in zip(lo, hi))
         check(self.lib.mp4x_ipc_allgather(pp[0], self._pp_sig[0], self.rank, self.p, lo_a, hi_a, rng.data_ptr(),
-                                          self.epoch | ZC_TAG, self._grid(maxv), edev, st),
+                                          self.epoch | ZC_TAG, self._grid(maxv, "gather"), edev, st),
               "mp4x_ipc_allgather(zero-copy)")
         return True
 
@@ -887,7 +1006,7 @@ class IpcAllreduce:
         pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
         check(self.lib.mp4x_ipc_copy_plan(pp[0], self._pp_sig[0], self.rank, self.p, sa, 0, pa, len(pull), None,
                                           out_ptr if pull else None, grid_len, buf_vecs, self.epoch | ZC_TAG,
-                                          self._grid(grid_len), edev, st), "mp4x_ipc_copy_plan(zero-copy)")
+                                          self._grid(grid_len, "plan"), edev, st), "mp4x_ipc_copy_plan(zero-copy)")
 
     def gather_registered(self, flat: torch.Tensor, froms, tos, root: int) -> bool:
         """Root pulls every rank's ``[froms[j], tos[j])`` straight from the peers' registered
@@ -937,12 +1056,7 @@ class IpcAllreduce:
         self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
         return None
 
-    def _blocks_for(self, nvec: int) -> int:
-        if not self.max_blocks:
-            return 0
-        return max(1, min(self.max_blocks, -(-nvec // 512)))
-
-    def _grid(self, nvec: int) -> int:
+    def _grid(self, nvec: int, family: str = "plan", dtype=None, op=None) -> int:
         """Explicit grid for a per-block-barrier kernel.  ``nvec`` must be RANK-INDEPENDENT (the
         largest segment of any rank): block b of every rank has to exist to meet block b of the
         peers, so ragged segments may not size the grid per rank.
@@ -950,8 +1064,8 @@ class IpcAllreduce:
         At least 8 blocks: workgroups are dealt round-robin over the 8 XCDs, so every XCD runs
         the barriers' system-scope release / acquire (each XCD has its own L2) even when the
         data would fit fewer blocks — the zero-copy forms read and write the peers' cached
-        tensors."""
-        cap = self.max_blocks or 256                   # kIpcMaxBlocks
+        tensors.  On a shared GPU the cap of the launched kernel applies (:meth:`grid_cap`)."""
+        cap = self.grid_cap(family, dtype, op)
         return max(min(8, cap), min(cap, -(-nvec // 512)))
 
     def reduce_scatter(self, view: torch.Tensor, froms, tos, op) -> bool:
@@ -982,7 +1096,8 @@ class IpcAllreduce:
             maxv = max(h - l_ for l_, h in zip(lo_a, hi_a))
             check(self.lib.mp4x_ipc_reduce_scatter_from(int(dtype_of_torch(view.dtype)), int(op.code),
                                                         self._pp_data[0], self._pp_sig[0], r, self.p, lo_a, hi_a,
-                                                        b16, b16 + mine_off, self.epoch, self._grid(maxv), edev, st),
+                                                        b16, b16 + mine_off, self.epoch,
+                                                        self._grid(maxv, "rs", view.dtype, op), edev, st),
                   "mp4x_ipc_reduce_scatter_from")
             if tmp is not None and tos[r] > froms[r]:
                 flat[froms[r]:tos[r]].view(torch.uint8).copy_(tmp[mine_off:(tos[r] - base) * es])
@@ -995,7 +1110,7 @@ class IpcAllreduce:
         maxv = max((t - f) * es // 16 for f, t in zip(froms, tos))
         check(self.lib.mp4x_ipc_reduce_scatter(int(dtype_of_torch(view.dtype)), int(op.code), self._pp_data[0],
                                                self._pp_sig[0], r, self.p, lo, hi, mine, self.epoch,
-                                               self._grid(maxv), edev, st), "mp4x_ipc_reduce_scatter")
+                                               self._grid(maxv, "rs", view.dtype, op), edev, st), "mp4x_ipc_reduce_scatter")
         if hi > lo:
             check(self.lib.mp4x_memcpy_async(flat[froms[r]:].data_ptr(), mine, (hi - lo) * 16, st), "ipc RS out")
         return True
@@ -1040,7 +1155,7 @@ class IpcAllreduce:
         maxlen = max(h - l_ for l_, h in zip(lo, hi))
         # peers' segments land in the OWN buffer (only the own segment is read remotely), then one copy out
         check(self.lib.mp4x_ipc_allgather(self._pp_data[0], self._pp_sig[0], r, self.p, lo, hi, self._data.value,
-                                          self.epoch, self._grid(maxlen), edev, st), "mp4x_ipc_allgather")
+                                          self.epoch, self._grid(maxlen, "gather"), edev, st), "mp4x_ipc_allgather")
         n = (tos[-1] - base) * es
         if n:
             check(self.lib.mp4x_memcpy_async(flat[base:].data_ptr(), self._data.value, n, st), "ipc AG out")
@@ -1248,7 +1363,8 @@ class IpcAllreduce:
             lo = r * sv
             hi = lo + lens[r] * es // 16
             check(self.lib.mp4x_ipc_reduce_scatter(dt, int(op.code), self._pp_data[0], self._pp_sig[0], r, p, lo, hi,
-                                                   buf + lo * 16, self.epoch, self._grid(max(lens) * es // 16), edev,
+                                                   buf + lo * 16, self.epoch,
+                                                   self._grid(max(lens) * es // 16, "rs", view.dtype, op), edev,
                                                    st), "mp4x_ipc_reduce_scatter")
             if lens[r]:
                 check(self.lib.mp4x_memcpy_async(flat[froms[r] + i * s:].data_ptr(), buf + lo * 16, lens[r] * es, st),
@@ -1277,7 +1393,8 @@ class IpcAllreduce:
             lo = (c_int64 * p)(*[j * sv for j in range(p)])
             hi = (c_int64 * p)(*[j * sv + lens[j] * es // 16 for j in range(p)])
             check(self.lib.mp4x_ipc_allgather(self._pp_data[0], self._pp_sig[0], r, p, lo, hi, buf, self.epoch,
-                                              self._grid(max(lens) * es // 16), edev, st), "mp4x_ipc_allgather")
+                                              self._grid(max(lens) * es // 16, "gather"), edev, st),
+                  "mp4x_ipc_allgather")
             for j in range(p):
                 if j != r and lens[j]:
                     check(self.lib.mp4x_memcpy_async(flat[froms[j] + i * s:].data_ptr(), buf + j * s * es,
@@ -1338,22 +1455,19 @@ class IpcAllreduce:
             check(self.lib.mp4x_quant_fp8(dt, base + off * es, m, own, own + soff, st), "fp8 quant")
             edev = self._next_epoch(st)
             check(self.lib.mp4x_ipc_fp8_allreduce(dt, self._pp_data[0], self._pp_sig[0], self.rank, self.p, cb, soff,
-                                                  base + off * es, m, self.epoch, self._blocks_for_waves(cb if _FP8_NARROW else -(-cb // 4)), edev,
-                                                  scale, st), "mp4x_ipc_fp8_allreduce")
+                                                  base + off * es, m, self.epoch,
+                                                  self._blocks_for_waves(cb if _FP8_NARROW else -(-cb // 4), view.dtype),
+                                                  edev, scale, st), "mp4x_ipc_fp8_allreduce")
             off += m
         return view
 
-    def _blocks_for_waves(self, waves: int) -> int:
-        """Grid of the fused fp8 two-shot.  On a GPU shared by the ranks (rehearsals) every rank's
-        blocks must be resident at once for the per-block barriers; this kernel (512 threads, a
-        40 KB LDS tile and a heavy register load per block) fits about half as many blocks per
-        CU as the generic budget assumes, so it takes half the shared grid
-        (``MP4X_FP8_BLOCK_DIV``, default 2): with the full budget, 8 ranks stalled at the start
-        barrier; with half, config 5 at 8 ranks runs exact (profiles/r3/configs_s2/)."""
-        if not self.max_blocks:
+    def _blocks_for_waves(self, waves: int, dtype) -> int:
+        """Grid of the fused fp8 two-shot (8 waves per block).  On a GPU shared by the ranks
+        (rehearsals) the cap of this kernel's occupancy applies (:meth:`grid_cap`; its 40 KB LDS
+        tile and register load fit fewer blocks per CU than the generic kernels)."""
+        if not self.shared_gpu:
             return 0
-        cap = max(1, self.max_blocks // max(1, int(os.environ.get("MP4X_FP8_BLOCK_DIV", "2"))))
-        return max(1, min(cap, -(-waves // 8)))
+        return max(1, min(self.grid_cap("fp8n" if _FP8_NARROW else "fp8", dtype), -(-waves // 8)))
 
     def prepare_graph(self):
         """Move the epoch counter to device memory so hipGraph replays get fresh epochs.
@@ -1374,6 +1488,10 @@ class IpcAllreduce:
         v = ctypes.c_uint32(0)
         check(self.lib.mp4x_ipc_error_word(self._sig, ctypes.byref(v), int(bool(clear)),
                                            stream_ptr(self._sig_stream)), "ipc_error_word")
+        if clear and self._herr:
+            # the pinned host copy too: a probe timeout that was read and handled here (autotune)
+            # must not fail the next call at its entry check
+            ctypes.c_uint32.from_address(self._herr.value).value = 0
         return int(v.value)
 
     def close(self, sync: bool = True):

@@ -173,9 +173,28 @@ class ProcessCommSlave:
                 return
 
     def close(self, code: int = 0) -> None:
-        """Reference ProcessCommSlave.close (:234-271)."""
+        """Reference ProcessCommSlave.close (:234-271).
+
+        A clean close (code 0) first drains this rank's device work and checks the IPC error
+        words: if a device collective gave up waiting for a peer, its result was invalid, so the
+        close reports it (master error log), closes with code 1 (the job fails, as the reference's
+        ``exception()`` -> ``close(1)``) and raises :class:`Mp4jException` afterwards."""
         if self.closed:
             return
+        failure = None
+        eng = self._device_engine
+        if not code and eng is not None:
+            try:
+                if eng.device.type == "cuda":
+                    import torch
+                    torch.cuda.synchronize(eng.device)
+                eng.check_failed()
+            except Mp4jException as e:
+                failure, code = e, 1
+                try:
+                    self.error(f"close: {e}")
+                except Exception:   # noqa: BLE001 — the master may be gone; the code still says it
+                    pass
         LOG.info("close code=%s", code)
         try:
             self.server.call("close", self.rank, int(code))
@@ -202,6 +221,8 @@ class ProcessCommSlave:
             self.server.close()
             if self._hb_client is not None:
                 self._hb_client.close()
+        if failure is not None:
+            raise failure
 
     def exception(self, e: BaseException) -> None:
         """Report the stack to the master, wait, then ``close(1)`` (reference :360-373)."""
@@ -237,9 +258,14 @@ class ProcessCommSlave:
         return self.rank
 
     def barrier(self) -> None:
-        """Master barrier (reference :432-438); device work queued before it is NOT waited for."""
+        """Master barrier (reference :432-438); device work queued before it is NOT waited for.
+        Raises if an IPC collective of this rank already timed out (``DeviceEngine.check_failed``,
+        pinned host words, no device sync) — after joining the barrier, so the peers are not
+        left waiting in it."""
         self._tick("barrier")
         self.server.call("barrier", self.rank)
+        if self._device_engine is not None:
+            self._device_engine.check_failed()
 
     def peer_barrier(self) -> None:
         """O(log p) barrier over the data plane (no master round trip)."""

@@ -1,0 +1,233 @@
+"""CPU unit tests of the IPC tier's policies (no GPU): the operator matrix it serves and the
+selection that follows from it, the co-residency grid-cap arithmetic, the spin-bound defaults,
+and the fail-stop checks at the call boundary."""
+import os
+
+import pytest
+import torch
+
+from mp4x import Operands, Operators
+from mp4x.exceptions import Mp4jException
+from mp4x.operators import OpCode
+from mp4x.parallel import ipc as ipc_mod
+from mp4x.parallel import occupancy as occ
+from mp4x.parallel.device_engine import DeviceEngine, _TunedTable
+
+ALL = {
+    "Double": (torch.float64, ("SUM", "MAX", "MIN", "PROD", "FLOAT_MAX_LOC", "FLOAT_MIN_LOC")),
+    "Float": (torch.float32, ("SUM", "MAX", "MIN", "PROD")),
+    "Long": (torch.int64, ("SUM", "MAX", "MIN", "BITS_AND", "BITS_OR", "BITS_XOR", "PROD", "INT_MAX_LOC",
+                           "INT_MIN_LOC")),
+    "Int": (torch.int32, ("SUM", "MAX", "MIN", "BITS_AND", "BITS_OR", "BITS_XOR", "PROD")),
+    "Short": (torch.int16, ("SUM", "MAX", "MIN", "BITS_AND", "BITS_OR", "BITS_XOR", "PROD")),
+    "Byte": (torch.int8, ("SUM", "MAX", "MIN", "BITS_AND", "BITS_OR", "BITS_XOR", "PROD")),
+    "BFloat16": (torch.bfloat16, ("SUM", "MAX", "MIN", "PROD")),
+    "Half": (torch.float16, ("SUM", "MAX", "MIN", "PROD")),
+}
+
+
+def test_ipc_serves_the_whole_operator_table():
+    for cls, (dt, ops) in ALL.items():
+        for name in ops:
+            assert ipc_mod.ipc_op_ok(dt, getattr(getattr(Operators, cls), name)), (cls, name)
+    from mp4x.operators import CustomOperator, lookup, DType
+    assert not ipc_mod.ipc_op_ok(torch.float32, CustomOperator(lambda a, b: a + b))
+    assert not ipc_mod.ipc_op_ok(torch.float32, lookup(DType.F32, OpCode.BAND))      # no bitwise on floats
+    assert not ipc_mod.ipc_op_ok(torch.int32, lookup(DType.I32, OpCode.IMAXLOC))     # *_LOC: packed words only
+
+
+def _engine(backend="nccl"):
+    e = object.__new__(DeviceEngine)
+    e.backend, e.device, e.ipc_enabled, e._zc = backend, torch.device("cuda", 0), True, True
+    e.ipc_twoshot_max, e.ipc_oneshot_max, e.algo, e.a2a_bytes, e.p = 16 << 20, 256 << 10, "auto", 0, 8
+    e._tuned, e._sel_memo, e._select_tuned = _TunedTable(), {}, False
+    return e
+
+
+def test_select_never_returns_a2a_for_a_builtin_op_with_a_mesh():
+    """SURVEY C20 on the xGMI tier: every built-in op at p <= 8 selects an IPC kernel (one kernel
+    per call) at every size; a2a only without a mesh or for custom operators."""
+    e = _engine()
+    opnd = Operands.DOUBLE_OPERAND()
+    for cls, (dt, ops) in ALL.items():
+        for name in ops:
+            op = getattr(getattr(Operators, cls), name)
+            for nb in (4096, 1 << 20, 64 << 20, 1 << 30):
+                for kind in ("allreduce", "reduce"):
+                    a = e.select(kind, nb, op, dt, opnd)
+                    assert a != "a2a", (cls, name, nb, kind)
+                    if not e.rccl_ok(op, dt):
+                        want = "ipc1" if kind == "allreduce" and nb <= e.ipc_oneshot_max else "ipc2"
+                        assert a == want, (cls, name, nb, kind, a)
+    e.ipc_enabled = False
+    assert e.select("allreduce", 4096, Operators.Long.BITS_OR, torch.int64, opnd) == "a2a"
+    e.ipc_enabled = True
+    from mp4x.operators import CustomOperator
+    assert e.select("allreduce", 4096, CustomOperator(lambda a, b: a), torch.float32, opnd) == "a2a"
+
+
+def test_select_memo_key_covers_every_tier_input():
+    """a2a_bytes, hier_min_bytes, the large-data mode, the layout and the device type
+    all feed _select; changing any of them must not return a stale memoised decision."""
+    e = _engine()
+    e.ipc_enabled = False
+    opnd = Operands.FLOAT_OPERAND()
+    sel = lambda: e.select("allreduce", 1 << 20, Operators.Float.SUM, torch.float32, opnd)   # noqa: E731
+    assert sel() == "rccl"
+    e.a2a_bytes = 1 << 10
+    assert sel() == "a2a"
+
+
+def test_large_reduce_scatter_of_a_non_rccl_op_takes_the_ipc_pieces():
+    e = _engine()
+    e._dm_large = "auto"
+
+    class _Whole:                 # a 64 MiB int64 device range (shape facts only)
+        dtype, is_cuda = torch.int64, True
+
+        def numel(self):
+            return (64 << 20) // 8
+
+        def element_size(self):
+            return 8
+    whole = _Whole()
+    e._dm_large_ok = lambda flat: False
+    assert e._large_choice("reduce_scatter", whole, Operators.Long.BITS_XOR) == "ipc"
+    assert e._large_choice("reduce_scatter", whole, Operators.Long.SUM) is None       # RCCL reduces it
+
+
+def test_blocks_per_cu_follows_the_cdna4_residency_rules():
+    # light kernel: waves bound by the 8-wave SIMD limit -> 4 blocks of 512 threads per CU
+    assert occ.blocks_per_cu({"sgpr": 40, "vgpr": 48, "agpr": 0, "lds": 4, "occ": 8}) == 4
+    # 128 VGPRs -> 4 waves/SIMD -> 2 blocks;  121 rounds up to 128 as well
+    assert occ.blocks_per_cu({"sgpr": 40, "vgpr": 121, "lds": 4, "occ": 4}) == 2
+    # 174 VGPRs -> 176 -> 2 waves/SIMD -> 1 block
+    assert occ.blocks_per_cu({"sgpr": 46, "vgpr": 174, "lds": 4, "occ": 2}) == 1
+    # SGPR-bound: 106 SGPRs -> 128 per wave -> 6 waves/SIMD (the compiler says 7) -> 3 blocks
+    assert occ.blocks_per_cu({"sgpr": 106, "vgpr": 42, "lds": 4, "occ": 7}) == 3
+    # LDS-bound: a 40 KB tile fits 4 blocks, 60 KB fits 2
+    assert occ.blocks_per_cu({"sgpr": 40, "vgpr": 32, "lds": 60 * 1024, "occ": 8}) == 2
+
+
+def test_shared_grid_cap_halves_the_resident_budget():
+    assert occ.shared_grid_cap(256, 4, 1) == 256              # a GPU of its own: no cap
+    assert occ.shared_grid_cap(256, 4, 8) == 64               # 256 * 2 / 8 (the r1-r3 generic budget)
+    assert occ.shared_grid_cap(256, 2, 8) == 32               # the fp8 two-shot at 8 ranks (config 5)
+    assert occ.shared_grid_cap(256, 1, 8) == 32               # at least one block per CU of budget
+    assert occ.shared_grid_cap(256, 4, 2) == 256
+    assert occ.shared_grid_cap(4, 1, 8) == 1                  # never 0
+
+
+def test_kernel_op_mirrors_the_native_dispatch():
+    assert occ.kernel_op("F32", 0) == 0 and occ.kernel_op("BF16", 1) == 1 and occ.kernel_op("F16", 2) == 2
+    assert occ.kernel_op("F64", 1) == -1 and occ.kernel_op("I16", 0) == -1 and occ.kernel_op("I64", 3) == -1
+
+
+def test_resource_table_parses_when_built():
+    path = occ._table_path()
+    if not os.path.exists(path):
+        pytest.skip("native library not built")
+    t = occ.load_table()
+    assert t, "empty resource table"
+    # every family is present, and the exact instantiation of a hot and a runtime-op kernel resolve
+    fams = {k for k, _ in t}
+    assert {"k_ipc_oneshot", "k_ipc_twoshot", "k_ipc_twoshot_push", "k_ipc_reduce_range", "k_ipc_gather",
+            "k_ipc_copy_plan", "k_ipc_fp8_twoshot"} <= fams
+    assert occ.table_bpc("twoshot", 1, "F32", 0, 8) >= 1
+    assert occ.table_bpc("rs", 5, "I8", 4, 8) >= 1
+    assert occ.table_bpc("fp8", 1, "F32", 0, 8) >= 1
+
+
+def test_parse_resource_remarks():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bn", os.path.join(os.path.dirname(__file__), "..", "tools",
+                                                                      "build_native.py"))
+    bn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bn)
+    text = """x.hip:2:1: remark: Function Name: _Z2kkILi2EEvPf [-Rpass-analysis=kernel-resource-usage]
+x.hip:2:1: remark:     TotalSGPRs: 8 [-Rpass-analysis=kernel-resource-usage]
+x.hip:2:1: remark:     VGPRs: 4 [-Rpass-analysis=kernel-resource-usage]
+x.hip:2:1: remark:     AGPRs: 0 [-Rpass-analysis=kernel-resource-usage]
+x.hip:2:1: remark:     Occupancy [waves/SIMD]: 8 [-Rpass-analysis=kernel-resource-usage]
+x.hip:2:1: remark:     LDS Size [bytes/block]: 512 [-Rpass-analysis=kernel-resource-usage]
+"""
+    assert bn.parse_resource_remarks(text) == {"_Z2kkILi2EEvPf": {"sgpr": 8, "vgpr": 4, "agpr": 0, "occ": 8,
+                                                                  "lds": 512}}
+
+
+def test_spin_bound_defaults_to_the_fail_stop_budget(monkeypatch):
+    monkeypatch.delenv("MP4X_IPC_SPIN_S", raising=False)
+    monkeypatch.delenv("MP4X_WATCHDOG_TIMEOUT", raising=False)
+    assert ipc_mod.spin_default() == 600.0
+    monkeypatch.setenv("MP4X_WATCHDOG_TIMEOUT", "900")
+    assert ipc_mod.spin_default() == 900.0
+    monkeypatch.setenv("MP4X_IPC_SPIN_S", "1")
+    assert ipc_mod.spin_default() == 1.0
+    assert ipc_mod.probe_spin() == 10.0
+
+
+class _Inst:
+    def __init__(self):
+        self.word = 0
+        self.spins = []
+
+    def raise_if_failed(self):
+        if self.word:
+            self.word = 0
+            raise Mp4jException("an earlier IPC collective timed out")
+
+    def set_spin(self, s):
+        self.spins.append(s)
+
+
+def test_every_device_collective_checks_the_error_words_at_entry():
+    e = _engine()
+    e.watchdog = None
+    e._ipc_large = e._ipc_fp8_big = e._hier = None
+    e._ipc_obj = _Inst()
+    e.stats = {}
+    e.coll = type("C", (), {"barrier": lambda self: None})()
+    e.barrier()                                   # clean: passes
+    e._ipc_obj.word = 2                           # a mid barrier of an earlier call timed out
+    with pytest.raises(Mp4jException, match="timed out"):
+        e.barrier()
+    e._ipc_obj.word = 1
+    with pytest.raises(Mp4jException):
+        e.allreduce(torch.zeros(4), 0, 4, Operators.Float.SUM)
+
+
+def test_probing_scope_uses_the_short_bound_and_restores(monkeypatch):
+    monkeypatch.delenv("MP4X_IPC_SPIN_S", raising=False)
+    monkeypatch.delenv("MP4X_WATCHDOG_TIMEOUT", raising=False)
+    e = _engine()
+    e._ipc_obj, e._ipc_large, e._ipc_fp8_big, e._hier = _Inst(), None, None, None
+    with e.probing():
+        with e.probing():                         # nested tuners: set once, restored once
+            late = _Inst()
+            e._probe_spin(late)                   # an instance created inside the scope
+        assert e._ipc_obj.spins == [10.0]
+    assert e._ipc_obj.spins == [10.0, 600.0] and late.spins == [10.0]
+
+
+def test_process_barrier_and_close_surface_a_timed_out_collective():
+    from mp4x import CommMaster, ProcessCommSlave
+    import tempfile
+    m = CommMaster(1, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
+    try:
+        comm = ProcessCommSlave("t", "127.0.0.1", m.port, heartbeat=False)
+        eng = _engine()
+        eng.device = torch.device("cpu")
+        eng._ipc_obj, eng._ipc_large, eng._ipc_fp8_big, eng._hier = _Inst(), None, None, None
+        eng.shutdown = eng.abort = lambda: None
+        comm._device_engine = eng
+        comm.barrier()
+        eng._ipc_obj.word = 3
+        with pytest.raises(Mp4jException):
+            comm.barrier()
+        eng._ipc_obj.word = 3
+        with pytest.raises(Mp4jException):
+            comm.close(0)                         # reported, closed with code 1, then raised
+        assert comm.closed
+    finally:
+        code = m.stop(timeout=5)
+    assert code == 1

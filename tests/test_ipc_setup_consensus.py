@@ -75,7 +75,8 @@ class _FakeLib:
         self.freed.append(ptr)
         return 0
 
-    def mp4x_ipc_set_spin(self, s):
+    def mp4x_ipc_set_spin(self, sig, seconds, stream):
+        self.spin = seconds
         return 0
 
     def mp4x_host_word_alloc(self, hptr, dptr):
@@ -257,3 +258,37 @@ def test_registration_lifecycle_pools_scratch_and_keeps_mappings(monkeypatch):
     for *_, inst in res:
         inst.close(sync=False)
     assert lib.closes >= opens                      # every mapping closed at close()
+
+
+def test_hier_submesh_failure_on_one_node_is_agreed_job_wide(monkeypatch):
+    """the per-node IPC meshes of the node-aware allreduce are built over
+    GLOBAL control-plane calls.  When one node's setup fails, every node must raise at the same
+    agreement point, so the global calls that follow stay paired (a node raising alone would pair
+    its next global call with the other nodes' setup calls)."""
+    from mp4x.parallel.hier import _GroupComm
+    p = 4
+    nodes = [[0, 1], [2, 3]]
+    tls = threading.local()
+    lib = _FakeLib(lambda: tls.rank == 2)          # rank 2's buffer allocation fails (node 1)
+    monkeypatch.setattr(ipc_mod.native, "hip", lambda: lib)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
+    server = _Server(p)
+    errors, after = [None] * p, [None] * p
+
+    def run(r):
+        tls.rank = r
+        try:
+            ipc_mod.IpcAllreduce(_GroupComm(_Comm(server, r), nodes[r // 2], 1), nbytes=1 << 16)
+        except Mp4jException as e:
+            errors[r] = str(e)
+        after[r] = server.call("allgather_obj", r, ("after", r))     # the next global call
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(p)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(20)
+    assert not any(t.is_alive() for t in threads), "a rank is stuck waiting for its peers"
+    assert all(e is not None for e in errors), errors
+    assert "another node" in errors[0] and "(0," in errors[2], errors     # node-local rank 0 of node 1
+    assert all(a == [("after", j) for j in range(p)] for a in after), after

@@ -1,0 +1,122 @@
+"""A rank that arrives late is waited for, not failed (p processes sharing one GPU).
+
+The reference's collectives block until their peers arrive (the ring step's
+``recvResultQueue.take()`` has no timeout, ProcessCommSlave.java:1355; liveness is judged on a
+600 s heartbeat gap, Server.java:82-83).  The IPC kernels' barrier spin bound defaults to the same
+fail-stop budget (``MP4X_WATCHDOG_TIMEOUT``, 600 s), so a rank that is 15 s late — a checkpoint
+save, an eval pass, a data-loader stall; beyond the 10 s bound of rounds 1-3 — still gets exact
+results on every kernel family, and no error word is set.  ``MP4X_TEST_STRAGGLE_S`` overrides the
+delay.  The never-arriving rank (short explicit bound) keeps failing fast: test_ipc_zc_gpu.py.
+"""
+import os
+import time
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from spawn_ranks import run_spawn  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+DELAY = float(os.environ.get("MP4X_TEST_STRAGGLE_S", "15"))
+
+
+def _progress(msg):
+    path = os.environ.get("MP4X_TEST_PROGRESS")
+    if path:
+        with open(path, "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+
+
+def _pat(n, r, m=13):
+    return (torch.arange(n, device="cuda", dtype=torch.int32) % m + r).float()
+
+
+def _sum(n, p, m=13):
+    i = torch.arange(n, device="cuda", dtype=torch.int32) % m
+    return (i * p + p * (p - 1) // 2).float()
+
+
+def _straggler_fn(comm, delay):
+    from mp4x import CommUtils, Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    inst = eng.ipc()
+    F, SUM = Operands.FLOAT_OPERAND(), Operators.Float.SUM
+    spin = inst.spin_s
+
+    def late():
+        comm.barrier()                     # everyone leaves together, then rank 1 dawdles
+        if r == 1:
+            time.sleep(delay)
+
+    res = {}
+
+    def check(name, ok, key):
+        torch.cuda.synchronize()
+        res[name] = (bool(ok), eng.stats.get(key, 0))
+        if r == 0:
+            _progress(f"p={p} {name} ok={bool(ok)}")
+
+    # staged one-shot / two-shot
+    for algo, n in (("ipc1", 16 << 10), ("ipc2", 1 << 20)):
+        eng.algo = algo
+        x = _pat(n, r)
+        late()
+        comm.allreduceArray(x, F, SUM, 0, n)
+        check(algo, torch.equal(x, _sum(n, p)), f"allreduce.{algo}")
+    # zero-copy pull / push on a registered tensor
+    n = 2 << 20
+    buf = torch.empty(n, device="cuda")
+    assert comm.registerBuffer(buf)
+    for algo in ("ipc2z", "ipc2w"):
+        eng.algo = algo
+        buf.copy_(_pat(n, r))
+        late()
+        comm.allreduceArray(buf, F, SUM, 0, n)
+        check(algo, torch.equal(buf, _sum(n, p)), f"allreduce.{algo}")
+    eng.algo = "auto"
+    # copy plan (broadcast from the late rank's peer and from the late rank itself)
+    for root in (0, 1):
+        m = 1 << 18
+        base = torch.arange(m, device="cuda", dtype=torch.int32).remainder_(113).float()
+        y = base.clone() if r == root else torch.zeros(m, device="cuda")
+        late()
+        comm.broadcastArray(y, F, 0, m, root)
+        check(f"copy_plan_root{root}", torch.equal(y, base), "broadcast.ipc")
+    # the zero-copy RS / AG halves on the registered tensor
+    counts = [n // p] * p
+    counts[-1] += n - sum(counts)
+    fr, to = CommUtils.getFromsFromCount(0, counts, p), CommUtils.getTosFromCount(0, counts, p)
+    buf.copy_(_pat(n, r))
+    late()
+    comm.reduceScatterArray(buf, F, SUM, 0, counts)
+    check("rs_zc", torch.equal(buf[fr[r]:to[r]], _sum(n, p)[fr[r]:to[r]]), "reduce_scatter.ipc_zc")
+    late()
+    comm.allgatherArray(buf, F, fr, to)
+    check("ag_zc", torch.equal(buf, _sum(n, p)), "allgather.ipc_zc")
+    comm.deregisterBuffer(buf)
+    # fused fp8 two-shot: deterministic, so the late call must equal an on-time call bit for bit
+    m = 1 << 20
+    g = torch.Generator(device="cuda").manual_seed(5 + r)
+    src = torch.randn(m, device="cuda", generator=g)
+    a = src.clone()
+    comm.allreduceArray(a, Operands.FLOAT_OPERAND(codec="fp8"), SUM, 0, m)
+    b = src.clone()
+    late()
+    comm.allreduceArray(b, Operands.FLOAT_OPERAND(codec="fp8"), SUM, 0, m)
+    check("fp8", torch.equal(a, b), "allreduce.fp8.ipc")
+    comm.barrier()
+    words = [i.error_word() for i in eng._ipc_all()] + [i.host_error() for i in eng._ipc_all()]
+    return res, words, spin
+
+
+@pytest.mark.parametrize("p", [2, 4])
+def test_rank_late_by_15s_on_every_ipc_family(p):
+    out = run_spawn(p, _straggler_fn, args=(DELAY,), timeout=int(12 * DELAY + 150))
+    for r, (res, words, spin) in out.items():
+        assert spin >= 60, spin                      # the default bound is the fail-stop budget
+        bad = {k: v for k, v in res.items() if not v[0] or v[1] < 1}
+        assert not bad, (r, bad)
+        assert not any(words), (r, words)

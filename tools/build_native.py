@@ -51,7 +51,7 @@ def torch_lib_dir():
 
 
 def headers():
-    return glob.glob(os.path.join(CSRC, "**", "*.h*"), recursive=True)
+    return [f for ext in ("*.h", "*.hpp") for f in glob.glob(os.path.join(CSRC, "**", ext), recursive=True)]
 
 
 def newer(src, obj, deps):
@@ -85,14 +85,25 @@ def build_hip(jobs, debug=False):
     def comp(so):
         s, o = so
         opt = ["-O1", "-g", "-DMP4X_DEBUG"] if debug else ["-O3"]
-        run([HIPCC, f"--offload-arch={ARCH}"] + opt + ["-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
-             "-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+        # the IPC kernels' register / LDS budgets are kept next to the library: the shared-GPU
+        # co-residency caps are derived from them (mp4x/parallel/occupancy.py)
+        res = not debug and os.path.basename(s).startswith("ipc")
+        out = run([HIPCC, f"--offload-arch={ARCH}"] + opt + ["-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
+                  + (["-Rpass-analysis=kernel-resource-usage"] if res else [])
+                  + ["-I", os.path.join(CSRC, "include"), "-c", s, "-o", o])
+        if res:
+            with open(o + ".res.txt", "w") as f:
+                f.write(out)
         return s
 
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for s in ex.map(comp, todo):
             print("  hipcc", os.path.relpath(s, ROOT))
     out = os.path.join(OUT, "libmp4x_hip_debug.so" if debug else "libmp4x_hip.so")
+    if not debug:
+        table = os.path.join(OUT, "ipc_kernel_resources.json")
+        if todo or not os.path.exists(table):
+            write_resource_table(sorted(o for o in objs if os.path.basename(o).startswith("ipc")), table)
     if todo or not os.path.exists(out):
         tl = torch_lib_dir()
         libdir = tl or "/opt/rocm/lib"
@@ -107,6 +118,47 @@ def build_hip(jobs, debug=False):
         run(link)
         print("  link ", os.path.relpath(out, ROOT), "(hip runtime from", libdir + ")")
     return out
+
+
+def parse_resource_remarks(text):
+    """{mangled kernel name: {"sgpr", "vgpr", "agpr", "lds", "occ"}} from the compiler's
+    ``-Rpass-analysis=kernel-resource-usage`` remarks."""
+    import re
+    keys = {"TotalSGPRs": "sgpr", "VGPRs": "vgpr", "AGPRs": "agpr", "LDS Size [bytes/block]": "lds",
+            "Occupancy [waves/SIMD]": "occ"}
+    table, cur = {}, None
+    for line in text.splitlines():
+        m = re.search(r"remark: Function Name: (\S+)", line)
+        if m:
+            cur = table.setdefault(m.group(1), {})
+            continue
+        m = re.search(r"remark:\s+([A-Za-z][^:]*?): (\d+) \[", line)
+        if m and cur is not None and m.group(1) in keys:
+            cur[keys[m.group(1)]] = int(m.group(2))
+    return table
+
+
+def write_resource_table(objs, path):
+    """Demangled IPC kernel name -> resources, from the remarks saved at compile time."""
+    import json
+    table = {}
+    for o in objs:
+        try:
+            with open(o + ".res.txt") as f:
+                table.update(parse_resource_remarks(f.read()))
+        except OSError:
+            pass
+    names = list(table)
+    dem = names
+    try:
+        r = subprocess.run(["c++filt"], input="\n".join(names), stdout=subprocess.PIPE, text=True, check=True)
+        dem = r.stdout.split("\n")[:len(names)]
+    except Exception:   # noqa: BLE001 — mangled names still parse for the family prefix
+        pass
+    out = {d: table[n] for n, d in zip(names, dem) if "k_ipc" in d}
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    print("  wrote", os.path.relpath(path, ROOT), f"({len(out)} kernels)")
 
 
 def build_host(jobs):
