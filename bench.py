@@ -311,6 +311,9 @@ def main():
         except Exception as e:   # noqa: BLE001 — evidence only
             topo = {"error": str(e)[:200]}
     selftest = None if (p == 1 or args.cpu) else comm.device.ipc_selftest
+    ipc_inst = None if (p == 1 or args.cpu) else comm.device._ipc_obj
+    ipc_info = None if ipc_inst is None else {"spin_s": ipc_inst.spin_s, "share": ipc_inst.share,
+                                              "grid_caps": ipc_inst.grid_caps_summary()}
     stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items() if k.startswith("allreduce")}
     if rank == 0:
         rec = {
@@ -328,9 +331,10 @@ def main():
             "data": "synthetic (torch.randn per rank)",
             "config": {"model": f"allreduceArray float[{n}] ({nbytes / 1e9:g} GB), Operators.Float.SUM",
                        "global_batch": p, "seq_len": n, "parallelism": f"dp{p}",
-                       "payload_bytes": nbytes, "algo": algo, "alloc": args.alloc, "registered": registered,
+                       "payload_bytes": nbytes, "algo": algo,
+                       "alloc": args.alloc if p > 1 else "n/a", "registered": registered if p > 1 else "n/a",
                        "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
-                       "autotune_iters": args.autotune_iters, "ipc_selftest": selftest,
+                       "autotune_iters": args.autotune_iters, "ipc_selftest": selftest, "ipc": ipc_info,
                        "calls": stats, "tier_sweep_ms": tiers, "topology": topo},
             "verified": verified,
             "max_abs_err": max_err,

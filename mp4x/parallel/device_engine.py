@@ -341,6 +341,14 @@ class DeviceEngine(AutotuneMixin):
                 self.ipc_enabled = False
                 return None
             bad = self._ipc_self_test(inst)
+            if bad and all(": zero_copy_" in b for b in bad):
+                # only the zero-copy forms failed (identically known on every rank: the verdict is
+                # agreed): keep the staged kernels, run registered / memAlloc tensors staged
+                LOG.warning("rank %d: IPC zero-copy self-test failed (%s): zero-copy forms disabled on every rank, "
+                            "staged IPC kernels kept", self.rank, bad)
+                self._zc = False
+                self.ipc_selftest = dict(self.ipc_selftest or {}, zero_copy=False)
+                bad = None
             if bad:
                 LOG.warning("rank %d: IPC self-test failed (%s): IPC tiers disabled on every rank, RCCL used",
                             self.rank, bad)
@@ -492,18 +500,20 @@ class DeviceEngine(AutotuneMixin):
         step("broadcast_1MiB", bcast)
         if self._zc:
             # on a dedicated plain allocation (a tensor from the caching allocator may sit in a
-            # segment too large to map, see ipc.IPC_OPEN_MAX)
-            try:
-                nbad = inst.selftest_zero_copy(n4m)
-                if nbad:
-                    fails.append(f"zero_copy_twoshot_4MiB: {'setup failed' if nbad < 0 else f'{nbad} wrong elements'}")
-                torch.cuda.synchronize(dev)
-                code = inst.host_error()
-                inst.raise_if_failed()
-                if code:
-                    fails.append(f"zero_copy_twoshot_4MiB: barrier timeout {code}")
-            except Exception as e:   # noqa: BLE001
-                fails.append(f"zero_copy_twoshot_4MiB: {type(e).__name__}: {e}")
+            # segment too large to map, see ipc.IPC_OPEN_MAX), then on a memAlloc (VMM) tensor
+            for name, fn in (("zero_copy_twoshot_and_plans_4MiB", lambda: inst.selftest_zero_copy(n4m)),
+                             ("zero_copy_memalloc_1MiB", lambda: inst.selftest_memalloc(min(cap, 1 << 18)))):
+                try:
+                    nbad = fn()
+                    if nbad:
+                        fails.append(f"{name}: {'setup failed' if nbad < 0 else f'{nbad} wrong elements'}")
+                    torch.cuda.synchronize(dev)
+                    code = inst.host_error()
+                    inst.raise_if_failed()
+                    if code:
+                        fails.append(f"{name}: barrier timeout {code}")
+                except Exception as e:   # noqa: BLE001
+                    fails.append(f"{name}: {type(e).__name__}: {e}")
         try:
             inst.set_spin(ipcm.spin_default())     # normal operation: the fail-stop budget
         except Exception as e:   # noqa: BLE001

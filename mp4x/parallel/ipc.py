@@ -837,9 +837,10 @@ class IpcAllreduce:
 
     def selftest_zero_copy(self, n: int) -> int:
         """Collective exact-pattern run of the zero-copy two-shot, pull AND push forms (f32 SUM,
-        ``n`` elements) on a dedicated plain device allocation per rank, mapped into every peer
-        like a registered tensor (+ a push scratch).  Returns the number of wrong elements on
-        this rank over both runs (-1: setup failed here)."""
+        ``n`` elements), then of the zero-copy copy plans (gather / scatter), on a dedicated plain
+        device allocation per rank, mapped into every peer like a registered tensor (+ a push
+        scratch); every form twice on the same memory.  Returns the number of wrong elements on
+        this rank over all runs (-1: setup failed here)."""
         nbytes = n * 4
         ptr, scr, opened, err = c_void_p(), c_void_p(), [], None
         hs = self.lib.mp4x_ipc_handle_size()
@@ -898,6 +899,7 @@ class IpcAllreduce:
                     torch.cuda.synchronize()
                     bad += int((got != exp * (self.p ** rep)).sum())
                 self.comm.server.call("barrier", self.rank)     # peers are done before the refill
+            bad += self._selftest_plans(ptr.value, peers, n, got, st)
         elif bad == 0:
             bad = -1
         torch.cuda.synchronize()
@@ -908,6 +910,80 @@ class IpcAllreduce:
             self.lib.mp4x_ipc_free(ptr)
         if scr:
             self.lib.mp4x_ipc_free(scr)
+        return bad
+
+    def _selftest_plans(self, ptr: int, peers, n: int, got: torch.Tensor, st) -> int:
+        """The zero-copy copy plans (gather / scatter pulling straight from the peers' mapped
+        allocations) on the self-test allocation, each twice with fresh data written by the
+        owners in between (a stale line on either side of the link shows as a wrong element).
+        Returns the number of wrong elements on this rank."""
+        p, r, root = self.p, self.rank, self.p - 1
+        nvec = n * 4 // 16
+        lo = [j * nvec // p for j in range(p)]
+        ln = [(j + 1) * nvec // p - lo[j] for j in range(p)]
+        bad = 0
+        for salt in (2, 3):
+            i = (torch.arange(n, device="cuda", dtype=torch.int32) + salt) % 13
+            check(self.lib.mp4x_memcpy_async(ptr, (i + r).float().data_ptr(), n * 4, st), "selftest fill")
+            torch.cuda.synchronize()
+            self.comm.server.call("barrier", self.rank)
+            pull = [(lo[j], lo[j], ln[j], j) for j in range(p) if j != root] if r == root else []
+            self._plan_registered(peers, pull, ptr, max(ln), nvec)        # gather to root
+            check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr, n * 4, st), "selftest read")
+            torch.cuda.synchronize()
+            exp = (i + r).float()
+            if r == root:
+                for j in range(p):
+                    exp[lo[j] * 4:(lo[j] + ln[j]) * 4] += j - r
+            bad += int((got != exp).sum())
+            self.comm.server.call("barrier", self.rank)     # the gather's reads are done
+            if r == root:                                   # new data at the root, then scatter
+                check(self.lib.mp4x_memcpy_async(ptr, (i + 100).float().data_ptr(), n * 4, st), "selftest fill")
+                torch.cuda.synchronize()
+            self.comm.server.call("barrier", self.rank)
+            pull = [(lo[r], lo[r], ln[r], root)] if r != root else []
+            self._plan_registered(peers, pull, ptr, max(ln), nvec)        # scatter from root
+            check(self.lib.mp4x_memcpy_async(got.data_ptr(), ptr, n * 4, st), "selftest read")
+            torch.cuda.synchronize()
+            if r != root:
+                exp[lo[r] * 4:(lo[r] + ln[r]) * 4] = (i + 100).float()[lo[r] * 4:(lo[r] + ln[r]) * 4]
+            else:
+                exp = (i + 100).float()
+            bad += int((got != exp).sum())
+            self.comm.server.call("barrier", self.rank)
+        return bad
+
+    def selftest_memalloc(self, n: int) -> int:
+        """Collective: a memAlloc (VMM chunks exported as dmabuf fds, imported by every peer)
+        tensor of ``n`` f32 through the zero-copy two-shot, pull and push, each twice on the same
+        memory (the second call reduces the first call's result).  Returns this rank's wrong
+        elements (-1: setup failed on some rank, agreed)."""
+        try:
+            t = self.mem_alloc(n * 4, torch.float32)
+        except Exception:   # noqa: BLE001 — agreed inside mem_alloc (every rank raises)
+            return -1
+        from ..operators import Operators, for_dtype, DType
+        op = for_dtype(Operators.Float.SUM, DType.F32)
+        bad = 0
+        try:
+            reg, _ = self._find(t)
+            for push in (False, True):
+                i = (torch.arange(n, device="cuda", dtype=torch.int32) + int(push)) % 13
+                t.copy_((i + self.rank).float())
+                exp = (i * self.p + self.p * (self.p - 1) // 2).float()
+                torch.cuda.synchronize()
+                self.comm.server.call("barrier", self.rank)
+                for rep in range(2):
+                    if push and reg.scratch is not None:
+                        self._push_ptrs(n * 4, op, reg.peers, reg.scratch, torch.float32)
+                    else:
+                        self.allreduce_registered_ptrs(t.data_ptr(), n * 4, op, reg.peers, torch.float32)
+                    torch.cuda.synchronize()
+                    bad += int((t != exp * (self.p ** rep)).sum())
+                self.comm.server.call("barrier", self.rank)
+        finally:
+            torch.cuda.synchronize()
+            self.mem_free(t)
         return bad
 
     def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0,
