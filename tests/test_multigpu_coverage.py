@@ -1,0 +1,66 @@
+"""CPU check that the cross-GPU test module (tests/test_multigpu_gpu.py, which auto-skips below p
+GPUs) runs EVERY schedule the device engine can select, so one multi-GPU lease validates the
+whole engine with RCCL underneath and no edits (VERDICT r3 Next #2).  The universe comes from the
+engine itself — its allreduce candidates (one GPU per rank, RCCL, a multi-node layout for
+``hier``), its capturable set, its codecs, and the schedules each RS / AG / rooted tuner can pin —
+so a new schedule without a cross-GPU test fails here."""
+import ast
+import os
+
+import torch
+
+from mp4x import Operators
+from mp4x.parallel.device_engine import DeviceEngine
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _covers():
+    src = open(os.path.join(HERE, "test_multigpu_gpu.py")).read()
+    tree = ast.parse(src)
+    covers, funcs = None, set()
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and any(getattr(t, "id", None) == "COVERS" for t in node.targets):
+            covers = ast.literal_eval(node.value)
+        if isinstance(node, ast.FunctionDef):
+            funcs.add(node.name)
+    return covers, funcs
+
+
+def _universe():
+    e = object.__new__(DeviceEngine)
+    e.backend, e.device, e.ipc_enabled, e._zc, e.p = "nccl", torch.device("cuda", 0), True, True, 8
+    e.ipc_twoshot_max, e.ipc_oneshot_max = 16 << 20, 256 << 10
+
+    class _Ipc:
+        shared_gpu = False
+    e._ipc_obj = _Ipc()
+    e._hier_ok = lambda op, dt, nb: True          # a multi-node layout lists the node-aware schedule
+    names = set()
+    for nb in (4096, 1 << 20, 64 << 20, 1 << 30):
+        names |= set(e.allreduce_candidates(nb, Operators.Float.SUM, torch.float32))
+    names |= set(DeviceEngine._CAPTURABLE) | {"zs", "fp8", "bf16"} | set(DeviceEngine._KNOWN_ALGOS["allreduce"])
+    uni = {f"allreduce:{a}" for a in names}
+    for kind, algos in DeviceEngine._KNOWN_ALGOS.items():
+        if kind == "allreduce":
+            continue
+        extra = {"rccl"} if kind in ("reduce_scatter", "allgather") else set()   # their unpinned default
+        uni |= {f"{kind}:{a}" for a in set(algos) | extra}
+    return uni
+
+
+def test_multigpu_module_names_every_schedule():
+    covers, funcs = _covers()
+    assert covers, "tests/test_multigpu_gpu.py has no COVERS table"
+    missing_tests = set(covers) - funcs
+    assert not missing_tests, f"COVERS names tests that do not exist: {missing_tests}"
+    covered = set().union(*map(set, covers.values()))
+    missing = _universe() - covered
+    assert not missing, f"schedules no cross-GPU test runs: {sorted(missing)}"
+
+
+def test_universe_is_not_trivially_small():
+    uni = _universe()
+    assert {"allreduce:rccl", "allreduce:ipc2z", "allreduce:hier", "allreduce:rccl_c112", "allreduce:zs",
+            "broadcast:composite", "gather:p2p", "reduce_scatter:ipc"} <= uni
+    assert len(uni) >= 25
