@@ -141,14 +141,10 @@ class AutotuneMixin:
         the same shape; the decision uses the MAX time over ranks, so all ranks agree.
 
         Returns {algo: seconds per call} (inf for a schedule that failed on any rank)."""
-        # one scratch tensor per (dtype, size), kept: a re-tune of the same class registers the
-        # same allocation again, whose peer mappings are cached (ipc.IpcAllreduce._open_peer_base)
-        key = (like.dtype, like.numel())
-        view = self._tune_scratch.get(key)
-        if view is None:
-            view = self._tune_scratch[key] = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
-        else:
-            view.zero_()
+        # a scratch tensor for this tune only: registered for the zero-copy candidates, deregistered
+        # and dropped afterwards (nothing is retained per size class; its memory goes back to the
+        # caching allocator and a re-tune of the class usually gets the same block again)
+        view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         op = self._op(operator, view)
         nbytes = view.numel() * view.element_size()
         if candidates is None and os.environ.get("MP4X_AUTOTUNE_CANDIDATES"):

@@ -191,7 +191,6 @@ class DeviceEngine(AutotuneMixin):
         self._tuned: Dict[tuple, str] = _TunedTable()
         self._sel_memo: Dict[tuple, tuple] = {}       # select() decisions of repeated call shapes
         self._dm_large = os.environ.get("MP4X_DM_LARGE", "auto")
-        self._tune_scratch: Dict[tuple, torch.Tensor] = {}   # autotune_allreduce scratch per (dtype, numel)
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
         self._select_tuned = False
         self._load_shared_tuning(shared=coll is None)
