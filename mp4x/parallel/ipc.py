@@ -85,6 +85,14 @@ DATA_COARSE = os.environ.get("MP4X_IPC_DATA_MEM", "uncached").lower() == "coarse
 # (measured: 2.0 GB opens in 0.1 ms, 2 GiB hangs — profiles/r2/ipc_open_probe.jsonl), so
 # registration refuses such allocations (every rank alike): the staged kernels run instead.
 IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
+# Memory lifetime (diagnosed with tools/repro/ipc_lifetime_repro.hip):
+# CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' allocations (refcounted
+#   per allocation) and frees its push scratch, instead of caching every mapping and pooling every
+#   scratch until close();
+# VMM_RELEASE — memFree releases the VMM chunks collectively, every importer's mapping first and
+#   the owners' memory after a barrier, instead of parking the allocation in a per-size pool.
+CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
+VMM_RELEASE = os.environ.get("MP4X_VMM_RELEASE", "1") == "1"
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64,
                     torch.int16, torch.int8, torch.uint8}
 _FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
@@ -147,14 +155,16 @@ def _agree(comm, rank, obj, is_bad):
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
         self.scratch = None
         self.keep = keep                 # the registered tensor: its memory stays allocated
         self.scratch_alloc = None        # own push scratch: (allocation, IPC handle bytes)
-        self.vmm: list = []              # memAlloc: own + imported VmmRegions
+        self.vmm: list = []              # memAlloc: own regions first (nown of them), then imported
+        self.nown = 0
+        self.peer_keys: list = []        # (rank, handle bytes) of every peer mapping this one uses
 
 
 class IpcAllreduce:
@@ -299,7 +309,8 @@ class IpcAllreduce:
         # registered caller tensors (zero-copy two-shot): (data_ptr, nbytes) -> (peer pointers,
         # every rank's push scratch or None)
         self._regs = {}
-        self._peer_bases = {}       # (rank, handle bytes) -> mapped address (opened once)
+        self._peer_bases = {}       # (rank, handle bytes) -> mapped address
+        self._peer_refs = {}        # (rank, handle bytes) -> registrations using the mapping
         self._scratch_pool = {}     # push-scratch bytes -> [(allocation, handle)] free for reuse
         self._scratch_size = {}     # push-scratch address -> bytes
         self._vmm_pool = {}         # memAlloc size -> [freed registrations] (see mem_free)
@@ -573,8 +584,11 @@ class IpcAllreduce:
                     continue
                 hk = (r, bytes(b[0]))
                 reg.peers.append(self._open_peer_base(hk, hs) + int(b[1]))
+                reg.peer_keys.append(hk)
                 if push:
-                    scr.append(self._open_peer_base((r, bytes(b[4])), hs))
+                    sk = (r, bytes(b[4]))
+                    scr.append(self._open_peer_base(sk, hs))
+                    reg.peer_keys.append(sk)
         except Exception as e:   # noqa: BLE001
             err = str(e)
         reg.scratch = scr if push else None
@@ -591,28 +605,41 @@ class IpcAllreduce:
         return True
 
     def _open_peer_base(self, hk, hs: int) -> int:
-        """Mapped address of peer allocation ``hk`` = (rank, handle bytes): opened once, cached
-        until close().  Mappings are never closed early: closing one and later opening a new
-        allocation handed out at recycled addresses made the new mapping read the wrong memory
-        on this ROCm (tests/test_ipc_zc_gpu.py push form at p = 4, tools/vmm_realloc_probe.py)."""
+        """Mapped address of peer allocation ``hk`` = (rank, handle bytes), opened once and
+        reference-counted per registration using it (several registered tensors can share one
+        caching-allocator segment); :meth:`_close_peer` closes it when the last one is released."""
         ent = self._peer_bases.get(hk)
         if ent is None:
             hb = ctypes.create_string_buffer(hk[1], hs)
             ptr = c_void_p()
             check(self.lib.mp4x_ipc_open_handle(hb, ctypes.byref(ptr)), f"ipc_open_handle(rank {hk[0]})")
             ent = self._peer_bases[hk] = ptr
+        self._peer_refs[hk] = self._peer_refs.get(hk, 0) + 1
         return ent.value
+
+    def _close_peer(self, hk) -> None:
+        """Drop one registration's use of peer mapping ``hk``; the last one closes it
+        (``CLOSE_PEERS``; otherwise it stays cached until close())."""
+        n = self._peer_refs.get(hk, 0) - 1
+        if n > 0:
+            self._peer_refs[hk] = n
+            return
+        self._peer_refs.pop(hk, None)
+        if CLOSE_PEERS:
+            ptr = self._peer_bases.pop(hk, None)
+            if ptr is not None:
+                self.lib.mp4x_ipc_close_handle(ptr)
 
     def _alloc_scratch(self, nbytes: int, hs: int):
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
         slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
         (allocation, IPC handle), or (None, None): the registration then has no push form.
-        A scratch of the same size that an earlier deregistration returned is reused (the peers'
-        mappings of it are cached by handle, so nothing is re-opened)."""
+        Without ``CLOSE_PEERS``, a scratch of the same size that an earlier deregistration
+        returned is reused (the peers' mappings of it stay cached by handle)."""
         chunk = -(-(nbytes // 16) // self.p)
         size = max(16, (self.p - 1) * chunk * 16)
         pooled = self._scratch_pool.get(size)
-        if pooled:
+        if pooled and not CLOSE_PEERS:
             return pooled.pop()
         ptr = c_void_p()
         try:
@@ -629,26 +656,37 @@ class IpcAllreduce:
         return ptr, h.raw
 
     def _free_scratch(self, scr) -> None:
-        """Back to the per-size pool (freed at close())."""
+        """Free a push scratch (``CLOSE_PEERS``: its peers close their mappings at their own
+        deregistration; until then the driver keeps the memory alive for them), or park it in
+        the per-size pool (freed at close())."""
         if scr and scr[0]:
-            self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
+            if CLOSE_PEERS:
+                self._scratch_size.pop(scr[0].value, None)
+                self.lib.mp4x_ipc_free(scr[0])
+            else:
+                self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
     def _release(self, reg: "_Reg") -> None:
-        """Return ``reg``'s scratch to the pool and drop its tensor reference (peer mappings stay
-        cached, see :meth:`_open_peer_base`); memAlloc regions are unmapped and released (only
-        at close(), see :meth:`mem_free`)."""
+        """Release what ``reg`` holds on this rank: its scratch, its uses of the peer mappings
+        (:meth:`_close_peer`) and its tensor reference; memAlloc regions are unmapped and released,
+        imported views first (the collective, ordered release is :meth:`mem_free`)."""
         self._free_scratch(reg.scratch_alloc)
         reg.scratch_alloc = None
+        for hk in reg.peer_keys:
+            self._close_peer(hk)
+        reg.peer_keys = []
         for region in reversed(reg.vmm):     # the peers' imported views first, own memory last
             region.free()
         reg.vmm = []
         reg.keep = None
 
     def deregister(self, t: torch.Tensor) -> None:
-        """Forget ``t``: its push scratch goes back to a per-size pool for the next registration
+        """Forget ``t``: once this rank's stream drained, its mappings of the peers' tensors and
+        scratches are closed (when no other registration uses them), its push scratch is freed
         and the reference to ``t`` is dropped.  Every peer deregisters its tensor at the same
-        point (the registration contract); the local stream is drained first.  A memAlloc tensor
-        stays registered until memFree."""
+        point (the registration contract): each closes its own mappings, and the memory a rank
+        frees stays alive in the driver until the last peer mapping of it is closed.  A memAlloc
+        tensor stays registered until memFree."""
         key = (t.data_ptr(), t.numel() * t.element_size())
         reg = self._regs.get(key)
         if reg is None or reg.vmm:
@@ -698,7 +736,7 @@ class IpcAllreduce:
         from . import vmm
         nb16 = -(-int(nbytes) // 16) * 16
         es = torch.empty((), dtype=dtype).element_size()
-        pooled = self._vmm_pool.get(nb16)
+        pooled = self._vmm_pool.get(nb16) if not VMM_RELEASE else None
         if pooled:
             # a freed allocation of this size (the same one on every rank: pool states agree)
             reg = pooled.pop()
@@ -741,6 +779,7 @@ class IpcAllreduce:
             scr.close_fds()
         reg = _Reg(keep=None)
         reg.vmm = [own] + ([scr] if scr is not None else [])
+        reg.nown = len(reg.vmm)
         scratch = []
         err = None
         try:
@@ -788,13 +827,23 @@ class IpcAllreduce:
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # no peer kernel still reads or writes it
         reg = self._regs.pop(key)
-        # Not released here: unmapping + releasing VMM chunks (own and imported) and then
-        # exporting / importing new ones made the NEXT allocation's peer mappings read zeros on
-        # this ROCm (gfx950, 3 ranks: tools/vmm_realloc_probe.py, profiles/r3/vmm_realloc.txt).
-        # The allocation is parked in a per-size pool instead and handed out again by the next
-        # memAlloc of the same size (every rank's pool state is identical: alloc / free are
-        # collective), so an alloc/free loop does not grow; everything is released at close().
-        self._vmm_pool.setdefault(key[1], []).append(reg)
+        if not VMM_RELEASE:
+            # park the allocation in a per-size pool, handed out again by the next memAlloc of the
+            # same size (every rank's pool state is identical: alloc / free are collective)
+            self._vmm_pool.setdefault(key[1], []).append(reg)
+            return
+        # Ordered, collective release.  Round 3 released every rank's imported views and its own
+        # chunks in one local pass, so an owner could release its chunks while a peer still had
+        # them imported and mapped; the next allocation's peer views then read zeros.  Here every
+        # importer unmaps and releases first, and the owners release only after all have.
+        for region in reg.vmm[reg.nown:]:
+            region.free()
+        torch.cuda.synchronize(self.device)
+        self.comm.server.call("barrier", self.rank)     # every peer released its imports
+        for region in reg.vmm[:reg.nown]:
+            region.free()
+        reg.vmm = []
+        reg.keep = None
 
     def allreduce_push(self, view: torch.Tensor, op, peers, scratch, scale: float = 1.0) -> torch.Tensor:
         """In place, on registered tensors, with every xGMI transfer a posted WRITE (see

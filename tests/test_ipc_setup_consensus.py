@@ -209,12 +209,15 @@ class _FakeTensor:
         return 4
 
 
-def test_registration_lifecycle_pools_scratch_and_keeps_mappings(monkeypatch):
-    """deregister() returns the push scratch to a per-size pool and keeps peer mappings cached
-    (closing + re-opening recycled addresses mapped the wrong memory on ROCm); a registration
-    holds its tensor; close() frees / closes everything."""
+@pytest.mark.parametrize("close_peers", [True, False])
+def test_registration_lifecycle(monkeypatch, close_peers):
+    """CLOSE_PEERS (default): deregister() closes this rank's mappings of the peers' allocations
+    once no registration uses them and frees the push scratch, so nothing accumulates per
+    registration.  Without it (the round-3 policy): scratch pooled per size, mappings cached until
+    close().  Either way a registration holds its tensor and close() releases everything."""
     p = 2
     lib = _CountingLib()
+    monkeypatch.setattr(ipc_mod, "CLOSE_PEERS", close_peers)
     monkeypatch.setattr(ipc_mod.native, "hip", lambda: lib)
     monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
     monkeypatch.setattr(ipc_mod.torch.cuda, "synchronize", lambda *a, **k: None)
@@ -223,25 +226,24 @@ def test_registration_lifecycle_pools_scratch_and_keeps_mappings(monkeypatch):
 
     def run(r):
         inst = ipc_mod.IpcAllreduce(_Comm(server, r), nbytes=1 << 16)
-        base_allocs, base_opens = lib.allocs, lib.opens
+        base_allocs = lib.allocs
         server.call("barrier", r)
         a = _FakeTensor(0x7000000 + r * 0x1000000, 1 << 16)
         b = _FakeTensor(0x7100000 + r * 0x1000000, 1 << 16)
         ok1 = inst.register(a)
         keeps = inst._find(a)[0].keep is a
+        opened = len(inst._peer_bases)
         inst.deregister(a)
         server.call("barrier", r)
-        allocs_after_first = lib.allocs
-        ok2 = inst.register(b)                       # same size: the pooled scratch comes back
+        after_dereg = (len(inst._peer_bases), sum(len(v) for v in inst._scratch_pool.values()))
+        ok2 = inst.register(b)
         server.call("barrier", r)
-        reused = lib.allocs == allocs_after_first
         inst.deregister(b)
-        ok3 = inst.register(a)                       # a again: its peer mapping is cached
+        ok3 = inst.register(a)
         server.call("barrier", r)
-        closes_before = lib.closes
         inst.deregister(a)
         server.call("barrier", r)
-        res[r] = (ok1, ok2, ok3, keeps, reused, closes_before, lib.allocs - base_allocs, inst)
+        res[r] = (ok1, ok2, ok3, keeps, opened, after_dereg, lib.allocs - base_allocs, inst)
 
     threads = [threading.Thread(target=run, args=(r,)) for r in range(p)]
     for t in threads:
@@ -249,15 +251,20 @@ def test_registration_lifecycle_pools_scratch_and_keeps_mappings(monkeypatch):
     for t in threads:
         t.join(20)
     assert not any(t.is_alive() for t in threads)
-    for ok1, ok2, ok3, keeps, reused, closes_before, allocs, inst in res:
-        assert ok1 and ok2 and ok3 and keeps and reused
-        assert closes_before == 0                    # nothing closed while the job runs
-        assert allocs <= p                           # one push scratch per rank, reused
+    for ok1, ok2, ok3, keeps, opened, after_dereg, allocs, inst in res:
+        assert ok1 and ok2 and ok3 and keeps
+        assert opened == 2                           # the peer's tensor segment + its push scratch
+        if close_peers:
+            assert after_dereg == (0, 0)             # mappings closed, scratch freed
+            assert not inst._peer_refs and not inst._peer_bases
+            assert allocs >= 3                       # one scratch per registration (freed at each)
+        else:
+            assert after_dereg == (2, 1)             # cached mappings, pooled scratch
+            assert allocs <= p                       # the pooled scratch came back
         assert not inst._regs
-    opens = lib.opens
     for *_, inst in res:
         inst.close(sync=False)
-    assert lib.closes >= opens                      # every mapping closed at close()
+    assert lib.closes >= lib.opens                   # every mapping closed by close() at the latest
 
 
 def test_hier_submesh_failure_on_one_node_is_agreed_job_wide(monkeypatch):
