@@ -308,6 +308,11 @@ def main():
                 rec["max_abs_error"] = worst
                 rec["exact"] = rel < (0.1 if codec == "fp8" else 1e-6)
             emit(rec)
+    if eng is not None and r == 0:
+        # the IPC instances' co-residency grid caps (shared GPU: derived per kernel from occupancy)
+        caps = {name: inst.grid_caps_summary() for name, inst in
+                (("default", eng._ipc_obj), ("large", eng._ipc_large), ("fp8", eng._ipc_fp8_big)) if inst is not None}
+        emit({"ipc_grid_caps": caps, "share": getattr(eng._ipc_obj, "share", None)})
     comm.close(0)
     if dist.is_initialized():
         dist.destroy_process_group()
