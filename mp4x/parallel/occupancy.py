@@ -18,7 +18,7 @@ not guessed per library:
   The API alone over-reports by one block per CU for SGPR-heavy kernels on ROCm 7.2
   (cdna_hip_programming.md §1), so the smaller of the two answers is used.
 
-The shared-GPU cap is ``CUs * max(1, bpc // 2) // share``: the ranks sharing a GPU get half of its
+The shared-GPU cap is ``CUs * bpc // (2 * share)``: the ranks sharing a GPU get half of its
 resident capacity between them — the other half absorbs the ranks' own non-IPC kernels (quantise,
 copies, torch) and dispatch imbalance across the 8 XCDs.  With the full capacity (fp8 two-shot at
 8 ranks: 2 blocks per CU, 64 blocks per rank) the ranks stalled at the start barrier; with half
@@ -78,7 +78,7 @@ def shared_grid_cap(cus: int, bpc: int, share: int) -> int:
     blocks per CU (half the resident capacity split between the ranks, at least 1 block)."""
     if share <= 1:
         return MAX_BLOCKS
-    return max(1, min(MAX_BLOCKS, cus * max(1, bpc // 2) // share))
+    return max(1, min(MAX_BLOCKS, cus * max(1, bpc) // (2 * share)))
 
 
 _TABLE: Optional[Dict[Tuple[str, Tuple[int, ...]], Dict[str, int]]] = None

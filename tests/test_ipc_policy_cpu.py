@@ -113,7 +113,8 @@ def test_shared_grid_cap_halves_the_resident_budget():
     assert occ.shared_grid_cap(256, 4, 1) == 256              # a GPU of its own: no cap
     assert occ.shared_grid_cap(256, 4, 8) == 64               # 256 * 2 / 8 (the r1-r3 generic budget)
     assert occ.shared_grid_cap(256, 2, 8) == 32               # the fp8 two-shot at 8 ranks (config 5)
-    assert occ.shared_grid_cap(256, 1, 8) == 32               # at least one block per CU of budget
+    assert occ.shared_grid_cap(256, 3, 8) == 48               # an SGPR-bound kernel: 3 blocks per CU
+    assert occ.shared_grid_cap(256, 1, 8) == 16
     assert occ.shared_grid_cap(256, 4, 2) == 256
     assert occ.shared_grid_cap(4, 1, 8) == 1                  # never 0
 
