@@ -1003,36 +1003,39 @@ class IpcAllreduce:
         return bad
 
     def selftest_memalloc(self, n: int) -> int:
-        """Collective: a memAlloc (VMM chunks exported as dmabuf fds, imported by every peer)
-        tensor of ``n`` f32 through the zero-copy two-shot, pull and push, each twice on the same
-        memory (the second call reduces the first call's result).  Returns this rank's wrong
+        """Collective: memAlloc (VMM chunks exported as dmabuf fds, imported by every peer)
+        tensors through the zero-copy two-shot, pull and push, each twice on the same memory (the
+        second call reduces the first call's result) — in TWO alloc / free cycles of different
+        sizes, so an allocation made after a memFree released memory is checked too (round 3 saw
+        every later allocation's peer views read zeros after a release).  Returns this rank's wrong
         elements (-1: setup failed on some rank, agreed)."""
-        try:
-            t = self.mem_alloc(n * 4, torch.float32)
-        except Exception:   # noqa: BLE001 — agreed inside mem_alloc (every rank raises)
-            return -1
         from ..operators import Operators, for_dtype, DType
         op = for_dtype(Operators.Float.SUM, DType.F32)
         bad = 0
-        try:
-            reg, _ = self._find(t)
-            for push in (False, True):
-                i = (torch.arange(n, device="cuda", dtype=torch.int32) + int(push)) % 13
-                t.copy_((i + self.rank).float())
-                exp = (i * self.p + self.p * (self.p - 1) // 2).float()
-                torch.cuda.synchronize()
-                self.comm.server.call("barrier", self.rank)
-                for rep in range(2):
-                    if push and reg.scratch is not None:
-                        self._push_ptrs(n * 4, op, reg.peers, reg.scratch, torch.float32)
-                    else:
-                        self.allreduce_registered_ptrs(t.data_ptr(), n * 4, op, reg.peers, torch.float32)
+        for m in (n, n // 2 + (3 << 12)):
+            try:
+                t = self.mem_alloc(m * 4, torch.float32)
+            except Exception:   # noqa: BLE001 — agreed inside mem_alloc (every rank raises)
+                return -1
+            try:
+                reg, _ = self._find(t)
+                for push in (False, True):
+                    i = (torch.arange(m, device="cuda", dtype=torch.int32) + int(push)) % 13
+                    t.copy_((i + self.rank).float())
+                    exp = (i * self.p + self.p * (self.p - 1) // 2).float()
                     torch.cuda.synchronize()
-                    bad += int((t != exp * (self.p ** rep)).sum())
-                self.comm.server.call("barrier", self.rank)
-        finally:
-            torch.cuda.synchronize()
-            self.mem_free(t)
+                    self.comm.server.call("barrier", self.rank)
+                    for rep in range(2):
+                        if push and reg.scratch is not None:
+                            self._push_ptrs(m * 4, op, reg.peers, reg.scratch, torch.float32)
+                        else:
+                            self.allreduce_registered_ptrs(t.data_ptr(), m * 4, op, reg.peers, torch.float32)
+                        torch.cuda.synchronize()
+                        bad += int((t != exp * (self.p ** rep)).sum())
+                    self.comm.server.call("barrier", self.rank)
+            finally:
+                torch.cuda.synchronize()
+                self.mem_free(t)
         return bad
 
     def allreduce_registered_ptrs(self, dst: int, total: int, op, peers, dtype, scale: float = 1.0,

@@ -232,3 +232,32 @@ def test_process_barrier_and_close_surface_a_timed_out_collective():
     finally:
         code = m.stop(timeout=5)
     assert code == 1
+
+
+@pytest.mark.parametrize("fails,zc,enabled", [
+    (["rank 1: zero_copy_memalloc_1MiB: 12 wrong elements"], False, True),      # zero-copy only: staged kept
+    (["rank 0: zero_copy_twoshot_and_plans_4MiB: barrier timeout 2", "rank 1: twoshot_4MiB: 3 wrong elements"],
+     True, False),                                                              # a core family: IPC off
+    (None, True, True)])
+def test_self_test_failure_scope(monkeypatch, fails, zc, enabled):
+    """A failed zero-copy self-test drops only the zero-copy forms on every rank (registered /
+    memAlloc tensors then run staged); any other failure disables IPC (the verdict is agreed, so
+    every rank takes the same branch)."""
+    import mp4x.parallel.ipc as ipcm
+
+    class _FakeInst:
+        closed = False
+
+        def __init__(self, comm, *a, **k):
+            pass
+
+        def close(self, *a, **k):
+            _FakeInst.closed = True
+
+    monkeypatch.setattr(ipcm, "IpcAllreduce", _FakeInst)
+    e = _engine()
+    e.comm, e.rank = object(), 0
+    e._ipc_self_test = lambda inst: fails
+    got = e.ipc()
+    assert e._zc is zc and e.ipc_enabled is enabled
+    assert (got is not None) is enabled and _FakeInst.closed is (not enabled)
