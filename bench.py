@@ -90,6 +90,117 @@ def _measure(torch, step, steps, sync_all):
     return wall, sorted(s.elapsed_time(e) for s, e in zip(starts, ends))
 
 
+def _timed_p50(torch, fn, iters, sync):
+    """p50 ms of ``iters`` calls of ``fn``, each bracketed by syncs (host clock)."""
+    ts = []
+    for _ in range(iters):
+        sync()
+        t0 = time.perf_counter()
+        fn()
+        sync()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+def _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev):
+    """BASELINE configs 3 / 4 / 5 on this job (evidence; each bounded, failures recorded, every
+    rank stops together).  Exact checks for 3 and 4, the fp64 error bound for 5."""
+    from mp4x import CommUtils, Operands, Operators
+    out = {}
+
+    def sync():
+        torch.cuda.synchronize()
+        comm.device.barrier()
+        torch.cuda.synchronize()
+
+    def cfg3():
+        n = 2_000_000_000 // p * p
+        x = comm.memAlloc(n, torch.bfloat16)
+        try:
+            B = Operands.BF16_OPERAND()
+            counts = [n // p] * p
+            fr, to = CommUtils.getFromsFromCount(0, counts, p), CommUtils.getTosFromCount(0, counts, p)
+            CH = 1 << 28
+            for s0 in range(0, n, CH):
+                i = torch.arange(s0, min(n, s0 + CH), device=dev)
+                x[s0:s0 + CH] = (i % 13 + rank).to(torch.bfloat16)
+
+            def step():
+                comm.reduceScatterArray(x, B, Operators.BFloat16.SUM, 0, counts)
+                comm.allgatherArray(x, B, fr, to)
+            step()
+            sync()
+            ok = True
+            for s0 in range(0, n, CH):
+                i = torch.arange(s0, min(n, s0 + CH), device=dev)
+                ok &= bool(torch.equal(x[s0:s0 + CH], (p * (i % 13) + p * (p - 1) // 2).to(torch.bfloat16)))
+            ms = _timed_p50(torch, step, 5, sync)
+            return {"ms": round(ms, 3), "exact": ok,
+                    "busbw_gbps": round(n * 2 / (ms * 1e-3) / 1e9 * 2 * (p - 1) / p, 2)}
+        finally:
+            comm.memFree(x)
+
+    def cfg4():
+        dim, nkeys = 64, 200_000
+        shared = nkeys // 2
+        ids = torch.cat([torch.arange(shared), 10_000_000 + rank * nkeys + torch.arange(nkeys - shared)]).to(dev)
+        vals = (torch.arange(nkeys * dim, device=dev) % 7 + rank).float().view(nkeys, dim)
+        fn = lambda: comm.allreduceSparse(ids, vals, Operators.Float.SUM)   # noqa: E731
+        rk, rv = fn()
+        sync()
+        # shared ids: sum over ranks of (row pattern + rank); own ids: that rank's row only
+        base = (torch.arange(shared * dim, device=dev) % 7).float().view(shared, dim)
+        order = torch.argsort(rk)
+        rk, rv = rk[order], rv[order]
+        ok = bool(torch.equal(rk[:shared].cpu(), torch.arange(shared))) and \
+            bool(torch.equal(rv[:shared], base * p + p * (p - 1) / 2)) and rk.numel() == shared + p * (nkeys - shared)
+        ms = _timed_p50(torch, fn, 5, sync)
+        return {"ms": round(ms, 3), "exact": ok, "keys_per_rank": nkeys, "dim": dim}
+
+    def cfg5():
+        n = 2_000_000_000
+        x = torch.empty(n, device=dev)
+        CH = 1 << 27
+
+        def fill(dst, r):
+            for c, s0 in enumerate(range(0, n, CH)):
+                g = torch.Generator(device=dev).manual_seed(r * 100003 + c)
+                dst[s0:s0 + CH] = torch.randn(min(CH, n - s0), device=dev, generator=g)
+        F8 = Operands.FLOAT_OPERAND(codec="fp8")
+        fill(x, rank)
+        comm.allreduceArray(x, F8, Operators.Float.SUM, 0, n)
+        sync()
+        num = den = 0.0
+        for c, s0 in enumerate(range(0, 1 << 28, CH)):        # error on the first 1 GB (bounded cost)
+            ref = torch.zeros(CH, dtype=torch.float64, device=dev)
+            for j in range(p):
+                g = torch.Generator(device=dev).manual_seed(j * 100003 + c)
+                ref += torch.randn(CH, device=dev, generator=g).double()
+            d = x[s0:s0 + CH].double() - ref
+            num += float((d * d).sum())
+            den += float((ref * ref).sum())
+        rel = (num / max(den, 1e-300)) ** 0.5
+        ms = _timed_p50(torch, lambda: comm.allreduceArray(x, F8, Operators.Float.SUM, 0, n, scale=1.0 / p), 3, sync)
+        del x
+        return {"ms": round(ms, 3), "rel_l2_error_vs_fp64": round(rel, 5), "exact": rel < 0.1,
+                "busbw_gbps": round(8e9 / (ms * 1e-3) / 1e9 * 2 * (p - 1) / p, 2)}
+
+    for name, fn in (("config3_rs_ag_4gb_bf16", cfg3), ("config4_sparse_200k_x64", cfg4),
+                     ("config5_fp8_8gb", cfg5)):
+        failed = 0.0
+        try:
+            out[name] = fn()
+        except Exception as e:   # noqa: BLE001 — evidence only; the headline is already measured
+            out[name] = {"error": str(e)[:200]}
+            failed = 1.0
+        torch.cuda.empty_cache()
+        flag = torch.tensor([failed], dtype=torch.float64, device=agree_dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if flag.item() > 0:
+            break
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,6 +222,8 @@ def main():
     ap.add_argument("--sweep-sizes", default="4096,65536,262144,1048576,4194304,16777216,67108864",
                     help="N>1: comma-separated byte sizes of the allreduce schedule sweep, in order")
     ap.add_argument("--no-rooted-sweep", action="store_true", help="N>1: skip the rooted collectives' sweep")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="N>1: skip the untimed BASELINE configs 3-5 (4 GB bf16 RS+AG, sparse map, 8 GB fp8) run last")
     args = ap.parse_args()
     if args.no_register:
         args.alloc = "plain"
@@ -296,6 +409,13 @@ def main():
                 break
         tiers["rooted"] = rooted
 
+    # the other BASELINE.json configs at this rank count, after everything above (never timed with
+    # the headline): config 3 (RS + AG of a 4 GB bf16 memAlloc tensor), config 4 (sparse rows,
+    # 200k keys x float[64] per rank, half shared), config 5 (8 GB f32 allreduce, fp8 wire codec)
+    configs = None
+    if p > 1 and not args.cpu and not args.no_configs and not (args.algo or args.codec):
+        configs = _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev)
+
     ref = REF_BUSBW_MBPS.get(p)
     topo = None
     if rank == 0 and not args.cpu:
@@ -335,7 +455,7 @@ def main():
                        "alloc": args.alloc if p > 1 else "n/a", "registered": registered if p > 1 else "n/a",
                        "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
                        "autotune_iters": args.autotune_iters, "ipc_selftest": selftest, "ipc": ipc_info,
-                       "calls": stats, "tier_sweep_ms": tiers, "topology": topo},
+                       "calls": stats, "tier_sweep_ms": tiers, "baseline_configs": configs, "topology": topo},
             "verified": verified,
             "max_abs_err": max_err,
             "busbw_gbps_per_rank": round(busbw, 3),
