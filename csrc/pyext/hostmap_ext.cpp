@@ -207,9 +207,9 @@ PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
     const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
     PyObject** items = PySequence_Fast_ITEMS(seq);
     bool ok = true;
+    PyObject* id = nullptr;                                    // the next id, made once per insert
     for (Py_ssize_t i = 0; i < n && ok; ++i) {
-      PyObject* id = PyLong_FromSsize_t(next);
-      if (!id) {
+      if (!id && !(id = PyLong_FromSsize_t(next))) {
         ok = false;
         break;
       }
@@ -219,9 +219,11 @@ PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
       } else if (got == id) {                                  // inserted: a new key
         if (PyList_Append(ids, items[i]) != 0) ok = false;
         ++next;
-      }
-      Py_DECREF(id);
+        Py_DECREF(id);                                         // the dict holds it now
+        id = nullptr;
+      }                                                        // known key: the id object is reused
     }
+    Py_XDECREF(id);
     Py_DECREF(seq);
     if (!ok) break;
   }

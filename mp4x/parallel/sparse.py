@@ -129,7 +129,10 @@ def allgather_keys(engine, new: List) -> List[List]:
         return engine.all_gather_object(list(new))
     host = getattr(engine.comm, "engine", None)
     if host is not None and hasattr(host, "allgather_bytes"):
-        return [decode_keys(b) for b in host.allgather_bytes(encode_keys(new))]
+        r = engine.rank
+        mine = list(new)
+        # this rank's own block is the list it already holds (no decode of its own bytes)
+        return [mine if j == r else decode_keys(b) for j, b in enumerate(host.allgather_bytes(encode_keys(mine)))]
     return engine.all_gather_object(list(new))
 
 
