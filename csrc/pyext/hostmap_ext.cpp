@@ -183,7 +183,8 @@ PyObject* stack_rows(PyObject*, PyObject* const* a, Py_ssize_t na) {
 // rank's block of proposed keys in rank order and give each key not in ``key2id`` yet the next id
 // (= len(id2key)), appending it to ``id2key``.  ONE dict operation per key (PyDict_SetDefault:
 // a single probe that inserts or finds) instead of the union dict + membership test + insert of
-// the Python form.  Blocks may be None.  Returns the number of new keys.
+// the Python form.  Blocks may be None.  Returns the number of new keys, or (number, new dict) when
+// it numbered a large first round into a presized dict the caller must use instead of key2id.
 PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
   if (na != 3 || !PyDict_CheckExact(a[0]) || !PyList_CheckExact(a[1])) {
     PyErr_SetString(PyExc_TypeError, "learn_keys(key2id: dict, id2key: list, proposals)");
@@ -192,6 +193,22 @@ PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
   PyObject* d = a[0];
   PyObject* ids = a[1];
   const Py_ssize_t base = PyList_GET_SIZE(ids);
+  // A large round into an EMPTY dictionary (a map collective's first call: ~1M keys) grows the
+  // dict through ~17 resizes that rehash every entry; presizing it to the proposals' total avoids
+  // them.  The caller then swaps the returned dict in (learn_keys returns (count, dict)).
+  PyObject* fresh = nullptr;
+  if (PyDict_GET_SIZE(d) == 0 && PyList_CheckExact(a[2])) {
+    Py_ssize_t total = 0;
+    for (Py_ssize_t b = 0; b < PyList_GET_SIZE(a[2]); ++b) {
+      PyObject* blk = PyList_GET_ITEM(a[2], b);
+      if (blk != Py_None && PyList_CheckExact(blk)) total += PyList_GET_SIZE(blk);
+    }
+    if (total > (1 << 16)) {
+      fresh = _PyDict_NewPresized(total);
+      if (!fresh) return nullptr;
+      d = fresh;
+    }
+  }
   Py_ssize_t next = base;
   PyObject* it = PyObject_GetIter(a[2]);
   if (!it) return nullptr;
@@ -228,7 +245,11 @@ PyObject* learn_keys(PyObject*, PyObject* const* a, Py_ssize_t na) {
     if (!ok) break;
   }
   Py_DECREF(it);
-  if (PyErr_Occurred()) return nullptr;
+  if (PyErr_Occurred()) {
+    Py_XDECREF(fresh);
+    return nullptr;
+  }
+  if (fresh) return Py_BuildValue("(nN)", next - base, fresh);
   return PyLong_FromSsize_t(next - base);
 }
 

@@ -73,7 +73,9 @@ class KeyDictionary:
         from ..ops import native
         ext = native.hostmap_ext()
         if ext is not None:       # one dict probe per key (csrc/pyext/hostmap_ext.cpp learn_keys)
-            ext.learn_keys(self.key2id, self.id2key, proposals)
+            got = ext.learn_keys(self.key2id, self.id2key, list(proposals))
+            if isinstance(got, tuple):        # a large first round went into a presized dict
+                self.key2id = got[1]
             return
         # C-level passes only (a first call numbers ~1M keys): order-preserving union of the
         # blocks, drop the known keys, number the rest in that order
