@@ -396,6 +396,13 @@ extern "C" int mp4x_ipc_set_spin(void* signal, double seconds, void* stream) {
   return (int)hipStreamSynchronize((hipStream_t)stream);
 }
 
+// Bump the device epoch counter of a graph-capturable instance (stream-ordered: the next IPC
+// kernel on `stream` reads the new epoch; see resolve_epoch).
+extern "C" int mp4x_ipc_bump_epoch(uint32_t* epoch_dev, void* stream) {
+  hipLaunchKernelGGL(k_ipc_bump_epoch, dim3(1), dim3(1), 0, (hipStream_t)stream, epoch_dev);
+  return (int)hipGetLastError();
+}
+
 // PCI bus id of the current device: ranks compare them to detect a GPU shared by several
 // ranks (single-GPU rehearsal), where the per-block barriers need every rank's blocks
 // co-resident and the block count must shrink accordingly.
