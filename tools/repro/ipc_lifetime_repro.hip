@@ -13,7 +13,8 @@
 //         zeros)?  Variants also keep the first import alive / keep fds open.
 //
 // Reads go through a kernel (the path of the zero-copy collectives) and through hipMemcpy.
-// Usage: ipc_lifetime_repro <ipc|vmm> <variant> [bytes]     (one JSON line per check)
+// Usage: ipc_lifetime_repro exporter <ipc|vmm> <variant> <name> [bytes] &
+//        ipc_lifetime_repro importer <ipc|vmm> <variant> <name> [bytes]   (one JSON line per check)
 // Build: hipcc --offload-arch=gfx950 -O2 -o ipc_lifetime_repro ipc_lifetime_repro.hip
 #include <hip/hip_runtime.h>
 
@@ -21,7 +22,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <cstddef>
 #include <sys/socket.h>
+#include <sys/un.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -288,29 +291,48 @@ static void vmm_importer(int s, size_t bytes, const std::string& v) {
   if (keep_import) vmm_free(a);
 }
 
+// Two independent processes (started by the caller, e.g. tools/gpu/r4_repro.sh), each
+// initialising its own HIP runtime as the ranks of a job do, meet on an abstract unix socket
+// (the same channel mp4x's memAlloc uses for its fds).  No fork / exec in this program.
+static int connect_pair(const std::string& name, bool server) {
+  int s = socket(AF_UNIX, SOCK_STREAM, 0);
+  if (s < 0) { perror("socket"); _exit(4); }
+  struct sockaddr_un a;
+  memset(&a, 0, sizeof(a));
+  a.sun_family = AF_UNIX;
+  const std::string path = "mp4x_repro_" + name;          // abstract namespace: leading NUL
+  memcpy(a.sun_path + 1, path.data(), path.size());
+  const socklen_t len = (socklen_t)(offsetof(struct sockaddr_un, sun_path) + 1 + path.size());
+  if (server) {
+    if (bind(s, (struct sockaddr*)&a, len) || listen(s, 1)) { perror("bind/listen"); _exit(4); }
+    int c = accept(s, nullptr, nullptr);
+    if (c < 0) { perror("accept"); _exit(4); }
+    close(s);
+    return c;
+  }
+  for (int i = 0; i < 200; ++i) {                          // the exporter may not listen yet
+    if (connect(s, (struct sockaddr*)&a, len) == 0) return s;
+    usleep(50000);
+  }
+  perror("connect");
+  _exit(4);
+}
+
 int main(int argc, char** argv) {
-  if (argc < 3) {
-    fprintf(stderr, "usage: %s <ipc|vmm> <variant> [bytes]\n", argv[0]);
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s <exporter|importer> <ipc|vmm> <variant> <socket name> [bytes]\n", argv[0]);
     return 2;
   }
-  const std::string mode = argv[1], v = argv[2];
-  const size_t bytes = argc > 3 ? strtoull(argv[3], nullptr, 10) : (8u << 20);
-  int sv[2];
-  if (socketpair(AF_UNIX, SOCK_STREAM, 0, sv)) { perror("socketpair"); return 4; }
-  // fork BEFORE any HIP call: each process initialises its own runtime
-  pid_t pid = fork();
-  if (pid == 0) {
-    close(sv[0]);
-    alarm(120);
-    if (mode == "ipc") ipc_importer(sv[1], bytes, v);
-    else vmm_importer(sv[1], bytes, v);
-    _exit(0);
-  }
-  close(sv[1]);
+  const std::string r = argv[1], mode = argv[2], v = argv[3];
+  const size_t bytes = argc > 5 ? strtoull(argv[5], nullptr, 10) : (8u << 20);
   alarm(120);
-  if (mode == "ipc") ipc_exporter(sv[0], bytes, v);
-  else vmm_exporter(sv[0], bytes, v);
-  int st = 0;
-  waitpid(pid, &st, 0);
-  return WIFEXITED(st) ? WEXITSTATUS(st) : 6;
+  const int s = connect_pair(argv[4], r == "exporter");
+  if (r == "exporter") {
+    if (mode == "ipc") ipc_exporter(s, bytes, v);
+    else vmm_exporter(s, bytes, v);
+  } else {
+    if (mode == "ipc") ipc_importer(s, bytes, v);
+    else vmm_importer(s, bytes, v);
+  }
+  return 0;
 }
