@@ -171,6 +171,17 @@ extern "C" int mp4x_vmm_free(void* va, size_t chunk, int n, const uint64_t* hand
   return teardown(va, chunk, n, handles, chunk * (size_t)n);
 }
 
+// Unmap + release the chunks but keep the VA range reserved (``mp4x_vmm_addr_free`` later): the
+// physical memory goes back to the device while no later reservation can land on these
+// addresses (MP4X_VMM_FRESH_VA, parallel/ipc.py mem_free).
+extern "C" int mp4x_vmm_release_keep_va(void* va, size_t chunk, int n, const uint64_t* handles) {
+  return teardown(va, chunk, n, handles, 0);
+}
+
+extern "C" int mp4x_vmm_addr_free(void* va, size_t bytes) {
+  return (int)hipMemAddressFree(va, bytes);
+}
+
 // System-scope release on every XCD: each workgroup's lane 0 issues a release fence at system
 // scope (L2 write-back of that XCD's dirty lines), with enough workgroups that every XCD runs
 // several of them.  Makes what earlier kernels wrote into coarse-grained memory visible to

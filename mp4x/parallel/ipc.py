@@ -89,10 +89,19 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 # CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' allocations (refcounted
 #   per allocation) and frees its push scratch, instead of caching every mapping and pooling every
 #   scratch until close();
-# VMM_RELEASE — memFree releases the VMM chunks collectively, every importer's mapping first and
-#   the owners' memory after a barrier, instead of parking the allocation in a per-size pool.
+# VMM_POLICY — what memFree does with a memAlloc allocation:
+#   "fresh_va": release the physical chunks collectively (every importer's mapping first, the
+#               owners' memory after a barrier) but keep every VA range reserved, so no later
+#               mapping of this process lands on recycled addresses (vmm.quarantine_va);
+#   "ordered":  the same release, VA ranges freed too;
+#   "pool":     park the allocation in a per-size pool that the next memAlloc of that size reuses
+#               (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
-VMM_RELEASE = os.environ.get("MP4X_VMM_RELEASE", "1") == "1"
+VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
+    "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "fresh_va")
+if VMM_POLICY not in ("fresh_va", "ordered", "pool"):
+    raise ValueError(f"MP4X_VMM_POLICY={VMM_POLICY!r}: expected fresh_va, ordered or pool")
+VMM_RELEASE = VMM_POLICY != "pool"
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64,
                     torch.int16, torch.int8, torch.uint8}
 _FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
@@ -676,9 +685,15 @@ class IpcAllreduce:
             self._close_peer(hk)
         reg.peer_keys = []
         for region in reversed(reg.vmm):     # the peers' imported views first, own memory last
-            region.free()
+            region.free(self._keep_va())
         reg.vmm = []
         reg.keep = None
+
+    @staticmethod
+    def _keep_va():
+        """The VA quarantine a released memAlloc range goes to (None: free the range)."""
+        from . import vmm
+        return vmm.va_quarantine() if VMM_POLICY == "fresh_va" else None
 
     def deregister(self, t: torch.Tensor) -> None:
         """Forget ``t``: once this rank's stream drained, its mappings of the peers' tensors and
@@ -836,12 +851,13 @@ class IpcAllreduce:
         # chunks in one local pass, so an owner could release its chunks while a peer still had
         # them imported and mapped; the next allocation's peer views then read zeros.  Here every
         # importer unmaps and releases first, and the owners release only after all have.
+        keep = self._keep_va()
         for region in reg.vmm[reg.nown:]:
-            region.free()
+            region.free(keep)
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # every peer released its imports
         for region in reg.vmm[:reg.nown]:
-            region.free()
+            region.free(keep)
         reg.vmm = []
         reg.keep = None
 
@@ -1637,7 +1653,7 @@ class IpcAllreduce:
         self._data = c_void_p()
         for region in reversed(getattr(self, "_data_regions", [])):   # imported views first
             try:
-                region.free()
+                region.free(self._keep_va())
             except Exception:   # noqa: BLE001 — best effort at teardown
                 pass
         self._data_regions = []

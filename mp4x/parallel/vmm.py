@@ -37,6 +37,8 @@ native.register_signatures({
     "mp4x_vmm_create": (c_int, [c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P, _INTP]),
     "mp4x_vmm_import": (c_int, [_INTP, c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P]),
     "mp4x_vmm_free": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
+    "mp4x_vmm_release_keep_va": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
+    "mp4x_vmm_addr_free": (c_int, [c_void_p, c_size_t]),
     "mp4x_release_all": (c_int, [c_void_p]),
 })
 
@@ -103,11 +105,53 @@ class VmmRegion:
                     pass
         self.fds = []
 
-    def free(self) -> None:
+    def free(self, keep_va: Optional[List] = None) -> None:
+        """Unmap + release the chunks and free the VA range — or, with ``keep_va`` (a list),
+        keep the range reserved and append ``(va, bytes)`` to it: the physical memory goes back
+        to the device but no later reservation of this process lands on these addresses
+        (:func:`free_ranges` releases them at communicator close)."""
         self.close_fds()
         if self.va:
-            check(self.lib.mp4x_vmm_free(c_void_p(self.va), self.chunk, self.n, self._handles), "vmm_free")
+            if keep_va is not None:
+                check(self.lib.mp4x_vmm_release_keep_va(c_void_p(self.va), self.chunk, self.n, self._handles),
+                      "vmm_release_keep_va")
+                if getattr(keep_va, "lib", 0) is None:
+                    keep_va.lib = self.lib
+                keep_va.append((self.va, self.nbytes))
+            else:
+                check(self.lib.mp4x_vmm_free(c_void_p(self.va), self.chunk, self.n, self._handles), "vmm_free")
             self.va = 0
+
+
+class _VaQuarantine(list):
+    """Process-wide list of VA ranges released with ``keep_va`` (they hold no physical memory).
+    Bounded by ``MP4X_VMM_VA_QUARANTINE`` bytes of address space (default 64 TiB, a small part
+    of the 48-bit GPU VA space): beyond it the oldest ranges are freed."""
+
+    def __init__(self):
+        super().__init__()
+        self.lib = None
+        self.cap = int(os.environ.get("MP4X_VMM_VA_QUARANTINE", 64 << 40))
+
+    def append(self, item) -> None:
+        super().append(item)
+        total = sum(b for _, b in self)
+        while len(self) > 1 and total > self.cap:
+            va, nb = self.pop(0)
+            total -= nb
+            if self.lib is not None:
+                self.lib.mp4x_vmm_addr_free(c_void_p(va), nb)
+
+
+_QUARANTINE = _VaQuarantine()
+
+
+def va_quarantine() -> _VaQuarantine:
+    return _QUARANTINE
+
+
+def quarantined_bytes() -> int:
+    return sum(b for _, b in _QUARANTINE)
 
 
 class _CudaArray:

@@ -4,6 +4,6 @@
 source "$(dirname "$0")/steps.sh"
 P=tools/repro/run_pair.sh
 for v in close_before_free close_after_free never_close; do step repro_ipc_$v 60 $P ipc $v; done
-for v in importer_first exporter_first keep_fds exporter_keeps importer_keeps concurrent; do step repro_vmm_$v 60 $P vmm $v; done
+for v in self_import importer_first fresh_va exporter_first keep_fds exporter_keeps importer_keeps concurrent; do step repro_vmm_$v 60 $P vmm $v; done
 cat gpurun_out/$OUT/repro_*.log | grep '^{' > gpurun_out/$OUT/repro.jsonl || true
 exit $STATUS

@@ -10,7 +10,9 @@
 //         the importer); importer imports, maps at its own VA, reads.  Then both release (order
 //         per variant: importer first, exporter first), the exporter creates a NEW chunk with
 //         pattern B and exports it; the importer imports and reads.  Does it see B (r3 saw
-//         zeros)?  Variants also keep the first import alive / keep fds open.
+//         zeros)?  Variants also keep the first import alive / keep fds open, keep the first VA
+//         ranges reserved so the second mapping lands at fresh addresses (fresh_va), or let the
+//         exporter import its own fd as a control (self_import).
 //
 // Reads go through a kernel (the path of the zero-copy collectives) and through hipMemcpy.
 // Usage: ipc_lifetime_repro exporter <ipc|vmm> <variant> <name> [bytes] &
@@ -208,6 +210,8 @@ struct Region {
   size_t bytes = 0;
 };
 
+static bool g_self_import = false;   // variant self_import: the exporter imports its own fd too
+
 static Region vmm_create(size_t bytes, uint32_t salt, int* fd) {
   Region r;
   r.bytes = bytes;
@@ -219,6 +223,16 @@ static Region vmm_create(size_t bytes, uint32_t salt, int* fd) {
   hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, 0, (uint32_t*)r.va, bytes / 4, salt);
   CK(hipDeviceSynchronize());
   CK(hipMemExportToShareableHandle(fd, r.h, hipMemHandleTypePosixFileDescriptor, 0));
+  if (!g_self_import) return r;
+  // control: can THIS process import its own fd?
+  hipMemGenericAllocationHandle_t hs{};
+  int dup_fd = *fd;
+  const hipError_t es = hipMemImportFromShareableHandle(&hs, (void*)&dup_fd, hipMemHandleTypePosixFileDescriptor);
+  printf("{\"mode\": \"vmm\", \"self_import\": \"%s\", \"fd\": %d, \"fd_size\": %lld}\n", hipGetErrorString(es),
+         *fd, (long long)lseek(*fd, 0, SEEK_END));
+  fflush(stdout);
+  lseek(*fd, 0, SEEK_SET);
+  if (es == hipSuccess) CK(hipMemRelease(hs));
   return r;
 }
 
@@ -226,23 +240,37 @@ static Region vmm_import(int fd, size_t bytes) {
   Region r;
   r.bytes = bytes;
   // HIP reads the fd THROUGH the handle pointer (tools/vmm_probe.py)
-  CK(hipMemImportFromShareableHandle(&r.h, (void*)&fd, hipMemHandleTypePosixFileDescriptor));
+  hipError_t e = hipMemImportFromShareableHandle(&r.h, (void*)&fd, hipMemHandleTypePosixFileDescriptor);
+  if (e != hipSuccess) {   // say what the fd is before giving up
+    char link[256] = {0}, path[64];
+    snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
+    ssize_t k = readlink(path, link, sizeof(link) - 1);
+    const off_t sz = fd >= 0 ? lseek(fd, 0, SEEK_END) : -1;
+    printf("{\"mode\": \"vmm\", \"import_error\": \"%s\", \"fd\": %d, \"fd_target\": \"%s\", \"fd_size\": %lld}\n",
+           hipGetErrorString(e), fd, k > 0 ? link : "?", (long long)sz);
+    fflush(stdout);
+    _exit(3);
+  }
   CK(hipMemAddressReserve(&r.va, bytes, 2u << 20, nullptr, 0));
   CK(hipMemMap(r.va, bytes, 0, r.h, 0));
   grant(r.va, bytes);
   return r;
 }
 
-static void vmm_free(Region& r) {
+// keep_va: unmap + release the physical chunk but keep the VA range reserved (freed at exit), so
+// the next reservation cannot land on the same addresses (variant fresh_va)
+static void vmm_free(Region& r, bool keep_va = false) {
   CK(hipDeviceSynchronize());
   CK(hipMemUnmap(r.va, r.bytes));
   CK(hipMemRelease(r.h));
-  CK(hipMemAddressFree(r.va, r.bytes));
-  r = Region();
+  if (!keep_va) CK(hipMemAddressFree(r.va, r.bytes));
+  r.h = hipMemGenericAllocationHandle_t{};
+  if (!keep_va) r = Region();
 }
 
 static void vmm_exporter(int s, size_t bytes, const std::string& v) {
   role = "exporter";
+  g_self_import = v == "self_import";
   CK(hipSetDevice(0));
   int fd1 = -1;
   Region a = vmm_create(bytes, 0xA0A0A0A0u, &fd1);
@@ -250,8 +278,8 @@ static void vmm_exporter(int s, size_t bytes, const std::string& v) {
   send_msg(s, z, 8, fd1);
   if (v != "keep_fds") close(fd1);
   sync_point(s, "read1");
-  if (v == "importer_first" || v == "keep_fds") sync_point(s, "imp_released");
-  if (v != "exporter_keeps") vmm_free(a);
+  if (v == "importer_first" || v == "keep_fds" || v == "fresh_va" || v == "self_import") sync_point(s, "imp_released");
+  if (v != "exporter_keeps") vmm_free(a, v == "fresh_va");
   if (v == "exporter_first") sync_point(s, "exp_released");
   int fd2 = -1;
   Region b = vmm_create(bytes, 0xB1B1B1B1u, &fd2);
@@ -261,13 +289,19 @@ static void vmm_exporter(int s, size_t bytes, const std::string& v) {
   send_msg(s, z, 8, fd2);
   if (v != "keep_fds") close(fd2);
   sync_point(s, "read2");
+  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"exporter_same_va\": %d}\n", v.c_str(), a.va == b.va);
+  fflush(stdout);
   vmm_free(b);
   if (v == "exporter_keeps") vmm_free(a);
+  if (v == "fresh_va") CK(hipMemAddressFree(a.va, a.bytes));
 }
 
 static void vmm_importer(int s, size_t bytes, const std::string& v) {
   role = "importer";
   CK(hipSetDevice(0));
+  void* warm = nullptr;                        // the runtime fully up before the first import
+  CK(hipMalloc(&warm, 4096));
+  CK(hipFree(warm));
   char z[8];
   int fd1 = recv_msg(s, z, 8);
   Region a = vmm_import(fd1, bytes);
@@ -275,20 +309,23 @@ static void vmm_importer(int s, size_t bytes, const std::string& v) {
   check_read(a.va, bytes / 4, 0xA0A0A0A0u, "first", v.c_str(), "vmm");
   sync_point(s, "read1");
   const bool keep_import = v == "importer_keeps";
-  if (!keep_import && v != "exporter_first") vmm_free(a);
-  if (v == "importer_first" || v == "keep_fds") sync_point(s, "imp_released");
+  void* const va1 = a.va;
+  if (!keep_import && v != "exporter_first") vmm_free(a, v == "fresh_va");
+  if (v == "importer_first" || v == "keep_fds" || v == "fresh_va" || v == "self_import") sync_point(s, "imp_released");
   if (v == "exporter_first") {
     sync_point(s, "exp_released");
     vmm_free(a);
   }
   int fd2 = recv_msg(s, z, 8);
   Region b = vmm_import(fd2, bytes);
-  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"importer_fd1\": %d, \"importer_fd2\": %d}\n", v.c_str(), fd1, fd2);
+  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"importer_fd1\": %d, \"importer_fd2\": %d, \"importer_same_va\": %d}\n",
+         v.c_str(), fd1, fd2, va1 == b.va);
   if (v != "keep_fds") close(fd2);
   check_read(b.va, bytes / 4, 0xB1B1B1B1u, "second", v.c_str(), "vmm");
   sync_point(s, "read2");
   vmm_free(b);
   if (keep_import) vmm_free(a);
+  if (v == "fresh_va") CK(hipMemAddressFree(a.va, a.bytes));
 }
 
 // Two independent processes (started by the caller, e.g. tools/gpu/r4_repro.sh), each

@@ -9,5 +9,9 @@ e=$!
 ri=$?
 wait $e
 re=$?
-[ $re -gt $ri ] && exit $re
-exit $ri
+r=$ri
+[ $re -gt $r ] && r=$re
+# the program's own failure codes (3 HIP error, 4 socket, 5 protocol) are an ordinary failed
+# check for the step runner; a signal / time limit (>= 124) stays abnormal
+[ $r -ge 3 ] && [ $r -le 5 ] && r=1
+exit $r
