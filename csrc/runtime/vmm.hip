@@ -40,6 +40,23 @@ hipMemAllocationProp make_prop(int dev) {
 // general is not).
 size_t va_alignment(size_t chunk) { return chunk % (2u << 20) == 0 ? (2u << 20) : 0; }
 
+// Address hint mode (MP4X_VMM_POLICY=hint, an A/B of the memFree lifetime study): every new
+// reservation asks for the address above the highest range reserved so far, so a range freed
+// earlier is never handed out again while its physical memory does go back to the device.
+bool g_hint_on = false;
+uintptr_t g_cursor = 0;
+
+hipError_t reserve(void** va, size_t total, size_t align) {
+  void* want = (g_hint_on && g_cursor) ? reinterpret_cast<void*>(g_cursor) : nullptr;
+  hipError_t e = hipMemAddressReserve(va, total, align, want, 0);
+  if (e == hipSuccess && g_hint_on) {
+    const uintptr_t end = reinterpret_cast<uintptr_t>(*va) + total + (4u << 20);   // a 4 MiB gap
+    const uintptr_t next = (end + (2u << 20) - 1) & ~(uintptr_t)((2u << 20) - 1);
+    if (next > g_cursor) g_cursor = next;
+  }
+  return e;
+}
+
 hipError_t grant(void* va, size_t bytes, int dev) {
   hipMemAccessDesc acc;
   std::memset(&acc, 0, sizeof(acc));
@@ -94,7 +111,7 @@ extern "C" int mp4x_vmm_create(size_t chunk, int n, void** va_out, uint64_t* han
     if (fds) fds[i] = -1;
   }
   void* va = nullptr;
-  e = hipMemAddressReserve(&va, total, va_alignment(chunk), nullptr, 0);
+  e = reserve(&va, total, va_alignment(chunk));
   if (e != hipSuccess) return (int)e;
   hipMemAllocationProp prop = make_prop(dev);
   int mapped = 0;
@@ -139,7 +156,7 @@ extern "C" int mp4x_vmm_import(const int* fds, size_t chunk, int n, void** va_ou
   const size_t total = chunk * (size_t)n;
   for (int i = 0; i < n; ++i) handles[i] = 0;
   void* va = nullptr;
-  e = hipMemAddressReserve(&va, total, va_alignment(chunk), nullptr, 0);
+  e = reserve(&va, total, va_alignment(chunk));
   if (e != hipSuccess) return (int)e;
   int mapped = 0;
   for (int i = 0; i < n && e == hipSuccess; ++i) {
@@ -180,6 +197,12 @@ extern "C" int mp4x_vmm_release_keep_va(void* va, size_t chunk, int n, const uin
 
 extern "C" int mp4x_vmm_addr_free(void* va, size_t bytes) {
   return (int)hipMemAddressFree(va, bytes);
+}
+
+// Turn the address hint mode on / off; returns the cursor (the next hinted address, 0 = none yet).
+extern "C" uint64_t mp4x_vmm_va_hint(int on) {
+  g_hint_on = on != 0;
+  return (uint64_t)g_cursor;
 }
 
 // System-scope release on every XCD: each workgroup's lane 0 issues a release fence at system

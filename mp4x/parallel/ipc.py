@@ -89,18 +89,23 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 # CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' allocations (refcounted
 #   per allocation) and frees its push scratch, instead of caching every mapping and pooling every
 #   scratch until close();
-# VMM_POLICY — what memFree does with a memAlloc allocation:
-#   "fresh_va": release the physical chunks collectively (every importer's mapping first, the
-#               owners' memory after a barrier) but keep every VA range reserved, so no later
-#               mapping of this process lands on recycled addresses (vmm.quarantine_va);
-#   "ordered":  the same release, VA ranges freed too;
-#   "pool":     park the allocation in a per-size pool that the next memAlloc of that size reuses
-#               (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
+# VMM_POLICY — what memFree does with a memAlloc allocation (tests/test_vmm_policy_gpu.py measures
+#   every one for exactness and device-memory growth):
+#   "fresh_va":       release the physical chunks collectively (every importer's mapping first, the
+#                     owners' memory after a barrier) but keep every VA range reserved, so no later
+#                     mapping of this process lands on recycled addresses (vmm.va_quarantine);
+#   "ordered":        the same release, VA ranges freed too;
+#   "hint":           "ordered", and every new reservation asks for an address above every range
+#                     reserved before (csrc/runtime/vmm.hip reserve());
+#   "keep_owner_va" / "keep_import_va": only the owner's / only the importers' ranges kept;
+#   "pool":           park the allocation in a per-size pool that the next memAlloc of that size
+#                     reuses (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
+VMM_POLICIES = ("fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
 VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
     "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "fresh_va")
-if VMM_POLICY not in ("fresh_va", "ordered", "pool"):
-    raise ValueError(f"MP4X_VMM_POLICY={VMM_POLICY!r}: expected fresh_va, ordered or pool")
+if VMM_POLICY not in VMM_POLICIES:
+    raise ValueError(f"MP4X_VMM_POLICY={VMM_POLICY!r}: expected one of {VMM_POLICIES}")
 VMM_RELEASE = VMM_POLICY != "pool"
 SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int32, torch.int64,
                     torch.int16, torch.int8, torch.uint8}
@@ -197,6 +202,8 @@ class IpcAllreduce:
         local_err = None
         try:
             self.lib = native.hip()
+            if VMM_POLICY == "hint":
+                self.lib.mp4x_vmm_va_hint(1)
             self.device = torch.cuda.current_device()
             hs = self.lib.mp4x_ipc_handle_size()
         except Exception as e:   # noqa: BLE001
@@ -684,16 +691,18 @@ class IpcAllreduce:
         for hk in reg.peer_keys:
             self._close_peer(hk)
         reg.peer_keys = []
-        for region in reversed(reg.vmm):     # the peers' imported views first, own memory last
-            region.free(self._keep_va())
+        for i in reversed(range(len(reg.vmm))):   # the peers' imported views first, own memory last
+            reg.vmm[i].free(self._keep_va(own=i < reg.nown))
         reg.vmm = []
         reg.keep = None
 
     @staticmethod
-    def _keep_va():
-        """The VA quarantine a released memAlloc range goes to (None: free the range)."""
+    def _keep_va(own: bool = True):
+        """The VA quarantine a released memAlloc range (this rank's own, or an imported peer
+        view) goes to under :data:`VMM_POLICY` (None: free the range)."""
         from . import vmm
-        return vmm.va_quarantine() if VMM_POLICY == "fresh_va" else None
+        keep = VMM_POLICY == "fresh_va" or VMM_POLICY == ("keep_owner_va" if own else "keep_import_va")
+        return vmm.va_quarantine() if keep else None
 
     def deregister(self, t: torch.Tensor) -> None:
         """Forget ``t``: once this rank's stream drained, its mappings of the peers' tensors and
@@ -851,13 +860,12 @@ class IpcAllreduce:
         # chunks in one local pass, so an owner could release its chunks while a peer still had
         # them imported and mapped; the next allocation's peer views then read zeros.  Here every
         # importer unmaps and releases first, and the owners release only after all have.
-        keep = self._keep_va()
         for region in reg.vmm[reg.nown:]:
-            region.free(keep)
+            region.free(self._keep_va(own=False))
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # every peer released its imports
         for region in reg.vmm[:reg.nown]:
-            region.free(keep)
+            region.free(self._keep_va(own=True))
         reg.vmm = []
         reg.keep = None
 

@@ -39,6 +39,7 @@ native.register_signatures({
     "mp4x_vmm_free": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
     "mp4x_vmm_release_keep_va": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
     "mp4x_vmm_addr_free": (c_int, [c_void_p, c_size_t]),
+    "mp4x_vmm_va_hint": (ctypes.c_uint64, [c_int]),
     "mp4x_release_all": (c_int, [c_void_p]),
 })
 

@@ -47,12 +47,14 @@ def _alloc_allreduce_fn(comm, n, reps):
     ok2 = (int(wrong.numel()), [(int(j), float(t2[j]), float(exp2[j])) for j in wrong[:4].tolist()])
     ptr2 = t2.data_ptr()
     comm.memFree(t2)
-    # same size again: the pooled allocation comes back (every rank alike), still exact
+    # same size again: exact (the pooled allocation itself under MP4X_VMM_POLICY=pool)
     t3 = comm.memAlloc(1 << 20, torch.float32)
     t3.copy_(i2 + r)
     comm.allreduceArray(t3, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, 1 << 20)
     torch.cuda.synchronize()
-    ok3 = (t3.data_ptr() == ptr2, int((t3 != exp2).sum()))
+    from mp4x.parallel import ipc as ipc_mod
+    # under the pool policy the same allocation comes back; otherwise any address will do
+    ok3 = (t3.data_ptr() == ptr2 or ipc_mod.VMM_POLICY != "pool", int((t3 != exp2).sum()))
     comm.memFree(t3)
     return bad, used, info, ok2 + ok3
 

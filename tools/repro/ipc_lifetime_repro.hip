@@ -6,13 +6,12 @@
 //         (usually at the recycled address), writes pattern B, exports again; importer opens the
 //         new handle and reads.  Does it see B?  Variants: importer closes before / after the
 //         exporter frees; importer does not close at all (the mp4x workaround).
-//   vmm : exporter hipMemCreate's a chunk, maps it, writes A, exports a dmabuf fd (SCM_RIGHTS to
-//         the importer); importer imports, maps at its own VA, reads.  Then both release (order
-//         per variant: importer first, exporter first), the exporter creates a NEW chunk with
-//         pattern B and exports it; the importer imports and reads.  Does it see B (r3 saw
-//         zeros)?  Variants also keep the first import alive / keep fds open, keep the first VA
-//         ranges reserved so the second mapping lands at fresh addresses (fresh_va), or let the
-//         exporter import its own fd as a control (self_import).
+//   vmm : REPRO_CYCLES (6) cycles; in cycle k the exporter hipMemCreate's a NEW chunk of
+//         bytes + k * 2 MiB, maps it, writes pattern k, exports a dmabuf fd (SCM_RIGHTS to the
+//         importer); the importer imports it, maps it at its own VA and reads it; then both
+//         release it (order / which side keeps its VA range reserved: see policy_of).  Does
+//         every cycle read its own pattern (r3 / r4 saw later allocations read wrong memory), and
+//         does device memory stay bounded (hipMemGetInfo after every cycle)?
 //
 // Reads go through a kernel (the path of the zero-copy collectives) and through hipMemcpy.
 // Usage: ipc_lifetime_repro exporter <ipc|vmm> <variant> <name> [bytes] &
@@ -25,6 +24,7 @@
 #include <cstring>
 #include <string>
 #include <cstddef>
+#include <vector>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <sys/wait.h>
@@ -210,8 +210,17 @@ struct Region {
   size_t bytes = 0;
 };
 
-static bool g_self_import = false;   // variant self_import: the exporter imports its own fd too
+// How the POSIX fd reaches hipMemImportFromShareableHandle: through a pointer to it (what the
+// runtime PyTorch-ROCm ships reads — tools/vmm_probe.py) or as the value itself
+// (REPRO_FD_BY_VALUE=1, the CUDA convention).
+static hipError_t import_fd(hipMemGenericAllocationHandle_t* h, int fd) {
+  static const bool by_value = getenv("REPRO_FD_BY_VALUE") && atoi(getenv("REPRO_FD_BY_VALUE"));
+  if (by_value) return hipMemImportFromShareableHandle(h, (void*)(intptr_t)fd, hipMemHandleTypePosixFileDescriptor);
+  int v = fd;
+  return hipMemImportFromShareableHandle(h, (void*)&v, hipMemHandleTypePosixFileDescriptor);
+}
 
+// Same call order as csrc/runtime/vmm.hip: reserve, create, map, export, then grant access.
 static Region vmm_create(size_t bytes, uint32_t salt, int* fd) {
   Region r;
   r.bytes = bytes;
@@ -219,113 +228,128 @@ static Region vmm_create(size_t bytes, uint32_t salt, int* fd) {
   CK(hipMemAddressReserve(&r.va, bytes, 2u << 20, nullptr, 0));
   CK(hipMemCreate(&r.h, bytes, &prop, 0));
   CK(hipMemMap(r.va, bytes, 0, r.h, 0));
+  CK(hipMemExportToShareableHandle(fd, r.h, hipMemHandleTypePosixFileDescriptor, 0));
   grant(r.va, bytes);
   hipLaunchKernelGGL(k_fill, dim3(256), dim3(256), 0, 0, (uint32_t*)r.va, bytes / 4, salt);
   CK(hipDeviceSynchronize());
-  CK(hipMemExportToShareableHandle(fd, r.h, hipMemHandleTypePosixFileDescriptor, 0));
-  if (!g_self_import) return r;
-  // control: can THIS process import its own fd?
-  hipMemGenericAllocationHandle_t hs{};
-  int dup_fd = *fd;
-  const hipError_t es = hipMemImportFromShareableHandle(&hs, (void*)&dup_fd, hipMemHandleTypePosixFileDescriptor);
-  printf("{\"mode\": \"vmm\", \"self_import\": \"%s\", \"fd\": %d, \"fd_size\": %lld}\n", hipGetErrorString(es),
-         *fd, (long long)lseek(*fd, 0, SEEK_END));
-  fflush(stdout);
-  lseek(*fd, 0, SEEK_SET);
-  if (es == hipSuccess) CK(hipMemRelease(hs));
   return r;
 }
 
 static Region vmm_import(int fd, size_t bytes) {
   Region r;
   r.bytes = bytes;
-  // HIP reads the fd THROUGH the handle pointer (tools/vmm_probe.py)
-  hipError_t e = hipMemImportFromShareableHandle(&r.h, (void*)&fd, hipMemHandleTypePosixFileDescriptor);
+  CK(hipMemAddressReserve(&r.va, bytes, 2u << 20, nullptr, 0));
+  hipError_t e = import_fd(&r.h, fd);
   if (e != hipSuccess) {   // say what the fd is before giving up
     char link[256] = {0}, path[64];
     snprintf(path, sizeof(path), "/proc/self/fd/%d", fd);
     ssize_t k = readlink(path, link, sizeof(link) - 1);
     const off_t sz = fd >= 0 ? lseek(fd, 0, SEEK_END) : -1;
-    printf("{\"mode\": \"vmm\", \"import_error\": \"%s\", \"fd\": %d, \"fd_target\": \"%s\", \"fd_size\": %lld}\n",
-           hipGetErrorString(e), fd, k > 0 ? link : "?", (long long)sz);
+    int rt = 0;
+    (void)hipRuntimeGetVersion(&rt);
+    printf("{\"mode\": \"vmm\", \"import_error\": \"%s\", \"fd\": %d, \"fd_target\": \"%s\", \"fd_size\": %lld, "
+           "\"hip_runtime\": %d}\n", hipGetErrorString(e), fd, k > 0 ? link : "?", (long long)sz, rt);
     fflush(stdout);
     _exit(3);
   }
-  CK(hipMemAddressReserve(&r.va, bytes, 2u << 20, nullptr, 0));
   CK(hipMemMap(r.va, bytes, 0, r.h, 0));
   grant(r.va, bytes);
   return r;
 }
 
 // keep_va: unmap + release the physical chunk but keep the VA range reserved (freed at exit), so
-// the next reservation cannot land on the same addresses (variant fresh_va)
-static void vmm_free(Region& r, bool keep_va = false) {
+// the next reservation cannot land on the same addresses
+static void vmm_free(Region& r, bool keep_va, std::vector<Region>& kept) {
   CK(hipDeviceSynchronize());
   CK(hipMemUnmap(r.va, r.bytes));
   CK(hipMemRelease(r.h));
-  if (!keep_va) CK(hipMemAddressFree(r.va, r.bytes));
-  r.h = hipMemGenericAllocationHandle_t{};
-  if (!keep_va) r = Region();
+  if (keep_va) kept.push_back(r);
+  else CK(hipMemAddressFree(r.va, r.bytes));
+  r = Region();
 }
 
+static size_t used_bytes() {
+  size_t fr = 0, tot = 0;
+  CK(hipMemGetInfo(&fr, &tot));
+  return tot - fr;
+}
+
+// Variants (which side keeps its VA ranges reserved after releasing; who releases first):
+//   ordered        importer releases first, then the owner; every VA range freed
+//   exporter_first the owner releases first, then the importer; every VA range freed
+//   fresh_va       importer first; both sides keep their VA ranges
+//   keep_owner_va  importer first; only the owner keeps its ranges
+//   keep_import_va importer first; only the importer keeps its ranges
+struct Policy {
+  bool exporter_first, keep_own, keep_imp;
+};
+
+static Policy policy_of(const std::string& v) {
+  if (v == "ordered") return {false, false, false};
+  if (v == "exporter_first") return {true, false, false};
+  if (v == "fresh_va") return {false, true, true};
+  if (v == "keep_owner_va") return {false, true, false};
+  if (v == "keep_import_va") return {false, false, true};
+  fprintf(stderr, "unknown vmm variant %s\n", v.c_str());
+  _exit(2);
+}
+
+static int cycles() { return getenv("REPRO_CYCLES") ? atoi(getenv("REPRO_CYCLES")) : 6; }
+
+// cycle k: a NEW allocation of bytes + k * 2 MiB (every size distinct) with pattern salt k
 static void vmm_exporter(int s, size_t bytes, const std::string& v) {
   role = "exporter";
-  g_self_import = v == "self_import";
+  const Policy pol = policy_of(v);
   CK(hipSetDevice(0));
-  int fd1 = -1;
-  Region a = vmm_create(bytes, 0xA0A0A0A0u, &fd1);
-  char z[8] = {0};
-  send_msg(s, z, 8, fd1);
-  if (v != "keep_fds") close(fd1);
-  sync_point(s, "read1");
-  if (v == "importer_first" || v == "keep_fds" || v == "fresh_va" || v == "self_import") sync_point(s, "imp_released");
-  if (v != "exporter_keeps") vmm_free(a, v == "fresh_va");
-  if (v == "exporter_first") sync_point(s, "exp_released");
-  int fd2 = -1;
-  Region b = vmm_create(bytes, 0xB1B1B1B1u, &fd2);
-  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"fd1\": %d, \"fd2\": %d, \"same_handle\": %d}\n", v.c_str(), fd1, fd2,
-         (void*)a.h == (void*)b.h);
-  fflush(stdout);
-  send_msg(s, z, 8, fd2);
-  if (v != "keep_fds") close(fd2);
-  sync_point(s, "read2");
-  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"exporter_same_va\": %d}\n", v.c_str(), a.va == b.va);
-  fflush(stdout);
-  vmm_free(b);
-  if (v == "exporter_keeps") vmm_free(a);
-  if (v == "fresh_va") CK(hipMemAddressFree(a.va, a.bytes));
+  std::vector<Region> kept;
+  void* prev = nullptr;
+  const size_t used0 = used_bytes();
+  for (int k = 0; k < cycles(); ++k) {
+    const size_t nb = bytes + (size_t)k * (2u << 20);
+    int fd = -1;
+    Region a = vmm_create(nb, 0xA0A0A0A0u + (uint32_t)k, &fd);
+    const bool same_va = a.va == prev;
+    prev = a.va;
+    uint64_t msg = nb;
+    send_msg(s, &msg, 8, fd);
+    close(fd);
+    sync_point(s, "read");
+    if (!pol.exporter_first) sync_point(s, "imp_released");
+    vmm_free(a, pol.keep_own, kept);
+    if (pol.exporter_first) sync_point(s, "exp_released");
+    sync_point(s, "cycle");
+    printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"cycle\": %d, \"exporter_same_va_as_prev\": %d, "
+           "\"device_used_growth_mb\": %.1f}\n", v.c_str(), k, (int)same_va, (double)((long long)used_bytes() - (long long)used0) / (1 << 20));
+    fflush(stdout);
+  }
+  for (auto& r : kept) CK(hipMemAddressFree(r.va, r.bytes));
 }
 
 static void vmm_importer(int s, size_t bytes, const std::string& v) {
   role = "importer";
+  const Policy pol = policy_of(v);
   CK(hipSetDevice(0));
-  void* warm = nullptr;                        // the runtime fully up before the first import
-  CK(hipMalloc(&warm, 4096));
-  CK(hipFree(warm));
-  char z[8];
-  int fd1 = recv_msg(s, z, 8);
-  Region a = vmm_import(fd1, bytes);
-  if (v != "keep_fds") close(fd1);
-  check_read(a.va, bytes / 4, 0xA0A0A0A0u, "first", v.c_str(), "vmm");
-  sync_point(s, "read1");
-  const bool keep_import = v == "importer_keeps";
-  void* const va1 = a.va;
-  if (!keep_import && v != "exporter_first") vmm_free(a, v == "fresh_va");
-  if (v == "importer_first" || v == "keep_fds" || v == "fresh_va" || v == "self_import") sync_point(s, "imp_released");
-  if (v == "exporter_first") {
-    sync_point(s, "exp_released");
-    vmm_free(a);
+  std::vector<Region> kept;
+  void* prev = nullptr;
+  for (int k = 0; k < cycles(); ++k) {
+    uint64_t nb = 0;
+    const int fd = recv_msg(s, &nb, 8);
+    Region a = vmm_import(fd, nb);
+    close(fd);
+    const bool same_va = a.va == prev;
+    prev = a.va;
+    printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"cycle\": %d, \"importer_same_va_as_prev\": %d}\n", v.c_str(), k,
+           (int)same_va);
+    char what[32];
+    snprintf(what, sizeof(what), "cycle%d", k);
+    check_read(a.va, nb / 4, 0xA0A0A0A0u + (uint32_t)k, what, v.c_str(), "vmm");
+    sync_point(s, "read");
+    if (pol.exporter_first) sync_point(s, "exp_released");
+    vmm_free(a, pol.keep_imp, kept);
+    if (!pol.exporter_first) sync_point(s, "imp_released");
+    sync_point(s, "cycle");
   }
-  int fd2 = recv_msg(s, z, 8);
-  Region b = vmm_import(fd2, bytes);
-  printf("{\"mode\": \"vmm\", \"variant\": \"%s\", \"importer_fd1\": %d, \"importer_fd2\": %d, \"importer_same_va\": %d}\n",
-         v.c_str(), fd1, fd2, va1 == b.va);
-  if (v != "keep_fds") close(fd2);
-  check_read(b.va, bytes / 4, 0xB1B1B1B1u, "second", v.c_str(), "vmm");
-  sync_point(s, "read2");
-  vmm_free(b);
-  if (keep_import) vmm_free(a);
-  if (v == "fresh_va") CK(hipMemAddressFree(a.va, a.bytes));
+  for (auto& r : kept) CK(hipMemAddressFree(r.va, r.bytes));
 }
 
 // Two independent processes (started by the caller, e.g. tools/gpu/r4_repro.sh), each
@@ -355,7 +379,14 @@ static int connect_pair(const std::string& name, bool server) {
   _exit(4);
 }
 
+// REPRO_AS_LIBRARY: built as a shared object whose entry point a tiny launcher calls after it
+// dlopen()ed the HIP runtime PyTorch ships (tools/repro/launcher.cpp) — the runtime instance every
+// mp4x rank runs on — instead of the /opt/rocm one a plain executable binds.
+#ifdef REPRO_AS_LIBRARY
+extern "C" int repro_main(int argc, char** argv) {
+#else
 int main(int argc, char** argv) {
+#endif
   if (argc < 5) {
     fprintf(stderr, "usage: %s <exporter|importer> <ipc|vmm> <variant> <socket name> [bytes]\n", argv[0]);
     return 2;

@@ -1,7 +1,8 @@
 #!/bin/bash
-# run_pair.sh <ipc|vmm> <variant> [bytes]: the exporter and the importer of
-# ipc_lifetime_repro as two independent processes; both outputs on stdout; rc = worst of both.
-B="$(dirname "$0")/ipc_lifetime_repro"
+# run_pair.sh <ipc|vmm> <variant> [bytes]: the exporter and the importer of ipc_lifetime_repro as
+# two independent processes; both outputs on stdout; rc = worst of both.  REPRO_BIN picks the build
+# (default: the one linked against PyTorch's HIP runtime, tools/repro/build.sh).
+B="${REPRO_BIN:-$(dirname "$0")/ipc_lifetime_repro}"
 name="$1_$2_$$"
 "$B" exporter "$1" "$2" "$name" "${3:-8388608}" &
 e=$!
