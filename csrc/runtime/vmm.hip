@@ -199,6 +199,99 @@ extern "C" int mp4x_vmm_addr_free(void* va, size_t bytes) {
   return (int)hipMemAddressFree(va, bytes);
 }
 
+// ---------------------------------------------------------------- chunk pool (memAlloc default)
+// On the HIP runtime PyTorch-ROCm ships, (a) hipMemRelease of an exported chunk never gives the
+// memory back to the device, and (b) once a process has called hipMemAddressFree on a range it
+// had mapped, the chunks it exports LATER read as other memory in the importers — shown with
+// plain HIP in tools/repro/ipc_lifetime_repro.hip (profiles/r4/lifetime/).  So memAlloc keeps
+// physical chunks for reuse (parallel/vmm.py ChunkPool) and never frees a VA range: an allocation
+// maps pooled chunks into a fresh range, memFree only unmaps.
+
+// One physical chunk of ``bytes`` (granularity multiple); ``fd`` (nullable) gets its dmabuf fd.
+extern "C" int mp4x_vmm_chunk_create(size_t bytes, uint64_t* handle, int* fd) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  hipMemAllocationProp prop = make_prop(dev);
+  hipMemGenericAllocationHandle_t h;
+  e = hipMemCreate(&h, bytes, &prop, 0);
+  if (e != hipSuccess) return (int)e;
+  if (fd) {
+    *fd = -1;
+    e = hipMemExportToShareableHandle(fd, h, hipMemHandleTypePosixFileDescriptor, 0);
+    if (e != hipSuccess) {
+      hipMemRelease(h);
+      return (int)e;
+    }
+  }
+  *handle = (uint64_t)(uintptr_t)h;
+  return 0;
+}
+
+// A peer's chunk from its dmabuf fd (the fd stays the caller's).
+extern "C" int mp4x_vmm_chunk_import(int fd, uint64_t* handle) {
+  hipMemGenericAllocationHandle_t h;
+  int v = fd;     // read THROUGH the pointer by this runtime (see mp4x_vmm_import)
+  hipError_t e = hipMemImportFromShareableHandle(&h, static_cast<void*>(&v), hipMemHandleTypePosixFileDescriptor);
+  if (e != hipSuccess) return (int)e;
+  *handle = (uint64_t)(uintptr_t)h;
+  return 0;
+}
+
+extern "C" int mp4x_vmm_chunk_release(uint64_t handle) {
+  return (int)hipMemRelease((hipMemGenericAllocationHandle_t)(uintptr_t)handle);
+}
+
+// Reserve a fresh range of sum(sizes) bytes and map ``n`` chunks back to back, read/write for the
+// current device.  On failure the chunks mapped so far are unmapped and the range is left
+// reserved (never freed, see above); *va_out gets it either way (0 if the reservation failed).
+extern "C" int mp4x_vmm_map_chunks(const uint64_t* handles, const size_t* sizes, int n, void** va_out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  size_t total = 0;
+  bool big = true;
+  for (int i = 0; i < n; ++i) {
+    total += sizes[i];
+    big = big && sizes[i] % (2u << 20) == 0;
+  }
+  void* va = nullptr;
+  *va_out = nullptr;
+  e = reserve(&va, total, big ? (2u << 20) : 0);
+  if (e != hipSuccess) return (int)e;
+  *va_out = va;
+  size_t off = 0;
+  int mapped = 0;
+  for (int i = 0; i < n && e == hipSuccess; ++i) {
+    e = hipMemMap(static_cast<char*>(va) + off, sizes[i], 0, (hipMemGenericAllocationHandle_t)(uintptr_t)handles[i], 0);
+    if (e == hipSuccess) {
+      off += sizes[i];
+      mapped = i + 1;
+    }
+  }
+  if (e == hipSuccess) e = grant(va, total, dev);
+  if (e != hipSuccess) {
+    off = 0;
+    for (int i = 0; i < mapped; ++i) {
+      hipMemUnmap(static_cast<char*>(va) + off, sizes[i]);
+      off += sizes[i];
+    }
+  }
+  return (int)e;
+}
+
+// Unmap ``n`` chunks mapped back to back at ``va`` (the range stays reserved, the chunks alive).
+extern "C" int mp4x_vmm_unmap_chunks(void* va, const size_t* sizes, int n) {
+  int first = 0;
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    hipError_t e = hipMemUnmap(static_cast<char*>(va) + off, sizes[i]);
+    if (e != hipSuccess && !first) first = (int)e;
+    off += sizes[i];
+  }
+  return first;
+}
+
 // Turn the address hint mode on / off; returns the cursor (the next hinted address, 0 = none yet).
 extern "C" uint64_t mp4x_vmm_va_hint(int on) {
   g_hint_on = on != 0;

@@ -89,8 +89,13 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 # CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' allocations (refcounted
 #   per allocation) and frees its push scratch, instead of caching every mapping and pooling every
 #   scratch until close();
-# VMM_POLICY — what memFree does with a memAlloc allocation (tests/test_vmm_policy_gpu.py measures
-#   every one for exactness and device-memory growth):
+# VMM_POLICY — how memAlloc / memFree manage memory (tests/test_vmm_policy_gpu.py measures every
+#   one for exactness and device-memory growth; tools/repro/ipc_lifetime_repro.hip shows, in plain
+#   HIP, why only the first and "fresh_va" / "pool" are exact on this runtime):
+#   "chunks":         (default) physical chunks of power-of-two sizes from a per-rank pool
+#                     (vmm.ChunkPool) mapped at a fresh VA range per allocation; memFree unmaps
+#                     and returns the chunks to the pool (reused by allocations of any size, no
+#                     fd exchange for a reused chunk); nothing released or VA-freed before close;
 #   "fresh_va":       release the physical chunks collectively (every importer's mapping first, the
 #                     owners' memory after a barrier) but keep every VA range reserved, so no later
 #                     mapping of this process lands on recycled addresses (vmm.va_quarantine);
@@ -101,9 +106,9 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 #   "pool":           park the allocation in a per-size pool that the next memAlloc of that size
 #                     reuses (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
-VMM_POLICIES = ("fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
+VMM_POLICIES = ("chunks", "fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
 VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
-    "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "fresh_va")
+    "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "chunks")
 if VMM_POLICY not in VMM_POLICIES:
     raise ValueError(f"MP4X_VMM_POLICY={VMM_POLICY!r}: expected one of {VMM_POLICIES}")
 VMM_RELEASE = VMM_POLICY != "pool"
@@ -169,7 +174,7 @@ def _agree(comm, rank, obj, is_bad):
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "chunks")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
@@ -179,6 +184,7 @@ class _Reg:
         self.vmm: list = []              # memAlloc: own regions first (nown of them), then imported
         self.nown = 0
         self.peer_keys: list = []        # (rank, handle bytes) of every peer mapping this one uses
+        self.chunks = None               # memAlloc under the chunk pool: this rank's chunks
 
 
 class IpcAllreduce:
@@ -330,6 +336,7 @@ class IpcAllreduce:
         self._scratch_pool = {}     # push-scratch bytes -> [(allocation, handle)] free for reuse
         self._scratch_size = {}     # push-scratch address -> bytes
         self._vmm_pool = {}         # memAlloc size -> [freed registrations] (see mem_free)
+        self._chunk_pool = None     # memAlloc chunk pool (VMM_POLICY "chunks", vmm.ChunkPool)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
 
@@ -695,13 +702,17 @@ class IpcAllreduce:
             reg.vmm[i].free(self._keep_va(own=i < reg.nown))
         reg.vmm = []
         reg.keep = None
+        if reg.chunks is not None and self._chunk_pool is not None:
+            self._chunk_pool.give(reg.chunks)
+            reg.chunks = []
 
     @staticmethod
     def _keep_va(own: bool = True):
         """The VA quarantine a released memAlloc range (this rank's own, or an imported peer
         view) goes to under :data:`VMM_POLICY` (None: free the range)."""
         from . import vmm
-        keep = VMM_POLICY == "fresh_va" or VMM_POLICY == ("keep_owner_va" if own else "keep_import_va")
+        keep = VMM_POLICY in ("chunks", "pool", "fresh_va") or \
+            VMM_POLICY == ("keep_owner_va" if own else "keep_import_va")
         return vmm.va_quarantine() if keep else None
 
     def deregister(self, t: torch.Tensor) -> None:
@@ -760,6 +771,8 @@ class IpcAllreduce:
         from . import vmm
         nb16 = -(-int(nbytes) // 16) * 16
         es = torch.empty((), dtype=dtype).element_size()
+        if VMM_POLICY == "chunks":
+            return self._mem_alloc_chunks(nbytes, nb16, es, dtype)
         pooled = self._vmm_pool.get(nb16) if not VMM_RELEASE else None
         if pooled:
             # a freed allocation of this size (the same one on every rank: pool states agree)
@@ -838,6 +851,87 @@ class IpcAllreduce:
         self._regs[(own.va, nb16)] = reg
         return t[:nbytes // es * es].view(dtype)
 
+    def _mem_alloc_chunks(self, nbytes: int, nb16: int, es: int, dtype: torch.dtype) -> torch.Tensor:
+        """memAlloc under the chunk pool (``VMM_POLICY == "chunks"``): this rank takes chunks from
+        its pool (new ones only when none of a size is free), maps them at a fresh VA range, and
+        tells every peer which chunk ids the tensor (and its push scratch) is made of; only NEW
+        chunks' fds travel, a reused chunk is mapped again from the handle each peer kept."""
+        from . import vmm
+        pool = self._chunk_pool
+        if pool is None:
+            pool = self._chunk_pool = vmm.ChunkPool(self.lib)
+        own_c, scr_c, maps = [], [], []
+        err = plan = None
+        try:
+            g = ctypes.c_size_t()
+            check(self.lib.mp4x_vmm_granularity(ctypes.byref(g)), "vmm_granularity")
+            own_c = pool.take(vmm.chunk_sizes(nb16, g.value))
+            maps.append(vmm.MappedRange(self.lib, [c.handle for c in own_c], [c.size for c in own_c]))
+            if PUSH_ON:
+                sbytes = (self.p - 1) * (-(-(nb16 // 16) // self.p)) * 16
+                scr_c = pool.take(vmm.chunk_sizes(max(16, sbytes), g.value))
+                maps.append(vmm.MappedRange(self.lib, [c.handle for c in scr_c], [c.size for c in scr_c]))
+            plan = ([(c.id, c.size, c.fd >= 0) for c in own_c], [(c.id, c.size, c.fd >= 0) for c in scr_c])
+        except Exception as e:   # noqa: BLE001 — agreed below
+            err = f"{type(e).__name__}: {e}"
+        plans = self.comm.server.call("allgather_obj", self.rank, (plan, err))
+        bad = [(i, e) for i, (_, e) in enumerate(plans) if e]
+        if bad:
+            for m in maps:
+                m.free()
+            pool.give(own_c + scr_c)
+            raise Mp4jException(f"memAlloc({nbytes}) failed on ranks {bad}")
+        push = all(pl[1] for pl, _ in plans)
+        new_own = [c for c in own_c + (scr_c if push else []) if c.fd >= 0]
+        got = {}
+        if any(new for pl, _ in plans for part in pl for (_, _, new) in part):
+            got = vmm.exchange_fds(self.comm.server, self.rank, self.p, [c.fd for c in new_own])
+        for c in new_own:                       # sent: every peer holds these chunks now
+            os.close(c.fd)
+            c.fd = -1                           # (an unsent chunk keeps its fd for a later send)
+        reg = _Reg(keep=None)
+        reg.vmm = list(maps) if push else maps[:1]
+        reg.nown = len(reg.vmm)
+        reg.chunks = own_c + scr_c
+        if not push and len(maps) > 1:
+            maps[1].free()
+        scratch = []
+        err = None
+        try:
+            for r in range(self.p):
+                if r == self.rank:
+                    reg.peers.append(maps[0].va)
+                    scratch.append(maps[1].va if push else 0)
+                    continue
+                fds = list(got.get(r, []))
+                try:
+                    parts = plans[r][0][0] + (plans[r][0][1] if push else [])
+                    for cid, _, new in parts:
+                        if new:
+                            pool.import_fd(r, cid, fds.pop(0))
+                    for part, dst in ((plans[r][0][0], reg.peers), (plans[r][0][1] if push else None, scratch)):
+                        if part is None:
+                            continue
+                        view = vmm.MappedRange(self.lib, [pool.peer[(r, cid)] for cid, _, _ in part],
+                                               [sz for _, sz, _ in part])
+                        reg.vmm.append(view)
+                        dst.append(view.va)
+                finally:
+                    for fd in got.get(r, []):
+                        os.close(fd)
+        except Exception as e:   # noqa: BLE001
+            err = f"{type(e).__name__}: {e}"
+        oks = self.comm.server.call("allgather_obj", self.rank, err)
+        if any(oks):
+            self.comm.server.call("barrier", self.rank)
+            self._release(reg)
+            raise Mp4jException(f"memAlloc({nbytes}) peer mapping failed on ranks "
+                                f"{[(i, o) for i, o in enumerate(oks) if o]}")
+        reg.scratch = scratch if push else None
+        t = vmm.tensor_at(maps[0].va, nb16, torch.uint8, torch.device("cuda", self.device))
+        self._regs[(maps[0].va, nb16)] = reg
+        return t[:nbytes // es * es].view(dtype)
+
     def mem_free(self, t: torch.Tensor) -> None:
         """Collective: release a :meth:`mem_alloc` tensor on every rank (its peers' mappings
         first, after every rank's stream drained)."""
@@ -851,6 +945,11 @@ class IpcAllreduce:
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # no peer kernel still reads or writes it
         reg = self._regs.pop(key)
+        if reg.chunks is not None:
+            # chunk pool: unmap every view (own + peers', VA ranges stay reserved) and return this
+            # rank's chunks to its pool; nothing is released (csrc/runtime/vmm.hip says why)
+            self._release(reg)
+            return
         if not VMM_RELEASE:
             # park the allocation in a per-size pool, handed out again by the next memAlloc of the
             # same size (every rank's pool state is identical: alloc / free are collective)
@@ -1683,6 +1782,9 @@ class IpcAllreduce:
                 pass
         self._regs = {}
         self._vmm_pool = {}
+        if getattr(self, "_chunk_pool", None) is not None:
+            self._chunk_pool.release_all()
+            self._chunk_pool = None
         for lst in getattr(self, "_scratch_pool", {}).values():
             for ptr, _ in lst:
                 self.lib.mp4x_ipc_free(ptr)

@@ -40,6 +40,11 @@ native.register_signatures({
     "mp4x_vmm_release_keep_va": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
     "mp4x_vmm_addr_free": (c_int, [c_void_p, c_size_t]),
     "mp4x_vmm_va_hint": (ctypes.c_uint64, [c_int]),
+    "mp4x_vmm_chunk_create": (c_int, [c_size_t, _U64P, _INTP]),
+    "mp4x_vmm_chunk_import": (c_int, [c_int, _U64P]),
+    "mp4x_vmm_chunk_release": (c_int, [ctypes.c_uint64]),
+    "mp4x_vmm_map_chunks": (c_int, [_U64P, ctypes.POINTER(c_size_t), c_int, ctypes.POINTER(c_void_p)]),
+    "mp4x_vmm_unmap_chunks": (c_int, [c_void_p, ctypes.POINTER(c_size_t), c_int]),
     "mp4x_release_all": (c_int, [c_void_p]),
 })
 
@@ -63,6 +68,132 @@ def chunk_plan(nbytes: int, gran: int, chunk: Optional[int] = None) -> (int, int
     if need <= cap:
         return need, 1
     return cap, -(-need // cap)
+
+
+def chunk_sizes(nbytes: int, gran: int, cap: Optional[int] = None) -> List[int]:
+    """Chunk sizes of a chunk-pool allocation of ``nbytes`` (largest first): ``cap``-byte chunks
+    (``MP4X_VMM_CHUNK`` rounded down to a power-of-two number of units), then the binary
+    decomposition of the rest in power-of-two multiples of the unit (2 MiB when the granularity
+    divides it).  Few distinct sizes, so a freed chunk serves later allocations of OTHER sizes
+    (:class:`ChunkPool`).  Pure function (unit-tested on CPU)."""
+    if nbytes <= 0:
+        raise Mp4jException("memAlloc needs a positive size")
+    gran = max(1, int(gran))
+    unit = _BIG_FRAG if _BIG_FRAG % gran == 0 else gran
+    top = max(unit, int(cap or os.environ.get("MP4X_VMM_CHUNK", DEFAULT_CHUNK)) // unit * unit)
+    top = unit << ((top // unit).bit_length() - 1)          # a power-of-two number of units
+    need = -(-int(nbytes) // unit) * unit
+    out = [top] * (need // top)
+    rem = need % top
+    s = top // 2
+    while rem:
+        if rem >= s:
+            out.append(s)
+            rem -= s
+        s //= 2
+    return out
+
+
+class Chunk:
+    """One physical chunk this rank owns: pool id (the same on every rank's books: alloc / free
+    are collective), size, generic allocation handle, dmabuf fd while it is new (not yet sent)."""
+    __slots__ = ("id", "size", "handle", "fd")
+
+    def __init__(self, cid: int, size: int, handle: int, fd: int):
+        self.id, self.size, self.handle, self.fd = cid, size, handle, fd
+
+
+class ChunkPool:
+    """This rank's physical memAlloc chunks: free ones per size, reused by later allocations of
+    any size (csrc/runtime/vmm.hip "chunk pool" says why nothing is released before close), plus
+    every peer chunk this rank imported, kept by (peer rank, chunk id) so a reused chunk is
+    mapped again with no fd exchange."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.free: Dict[int, List[Chunk]] = {}
+        self.owned: List[Chunk] = []
+        self.peer: Dict[tuple, int] = {}
+        self._next = 0
+
+    def take(self, sizes: List[int]) -> List[Chunk]:
+        out = []
+        try:
+            for sz in sizes:
+                lst = self.free.get(sz)
+                if lst:
+                    out.append(lst.pop())
+                    continue
+                h = ctypes.c_uint64()
+                fd = ctypes.c_int(-1)
+                check(self.lib.mp4x_vmm_chunk_create(sz, ctypes.byref(h), ctypes.byref(fd)), "vmm_chunk_create")
+                c = Chunk(self._next, sz, h.value, fd.value)
+                self._next += 1
+                self.owned.append(c)
+                out.append(c)
+        except Exception:
+            self.give(out)
+            raise
+        return out
+
+    def give(self, chunks: List[Chunk]) -> None:
+        for c in chunks:
+            self.free.setdefault(c.size, []).append(c)
+
+    def import_fd(self, rank: int, cid: int, fd: int) -> int:
+        h = ctypes.c_uint64()
+        check(self.lib.mp4x_vmm_chunk_import(fd, ctypes.byref(h)), "vmm_chunk_import")
+        self.peer[(rank, cid)] = h.value
+        return h.value
+
+    @property
+    def pooled_bytes(self) -> int:
+        return sum(c.size for c in self.owned)
+
+    def release_all(self) -> None:
+        """At close: every imported and owned chunk (best effort; nothing may map them any more)."""
+        for h in self.peer.values():
+            self.lib.mp4x_vmm_chunk_release(h)
+        self.peer = {}
+        for c in self.owned:
+            if c.fd is not None and c.fd >= 0:
+                try:
+                    os.close(c.fd)
+                except OSError:
+                    pass
+            self.lib.mp4x_vmm_chunk_release(c.handle)
+        self.owned, self.free = [], {}
+
+
+class MappedRange:
+    """Chunks mapped back to back at a fresh VA range of this process (own or a peer's).
+    :meth:`free` only unmaps: the range stays reserved (recorded in the VA quarantine), the chunks
+    stay with their pool."""
+
+    def __init__(self, lib, handles: List[int], sizes: List[int]):
+        self.lib = lib
+        self.sizes = list(sizes)
+        self._sizes = (c_size_t * len(sizes))(*sizes)
+        n = len(handles)
+        va = c_void_p()
+        rc = lib.mp4x_vmm_map_chunks((ctypes.c_uint64 * n)(*handles), self._sizes, n, ctypes.byref(va))
+        if va.value:
+            _QUARANTINE.append((va.value, sum(sizes)))
+        check(rc, "vmm_map_chunks")
+        self.va = va.value
+        self.fds: List[int] = []
+
+    @property
+    def nbytes(self) -> int:
+        return sum(self.sizes)
+
+    def close_fds(self) -> None:
+        pass
+
+    def free(self, keep_va=None) -> None:
+        if self.va:
+            check(self.lib.mp4x_vmm_unmap_chunks(c_void_p(self.va), self._sizes, len(self.sizes)), "vmm_unmap_chunks")
+            self.va = 0
 
 
 class VmmRegion:
@@ -125,23 +256,13 @@ class VmmRegion:
 
 
 class _VaQuarantine(list):
-    """Process-wide list of VA ranges released with ``keep_va`` (they hold no physical memory).
-    Bounded by ``MP4X_VMM_VA_QUARANTINE`` bytes of address space (default 64 TiB, a small part
-    of the 48-bit GPU VA space): beyond it the oldest ranges are freed."""
+    """Process-wide record of the VA ranges this process keeps reserved instead of freeing
+    (hipMemAddressFree breaks later exports on this runtime, see csrc/runtime/vmm.hip): they
+    hold no physical memory, only address space (the GPU VA space is 2^48 bytes)."""
 
     def __init__(self):
         super().__init__()
         self.lib = None
-        self.cap = int(os.environ.get("MP4X_VMM_VA_QUARANTINE", 64 << 40))
-
-    def append(self, item) -> None:
-        super().append(item)
-        total = sum(b for _, b in self)
-        while len(self) > 1 and total > self.cap:
-            va, nb = self.pop(0)
-            total -= nb
-            if self.lib is not None:
-                self.lib.mp4x_vmm_addr_free(c_void_p(va), nb)
 
 
 _QUARANTINE = _VaQuarantine()

@@ -50,6 +50,7 @@ def _memalloc_cycles(comm):
         bad += int((t != _exp(n, p)).sum())
         comm.memFree(t)
         del t
+        torch.cuda.empty_cache()                        # temporaries of the check are not memAlloc's
         comm.barrier()
         samples.append(_used())
     return bad, samples, dict(comm.device.stats)
