@@ -917,6 +917,10 @@ class DeviceEngine(AutotuneMixin):
                 inst.close()
             from .ipc import IpcAllreduce
             inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8")
+            bad = self._probe_staging(inst)
+            if bad:
+                inst.close()
+                raise Mp4jException(f"staging self-test failed: {bad}")
             self._probe_spin(inst)
             if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
                 inst.prepare_graph()
@@ -927,6 +931,34 @@ class DeviceEngine(AutotuneMixin):
             return self.ipc_large()
         self._ipc_fp8_big = inst
         return inst
+
+    def _probe_staging(self, inst) -> list:
+        """Collective first-contact check of a NEW instance's staging buffer (the whole-tensor fp8
+        one is VMM-built, coarse-grained, above 2 GiB): the staged two-shot twice on the same
+        tensor (the second call reduces the first call's result, so a stale line on either side of
+        a link shows as a wrong element), exact, short spin bound.  Returns every rank's failures
+        (agreed through the control plane; empty = fine)."""
+        from . import ipc as ipcm
+        from ..operators import Operators
+        fails = []
+        try:
+            inst.set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2")))
+            op = for_dtype(Operators.Float.SUM, DType.F32)
+            n = min(inst.nbytes // 4, 1 << 20)
+            t = torch.empty(n, dtype=torch.float32, device=self.device)
+            exp = self._fill_probe(t, op)
+            for rep in range(2):
+                inst.allreduce(t, op, algo=ipcm.TWOSHOT)
+                torch.cuda.synchronize(self.device)
+                inst.raise_if_failed()
+                nbad = int((t != exp * (self.p ** rep)).sum())
+                if nbad:
+                    fails.append(f"staged_twoshot_{rep}: {nbad} wrong elements")
+            inst.set_spin(ipcm.spin_default())
+        except Exception as e:   # noqa: BLE001
+            fails.append(f"{type(e).__name__}: {e}")
+        allf = self.comm.server.call("allgather_obj", self.rank, fails)
+        return [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
 
     def _sync(self):
         if self.device.type == "cuda":
