@@ -387,6 +387,11 @@ extern "C" void mp4x_set_k1_grid(int64_t cap) { g_k1_grid = cap; }
 
 extern "C" const char* mp4x_version(void) { return "mp4x-native 0.1 gfx950"; }
 
+// Reads and clears this thread's last HIP error.  mp4x reports its own failures through return
+// codes; a failed HIP call must not stay "last error" for PyTorch's next kernel-launch check to
+// report as its own (native.check() and the best-effort release paths call this).
+extern "C" int mp4x_clear_error(void) { return (int)hipGetLastError(); }
+
 extern "C" int mp4x_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -294,7 +294,10 @@ template <typename F> inline int with_nr(int p, F&& f) {
 // Blocks per CU the occupancy API admits for `kern` at kIpcThreads threads (min-folded into *m).
 template <typename K> inline void occ_min(K kern, int* m) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, kIpcThreads, 0) != hipSuccess) n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, kIpcThreads, 0) != hipSuccess) {
+    n = 0;
+    (void)hipGetLastError();      // a failed query must not surface as PyTorch's next error
+  }
   if (n < *m) *m = n;
 }
 

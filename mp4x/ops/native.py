@@ -11,6 +11,7 @@ silent fallback: every device collective that needs a kernel goes through here.
 from __future__ import annotations
 
 import ctypes
+import logging
 import os
 import threading
 from typing import Sequence
@@ -65,6 +66,7 @@ _HIP_SIGS = {
     "mp4x_set_k1_variant": (None, [c_int]),
     "mp4x_set_k1_grid": (None, [c_int64]),
     "mp4x_version": (ctypes.c_char_p, []),
+    "mp4x_clear_error": (c_int, []),
     "mp4x_device_count": (c_int, []),
 }
 
@@ -218,10 +220,34 @@ def available() -> bool:
         return False
 
 
+def clear_hip_error() -> int:
+    """Read and clear this thread's last HIP error (0 if none, or if the library is not loaded):
+    a HIP call that failed inside mp4x must not stay "last error" for PyTorch's next kernel-launch
+    check to report as ITS failure."""
+    lib = _hip
+    if lib is None:
+        return 0
+    try:
+        return int(lib.mp4x_clear_error())
+    except Exception:   # noqa: BLE001 — an older library without the symbol
+        return 0
+
+
 def check(rc: int, where: str) -> None:
     if rc != 0:
+        if rc < 1000:
+            clear_hip_error()
         msgs = {1001: "bad argument", 1002: "unsupported dtype/op"}
         raise NativeError(where, rc, msgs.get(rc, "hip error"))
+
+
+def soft_check(rc: int, where: str, log=None) -> int:
+    """Best-effort release calls (close a mapping, free a buffer): a failure is logged and the
+    HIP error state cleared instead of raised."""
+    if rc:
+        clear_hip_error()
+        (log or logging.getLogger("mp4x.native")).warning("%s failed: hip error %d", where, rc)
+    return rc
 
 
 def ptr_array(ptrs: Sequence[int]):

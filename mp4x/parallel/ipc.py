@@ -651,7 +651,7 @@ class IpcAllreduce:
         if CLOSE_PEERS:
             ptr = self._peer_bases.pop(hk, None)
             if ptr is not None:
-                self.lib.mp4x_ipc_close_handle(ptr)
+                native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
 
     def _alloc_scratch(self, nbytes: int, hs: int):
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
@@ -673,7 +673,7 @@ class IpcAllreduce:
             check(self.lib.mp4x_ipc_get_handle(ptr, h), "ipc_get_handle(scratch)")
         except Exception:   # noqa: BLE001
             if ptr:
-                self.lib.mp4x_ipc_free(ptr)
+                native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)
             return None, None
         self._scratch_size[ptr.value] = size
         return ptr, h.raw
@@ -685,7 +685,7 @@ class IpcAllreduce:
         if scr and scr[0]:
             if CLOSE_PEERS:
                 self._scratch_size.pop(scr[0].value, None)
-                self.lib.mp4x_ipc_free(scr[0])
+                native.soft_check(self.lib.mp4x_ipc_free(scr[0]), "ipc_free", LOG)
             else:
                 self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
@@ -1077,11 +1077,11 @@ class IpcAllreduce:
         torch.cuda.synchronize()
         self.comm.server.call("barrier", self.rank)         # every peer is done before unmapping
         for q in opened:
-            self.lib.mp4x_ipc_close_handle(q)
+            native.soft_check(self.lib.mp4x_ipc_close_handle(q), "ipc_close_handle", LOG)
         if ptr:
-            self.lib.mp4x_ipc_free(ptr)
+            native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)
         if scr:
-            self.lib.mp4x_ipc_free(scr)
+            native.soft_check(self.lib.mp4x_ipc_free(scr), "ipc_free", LOG)
         return bad
 
     def _selftest_plans(self, ptr: int, peers, n: int, got: torch.Tensor, st) -> int:
@@ -1753,10 +1753,10 @@ class IpcAllreduce:
         if self._sig and self._herr:
             self.lib.mp4x_ipc_set_host_error(self._sig, None)
         for ptr in self._opened:
-            self.lib.mp4x_ipc_close_handle(ptr)
+            native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
         self._opened = []
         if self._data and not getattr(self, "_vmm_data", False):
-            self.lib.mp4x_ipc_free(self._data)
+            native.soft_check(self.lib.mp4x_ipc_free(self._data), "ipc_free", LOG)
         self._data = c_void_p()
         for region in reversed(getattr(self, "_data_regions", [])):   # imported views first
             try:
@@ -1765,14 +1765,14 @@ class IpcAllreduce:
                 pass
         self._data_regions = []
         if self._sig:
-            self.lib.mp4x_ipc_free(self._sig)
+            native.soft_check(self.lib.mp4x_ipc_free(self._sig), "ipc_free", LOG)
             self._sig = c_void_p()
         if self._herr:
             self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
         for ptr in getattr(self, "_peer_bases", {}).values():
-            self.lib.mp4x_ipc_close_handle(ptr)
+            native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
         self._peer_bases = {}
         pooled = [r for lst in getattr(self, "_vmm_pool", {}).values() for r in lst]
         for reg in list(getattr(self, "_regs", {}).values()) + pooled:
@@ -1787,5 +1787,5 @@ class IpcAllreduce:
             self._chunk_pool = None
         for lst in getattr(self, "_scratch_pool", {}).values():
             for ptr, _ in lst:
-                self.lib.mp4x_ipc_free(ptr)
+                native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)
         self._scratch_pool = {}

@@ -153,7 +153,7 @@ class ChunkPool:
     def release_all(self) -> None:
         """At close: every imported and owned chunk (best effort; nothing may map them any more)."""
         for h in self.peer.values():
-            self.lib.mp4x_vmm_chunk_release(h)
+            native.soft_check(self.lib.mp4x_vmm_chunk_release(h), "vmm_chunk_release")
         self.peer = {}
         for c in self.owned:
             if c.fd is not None and c.fd >= 0:
@@ -161,7 +161,7 @@ class ChunkPool:
                     os.close(c.fd)
                 except OSError:
                     pass
-            self.lib.mp4x_vmm_chunk_release(c.handle)
+            native.soft_check(self.lib.mp4x_vmm_chunk_release(c.handle), "vmm_chunk_release")
         self.owned, self.free = [], {}
 
 
