@@ -885,7 +885,13 @@ class IpcAllreduce:
         new_own = [c for c in own_c + (scr_c if push else []) if c.fd >= 0]
         got = {}
         if any(new for pl, _ in plans for part in pl for (_, _, new) in part):
-            got = vmm.exchange_fds(self.comm.server, self.rank, self.p, [c.fd for c in new_own])
+            try:
+                got = vmm.exchange_fds(self.comm.server, self.rank, self.p, [c.fd for c in new_own])
+            except Exception:   # agreed inside exchange_fds: every rank is here
+                for m in maps:
+                    m.free()
+                pool.give(own_c + scr_c)          # unsent: their fds stay open for a later send
+                raise
         for c in new_own:                       # sent: every peer holds these chunks now
             os.close(c.fd)
             c.fd = -1                           # (an unsent chunk keeps its fd for a later send)
