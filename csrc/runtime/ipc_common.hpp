@@ -105,6 +105,26 @@ struct Segs {
   int64_t hi[kIpcMaxRanks];
 };
 
+// Lane t's peer Signal block: a select chain over the kernel argument's pointers (held in SGPRs)
+// instead of P.sig[t], whose per-lane index made every barrier a vector load from the kernarg
+// segment before the flag store.
+__device__ __forceinline__ uint64_t sgpr64(const void* v) {   // a wave-uniform pointer, in SGPRs
+  const uint64_t x = reinterpret_cast<uint64_t>(v);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(x >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+__device__ __forceinline__ Signal* sig_of(const IpcPtrs& P, int t) {
+  uint64_t s = sgpr64(P.sig[0]);
+#pragma unroll
+  for (int k = 1; k < kIpcMaxRanks; ++k) {
+    const uint64_t v = sgpr64(P.sig[k]);
+    s = t == k ? v : s;
+  }
+  return reinterpret_cast<Signal*>(s);
+}
+
 __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int rank, int p, uint32_t epoch,
                                               Signal* self) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its stores
@@ -116,17 +136,22 @@ __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int r
   if (t < p) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    Signal* peer = P.sig[t];
+    Signal* peer = sig_of(P, t);
     uint32_t* slot = which == 0 ? &peer->start[blockIdx.x][rank]
                    : which == 1 ? &peer->mid[blockIdx.x][rank] : &peer->end[blockIdx.x][rank];
     __hip_atomic_store(slot, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t* mine = which == 0 ? &self->start[blockIdx.x][t]
                    : which == 1 ? &self->mid[blockIdx.x][t] : &self->end[blockIdx.x][t];
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    uint64_t spin = __hip_atomic_load(&self->spin_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (spin == 0) spin = kDefaultSpinTicks;
+    // the bound is read only by a lane that has to wait: the fast path (peers already there)
+    // pays one uncached round trip, not two (r4 latency: +4 us per kernel when it was read first)
+    uint64_t spin = 0;
     uint32_t seen;
     while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
+      if (spin == 0) {
+        spin = __hip_atomic_load(&self->spin_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (spin == 0) spin = kDefaultSpinTicks;
+      }
       __builtin_amdgcn_s_sleep(2);
       const bool other_protocol = seen != epoch && ((seen ^ epoch) & ~kTagMask) == 0;
       if (other_protocol || __builtin_amdgcn_s_memrealtime() - t0 > spin) {
