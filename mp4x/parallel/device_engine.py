@@ -606,10 +606,10 @@ class DeviceEngine(AutotuneMixin):
         memo = getattr(self, "_sel_memo", None)
         if gen is None or memo is None:
             return self._select(kind, nbytes, op, dtype, operand)
+        # the tier state (every attribute _select reads: _TIER_ATTRS) enters as ONE version number
+        # that any assignment to those attributes bumps — hashing them all per call cost ~1 us
         key = (kind, nbytes, op, dtype, getattr(operand, "codec", None), getattr(operand, "compress", False),
-               self.algo, gen, self.ipc_enabled, self.ipc_oneshot_max, self.ipc_twoshot_max, self._hier_failed,
-               self.backend, self.a2a_bytes, self.hier_min_bytes, self._dm_large, self.layout.multi_node,
-               self.device.type)
+               gen, self._state_ver)
         try:
             hit = memo.get(key)
         except TypeError:       # an unhashable custom operator: no memo
@@ -1606,6 +1606,36 @@ def _watched(name, fn):
     wrapper.__wrapped__ = fn
     return wrapper
 
+
+# Attributes the schedule choice reads (DeviceEngine._select): properties whose setter bumps
+# ``_state_ver``, the select memo's view of them (class-level defaults kept).
+_TIER_ATTRS = ("algo", "ipc_enabled", "ipc_oneshot_max", "ipc_twoshot_max", "_hier_failed", "backend", "a2a_bytes",
+               "hier_min_bytes", "_dm_large", "layout", "device")
+
+
+def _tier_attr(name, default):
+    slot = "_tier_" + name
+
+    def get(self):
+        try:
+            return self.__dict__[slot]
+        except KeyError:
+            if default is _NO_DEFAULT:
+                raise AttributeError(name) from None
+            return default
+
+    def put(self, v):
+        d = self.__dict__
+        d[slot] = v
+        d["_state_ver"] = d.get("_state_ver", 0) + 1
+
+    return property(get, put, doc=f"tier input {name!r} (assignments invalidate the select memo)")
+
+
+_NO_DEFAULT = object()
+DeviceEngine._state_ver = 0
+for _n in _TIER_ATTRS:
+    setattr(DeviceEngine, _n, _tier_attr(_n, DeviceEngine.__dict__.get(_n, _NO_DEFAULT)))
 
 _WATCHED = ["allreduce", "autotune_allreduce", "autotune_reduce_scatter", "autotune_allgather", "autotune_reduce",
             "autotune_broadcast", "autotune_gather", "autotune_scatter", "reduce_scatter", "allgather", "broadcast", "reduce", "gather",

@@ -278,6 +278,7 @@ class IpcAllreduce:
         self.share = share
         self.shared_gpu = share > 1
         self.grid_caps = {}
+        self._cap_fast = {}          # (family, torch dtype, operator) -> cap: the per-call lookup
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
         err = None
@@ -397,10 +398,14 @@ class IpcAllreduce:
         computes the same value), memoised and logged once per kernel."""
         if not self.shared_gpu:
             return occupancy.MAX_BLOCKS
+        fast = self._cap_fast.get((family, dtype, op))
+        if fast is not None:                       # the per-call path: one dict probe
+            return fast
         code = int(op.code) if op is not None else 0
         key = (family, dtype, code)
         cap = self.grid_caps.get(key)
         if cap is not None:
+            self._cap_fast[(family, dtype, op)] = cap
             return cap
         dt = int(dtype_of_torch(dtype)) if dtype is not None else int(DType.F32)
         n = ctypes.c_int(0)
@@ -423,6 +428,7 @@ class IpcAllreduce:
         bpc = min(known) if known else 1
         cap = occupancy.shared_grid_cap(self.cus, bpc, self.share)
         self.grid_caps[key] = cap
+        self._cap_fast[(family, dtype, op)] = cap
         LOG.info("rank %d: grid cap %s %s op=%d p=%d share=%d: %d blocks (blocks/CU: api %s, compiler %s)",
                  self.rank, family, DType(dt).name, code, self.p, self.share, cap, api, tbl)
         return cap
