@@ -212,6 +212,28 @@ def hostmap_ext():
     return _hostmap_ext or None
 
 
+_launch_ext = None
+
+
+def launch_ext():
+    """The ctypes-free launcher of the IPC allreduce (``_mp4x_launch``, csrc/pyext/launch_ext.cpp),
+    bound to THIS process's libmp4x_hip.so, or None when not built or ``MP4X_LAUNCH_EXT=0``."""
+    global _launch_ext
+    if _launch_ext is None:
+        with _lock:
+            if _launch_ext is None:
+                mod = False
+                if os.environ.get("MP4X_LAUNCH_EXT", "1") != "0":
+                    try:
+                        lib = hip()
+                        mod = _load_ext("_mp4x_launch")
+                        mod.bind(ctypes.cast(lib.mp4x_ipc_allreduce_ex, ctypes.c_void_p).value)
+                    except Exception:   # noqa: BLE001 — ctypes path stays
+                        mod = False
+                _launch_ext = mod
+    return _launch_ext or None
+
+
 def available() -> bool:
     try:
         hip()

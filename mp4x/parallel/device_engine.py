@@ -768,7 +768,7 @@ class DeviceEngine(AutotuneMixin):
                 and self._ipc_obj.registered(view) is not None:
             algo = "ipc2z"      # registered on this rank (registration is collective): zero-copy
         self._count("allreduce." + algo)
-        fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view))
+        fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view), capturing=capturing)
         self._post_scale(view, scale, fused)
         return arr
 
@@ -814,14 +814,17 @@ class DeviceEngine(AutotuneMixin):
                 and self._ipc_obj._find(t)[0].vmm:
             self._ipc_obj.mem_free(t)
 
-    def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0) -> bool:
-        """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused)."""
+    def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0,
+                       capturing: Optional[bool] = None) -> bool:
+        """Run schedule ``algo``; returns True when ``scale`` was applied inside it (fused).
+        ``capturing``: whether a hipGraph capture is in progress, when the caller knows."""
         if algo == "ipc1" or algo == "ipc2":
             # the latency tier first: a staged one-/two-shot on the default instance, not capturing
             inst = self._ipc_obj
-            if inst is not None and view.numel() * view.element_size() <= self.ipc_twoshot_max \
-                    and not capturing_now():
-                inst.allreduce(view, op, algo=0 if algo == "ipc1" else 1, scale=scale)   # ipc.ONESHOT / TWOSHOT
+            if capturing is None:
+                capturing = capturing_now()
+            if inst is not None and not capturing and view.numel() * view.element_size() <= self.ipc_twoshot_max:
+                inst.allreduce(view, op, algo=0 if algo == "ipc1" else 1, scale=scale, capturing=False)
                 return True
         algo, grid = zc_grid(algo)
         if algo in ("ipc1", "ipc2", "ipc2p", "ipc2z", "ipc2w") and self.ipc() is None:

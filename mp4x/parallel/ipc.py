@@ -322,6 +322,9 @@ class IpcAllreduce:
             raise Mp4jException(f"IPC peer mapping failed on ranks {bad or 'of another node'}")
         self._pp_data = ptr_array(self.data_ptrs)
         self._pp_sig = ptr_array(self.sig_ptrs)
+        # integer addresses of the two pointer arrays, for the ctypes-free launcher
+        self._pp_data_addr = ctypes.addressof(self._pp_data[1])
+        self._pp_sig_addr = ctypes.addressof(self._pp_sig[1])
         self.epoch = 0
         self._pp_hi = None         # peer pointers of the upper half-buffers (pipelined large path)
         self._copy_stream = None
@@ -442,7 +445,8 @@ class IpcAllreduce:
         return ipc_op_ok(t.dtype, op)
 
     def allreduce(self, view: torch.Tensor, op, algo: int = ONESHOT, out: Optional[torch.Tensor] = None,
-                  blocks: int = 0, overlap: Optional[bool] = None, scale: float = 1.0) -> torch.Tensor:
+                  blocks: int = 0, overlap: Optional[bool] = None, scale: float = 1.0,
+                  capturing: Optional[bool] = None) -> torch.Tensor:
         """In place (or into ``out``) allreduce of a contiguous device tensor.
 
         ``overlap`` (messages larger than the buffer): pipeline half-buffer pieces with the
@@ -472,7 +476,8 @@ class IpcAllreduce:
             blocks = max(1, min(cap, -(-min(total, self.nbytes) // 16 // vec_per_block)))
         if overlap is None:
             overlap = self._overlap_default
-        capturing = capturing_now()
+        if capturing is None:                      # the engine's latency path already knows
+            capturing = capturing_now()
         if total > self.nbytes and overlap and not capturing:
             return self._allreduce_pipelined(view.view(torch.uint8), out.view(torch.uint8), total, dt, op, algo,
                                              blocks, out, scale)
@@ -486,6 +491,8 @@ class IpcAllreduce:
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
         sp, dp = view.data_ptr(), out.data_ptr()
         fused = sp % 16 == 0 and self._fuse_copy   # copy-in inside the kernel: one launch
+        lx = native.launch_ext()
+        code = int(op.code)
         while off < total:
             m = min(piece, total - off)
             if not fused:
@@ -494,10 +501,14 @@ class IpcAllreduce:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
-            check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), self._pp_data[0], self._pp_sig[0],
-                                                 self.rank, self.p, m, sp + off if fused else None,
-                                                 dp + off, self.epoch, blocks, edev, scale, st),
-                  "mp4x_ipc_allreduce")
+            if lx is not None:
+                rc = lx.allreduce_ex(algo, dt, code, self._pp_data_addr, self._pp_sig_addr, self.rank, self.p, m,
+                                     sp + off if fused else None, dp + off, self.epoch, blocks, edev, scale, st)
+            else:
+                rc = self.lib.mp4x_ipc_allreduce_ex(algo, dt, code, self._pp_data[0], self._pp_sig[0], self.rank,
+                                                    self.p, m, sp + off if fused else None, dp + off, self.epoch,
+                                                    blocks, edev, scale, st)
+            check(rc, "mp4x_ipc_allreduce")
             off += m
         return out
 

@@ -1,0 +1,45 @@
+"""The ctypes-free launcher (csrc/pyext/launch_ext.cpp) passes every argument of
+mp4x_ipc_allreduce_ex through unchanged: bound here to a ctypes callback with the same C
+signature (CPU, no HIP) that records what it receives."""
+import ctypes
+
+import pytest
+
+from mp4x.ops import native
+
+PROTO = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p)
+
+
+def test_allreduce_ex_marshals_every_argument():
+    try:
+        mod = native._load_ext("_mp4x_launch")
+    except native.NativeUnavailable:
+        pytest.skip("_mp4x_launch not built")
+    seen = []
+
+    def fake(*args):
+        seen.append(args)
+        return 7
+
+    cb = PROTO(fake)
+    mod.bind(ctypes.cast(cb, ctypes.c_void_p).value)
+    try:
+        _check(mod, seen)
+    finally:
+        mod.bind(0)                 # the callback dies with this test: unbind (calls then raise)
+    with pytest.raises(RuntimeError):
+        mod.allreduce_ex(*([0] * 13 + [1.0, 0]))
+
+
+def _check(mod, seen):
+    rc = mod.allreduce_ex(1, 2, 3, 0x1000, 0x2000, 5, 8, (5 << 32) + 16, None, 0x3000, 0xFFFFFFF0, 48, None, 0.125,
+                          0x4000)
+    assert rc == 7
+    (a,) = seen
+    assert a[:3] == (1, 2, 3) and a[3] == 0x1000 and a[4] == 0x2000 and a[5:8] == (5, 8, (5 << 32) + 16)
+    assert a[8] is None and a[9] == 0x3000 and a[10] == 0xFFFFFFF0 and a[11] == 48 and a[12] is None
+    assert a[13] == pytest.approx(0.125) and a[14] == 0x4000
+    with pytest.raises(TypeError):
+        mod.allreduce_ex(1, 2, 3)

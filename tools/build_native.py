@@ -217,6 +217,19 @@ def build_hostmapext():
     return out
 
 
+def build_launchext():
+    """``_mp4x_launch``: plain CPython extension, the ctypes-free per-call launch of the IPC
+    allreduce (csrc/pyext/launch_ext.cpp; calls libmp4x_hip.so through a bound pointer)."""
+    import sysconfig
+    src = os.path.join(CSRC, "pyext", "launch_ext.cpp")
+    out = os.path.join(OUT, "_mp4x_launch" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if os.path.exists(src) and newer(src, out, []):
+        run(["g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-shared", "-I", sysconfig.get_paths()["include"],
+             src, "-o", out])
+        print("  g++  ", os.path.relpath(src, ROOT), "->", os.path.relpath(out, ROOT))
+    return out
+
+
 def build_mapext():
     """``_mp4x_map``: CPython extension reading ``at::Tensor`` facts directly (libtorch headers,
     linked against the torch libraries PyTorch itself loads; rpath to torch/lib)."""
@@ -257,6 +270,7 @@ def main(argv=None):
     build_pyext(build_host(a.j))
     build_mapext()
     build_hostmapext()
+    build_launchext()
     return 0
 
 
