@@ -31,6 +31,7 @@ def test_allreduce_ex_marshals_every_argument():
         mod.bind(0)                 # the callback dies with this test: unbind (calls then raise)
     with pytest.raises(RuntimeError):
         mod.allreduce_ex(*([0] * 13 + [1.0, 0]))
+    native._launch_ext = None       # the next native.launch_ext() binds the real library again
 
 
 def _check(mod, seen):
