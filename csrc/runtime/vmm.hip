@@ -188,15 +188,11 @@ extern "C" int mp4x_vmm_free(void* va, size_t chunk, int n, const uint64_t* hand
   return teardown(va, chunk, n, handles, chunk * (size_t)n);
 }
 
-// Unmap + release the chunks but keep the VA range reserved (``mp4x_vmm_addr_free`` later): the
-// physical memory goes back to the device while no later reservation can land on these
-// addresses (MP4X_VMM_FRESH_VA, parallel/ipc.py mem_free).
+// Unmap + release the chunks but keep the VA range reserved for the rest of the process: no
+// later reservation lands on these addresses, and no hipMemAddressFree happens (see the chunk
+// pool below for why).  MP4X_VMM_POLICY fresh_va / keep_*_va, parallel/ipc.py mem_free.
 extern "C" int mp4x_vmm_release_keep_va(void* va, size_t chunk, int n, const uint64_t* handles) {
   return teardown(va, chunk, n, handles, 0);
-}
-
-extern "C" int mp4x_vmm_addr_free(void* va, size_t bytes) {
-  return (int)hipMemAddressFree(va, bytes);
 }
 
 // ---------------------------------------------------------------- chunk pool (memAlloc default)

@@ -38,7 +38,6 @@ native.register_signatures({
     "mp4x_vmm_import": (c_int, [_INTP, c_size_t, c_int, ctypes.POINTER(c_void_p), _U64P]),
     "mp4x_vmm_free": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
     "mp4x_vmm_release_keep_va": (c_int, [c_void_p, c_size_t, c_int, _U64P]),
-    "mp4x_vmm_addr_free": (c_int, [c_void_p, c_size_t]),
     "mp4x_vmm_va_hint": (ctypes.c_uint64, [c_int]),
     "mp4x_vmm_chunk_create": (c_int, [c_size_t, _U64P, _INTP]),
     "mp4x_vmm_chunk_import": (c_int, [c_int, _U64P]),
@@ -247,8 +246,6 @@ class VmmRegion:
             if keep_va is not None:
                 check(self.lib.mp4x_vmm_release_keep_va(c_void_p(self.va), self.chunk, self.n, self._handles),
                       "vmm_release_keep_va")
-                if getattr(keep_va, "lib", 0) is None:
-                    keep_va.lib = self.lib
                 keep_va.append((self.va, self.nbytes))
             else:
                 check(self.lib.mp4x_vmm_free(c_void_p(self.va), self.chunk, self.n, self._handles), "vmm_free")
@@ -259,10 +256,6 @@ class _VaQuarantine(list):
     """Process-wide record of the VA ranges this process keeps reserved instead of freeing
     (hipMemAddressFree breaks later exports on this runtime, see csrc/runtime/vmm.hip): they
     hold no physical memory, only address space (the GPU VA space is 2^48 bytes)."""
-
-    def __init__(self):
-        super().__init__()
-        self.lib = None
 
 
 _QUARANTINE = _VaQuarantine()
