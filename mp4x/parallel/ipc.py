@@ -1199,11 +1199,28 @@ class IpcAllreduce:
         blocks = self._grid(total // 16, "twoshot", dtype, op)   # >= 8: every XCD passes the barriers
         if grid > 0:
             blocks = min(grid, self.grid_cap("twoshot", dtype, op))
-        pp = ptr_array(peers)
-        check(self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
-                                             self._pp_sig[0], self.rank, self.p, total, None, dst,
-                                             self.epoch | ZC_TAG, blocks, edev, scale, st),
-              "mp4x_ipc_allreduce(zero-copy)")
+        pp = self._peer_pp(peers)
+        lx = native.launch_ext()
+        if lx is not None:
+            rc = lx.allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), ctypes.addressof(pp[1]),
+                                 self._pp_sig_addr, self.rank, self.p, total, None, dst, self.epoch | ZC_TAG, blocks,
+                                 edev, scale, st)
+        else:
+            rc = self.lib.mp4x_ipc_allreduce_ex(TWOSHOT, int(dtype_of_torch(dtype)), int(op.code), pp[0],
+                                                self._pp_sig[0], self.rank, self.p, total, None, dst,
+                                                self.epoch | ZC_TAG, blocks, edev, scale, st)
+        check(rc, "mp4x_ipc_allreduce(zero-copy)")
+
+    def _peer_pp(self, peers):
+        """The native pointer array of a registration's peer list, built once per list object
+        (the per-call path of the zero-copy forms; a registration keeps its list)."""
+        cache = self.__dict__.setdefault("_pp_cache", {})
+        ent = cache.get(id(peers))
+        if ent is None or ent[0] is not peers:
+            if len(cache) >= 256:
+                cache.clear()
+            ent = cache[id(peers)] = (peers, ptr_array(peers))
+        return ent[1]
 
     # ---------------------------------------------------------------- zero-copy RS / AG
     # On a registered tensor the direct reduce-scatter / all-gather kernels read the peers'
