@@ -190,8 +190,10 @@ class MappedRange:
         pass
 
     def free(self, keep_va=None) -> None:
+        """Unmap (best effort: a failed unmap only leaves address space mapped, logged)."""
         if self.va:
-            check(self.lib.mp4x_vmm_unmap_chunks(c_void_p(self.va), self._sizes, len(self.sizes)), "vmm_unmap_chunks")
+            native.soft_check(self.lib.mp4x_vmm_unmap_chunks(c_void_p(self.va), self._sizes, len(self.sizes)),
+                              "vmm_unmap_chunks")
             self.va = 0
 
 
