@@ -414,7 +414,11 @@ def main():
     # 200k keys x float[64] per rank, half shared), config 5 (8 GB f32 allreduce, fp8 wire codec)
     configs = None
     if p > 1 and not args.cpu and not args.no_configs and not (args.algo or args.codec):
-        configs = _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev)
+        # a bounded IPC spin (60 s) for these evidence runs: a kernel that cannot complete raises
+        # (recorded, every rank stops together) long before the watchdog's 600 s would end the
+        # whole job and lose the headline line
+        with comm.device.probing(float(os.environ.get("MP4X_BENCH_CONFIG_SPIN_S", 60))):
+            configs = _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev)
 
     ref = REF_BUSBW_MBPS.get(p)
     topo = None

@@ -133,6 +133,7 @@ class DeviceEngine(AutotuneMixin):
     _hier_failed = False
     hier_min_bytes = 1 << 20
     _probe_depth = 0
+    _probe_s: Optional[float] = None      # explicit bound of the innermost probing(seconds) scope
     _ipc_obj = _ipc_large = _ipc_fp8_big = None
 
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
@@ -387,26 +388,33 @@ class DeviceEngine(AutotuneMixin):
     def _probe_spin(self, inst) -> None:
         if self._probe_depth and inst is not None:
             from .ipc import probe_spin
-            inst.set_spin(probe_spin())
+            inst.set_spin(self._probe_s or probe_spin())
 
     @contextlib.contextmanager
-    def probing(self):
+    def probing(self, seconds: Optional[float] = None):
         """Autotune / probe scope: every IPC instance (also ones created inside) uses the short
-        probe spin bound (``MP4X_IPC_PROBE_SPIN_S``), so a candidate that cannot complete on this
-        topology is ruled out in seconds; the fail-stop bound is restored afterwards."""
+        probe spin bound (``MP4X_IPC_PROBE_SPIN_S``, or ``seconds``), so a candidate that cannot
+        complete on this topology is ruled out in seconds instead of after the fail-stop budget;
+        that budget is restored afterwards.  Collective in effect (every rank enters it around
+        the same calls)."""
         from .ipc import probe_spin, spin_default
         self._probe_depth += 1
+        prev = self._probe_s
+        if seconds is not None:
+            self._probe_s = float(seconds)
         try:
-            if self._probe_depth == 1:
+            if self._probe_depth == 1 or seconds is not None:
                 for inst in self._ipc_all():
-                    inst.set_spin(probe_spin())
+                    inst.set_spin(self._probe_s or probe_spin())
             yield
         finally:
             self._probe_depth -= 1
-            if self._probe_depth == 0:
+            self._probe_s = prev
+            restore = spin_default() if self._probe_depth == 0 else (self._probe_s or probe_spin())
+            if self._probe_depth == 0 or seconds is not None:
                 for inst in self._ipc_all():
                     try:
-                        inst.set_spin(spin_default())
+                        inst.set_spin(restore)
                     except Exception as e:   # noqa: BLE001 — a dead mesh is reported by the next call
                         LOG.warning("rank %d: could not restore the IPC spin bound: %s", self.rank, e)
 

@@ -210,6 +210,25 @@ def test_probing_scope_uses_the_short_bound_and_restores(monkeypatch):
     assert e._ipc_obj.spins == [10.0, 600.0] and late.spins == [10.0]
 
 
+def test_probing_scope_with_an_explicit_bound_nests(monkeypatch):
+    """bench.py's baseline configs run under probing(60): a kernel that cannot complete raises
+    after 60 s instead of the 600 s fail-stop budget; an autotune inside keeps ITS bound and the
+    outer one comes back after it."""
+    monkeypatch.delenv("MP4X_IPC_SPIN_S", raising=False)
+    monkeypatch.delenv("MP4X_WATCHDOG_TIMEOUT", raising=False)
+    e = _engine()
+    e._ipc_obj, e._ipc_large, e._ipc_fp8_big, e._hier = _Inst(), None, None, None
+    with e.probing(60):
+        late = _Inst()
+        e._probe_spin(late)
+        with e.probing():                         # a tuner inside: the explicit outer bound stays
+            pass
+        with e.probing(5):
+            pass
+    assert e._ipc_obj.spins == [60.0, 5.0, 60.0, 600.0] and late.spins == [60.0]
+    assert e._probe_depth == 0 and e._probe_s is None
+
+
 def test_process_barrier_and_close_surface_a_timed_out_collective():
     from mp4x import CommMaster, ProcessCommSlave
     import tempfile
