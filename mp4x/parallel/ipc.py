@@ -927,27 +927,31 @@ class IpcAllreduce:
                     scratch.append(maps[1].va if push else 0)
                     continue
                 fds = list(got.get(r, []))
-                try:
-                    parts = plans[r][0][0] + (plans[r][0][1] if push else [])
-                    for cid, _, new in parts:
-                        if new:
-                            pool.import_fd(r, cid, fds.pop(0))
-                    for part, dst in ((plans[r][0][0], reg.peers), (plans[r][0][1] if push else None, scratch)):
-                        if part is None:
-                            continue
-                        view = vmm.MappedRange(self.lib, [pool.peer[(r, cid)] for cid, _, _ in part],
-                                               [sz for _, sz, _ in part])
-                        reg.vmm.append(view)
-                        dst.append(view.va)
-                finally:
-                    for fd in got.get(r, []):
-                        os.close(fd)
+                parts = plans[r][0][0] + (plans[r][0][1] if push else [])
+                for cid, _, new in parts:
+                    if new:
+                        pool.import_fd(r, cid, fds.pop(0))
+                for part, dst in ((plans[r][0][0], reg.peers), (plans[r][0][1] if push else None, scratch)):
+                    if part is None:
+                        continue
+                    view = vmm.MappedRange(self.lib, [pool.peer[(r, cid)] for cid, _, _ in part],
+                                           [sz for _, sz, _ in part])
+                    reg.vmm.append(view)
+                    dst.append(view.va)
         except Exception as e:   # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
+        finally:
+            for fl in got.values():             # every received fd, also after a failure midway
+                for fd in fl:
+                    os.close(fd)
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
             self.comm.server.call("barrier", self.rank)
+            # a chunk sent in THIS call may be missing on some peer: never hand it out again
+            sent = set(map(id, new_own))
+            reg.chunks = [c for c in reg.chunks if id(c) not in sent]
             self._release(reg)
+            pool.discard(new_own)
             raise Mp4jException(f"memAlloc({nbytes}) peer mapping failed on ranks "
                                 f"{[(i, o) for i, o in enumerate(oks) if o]}")
         reg.scratch = scratch if push else None

@@ -139,6 +139,16 @@ class ChunkPool:
         for c in chunks:
             self.free.setdefault(c.size, []).append(c)
 
+    def discard(self, chunks: List[Chunk]) -> None:
+        """Drop chunks for good (a failed allocation sent them and some peer may not hold
+        them): released, never handed out again."""
+        gone = set(map(id, chunks))
+        self.owned = [c for c in self.owned if id(c) not in gone]
+        for lst in self.free.values():
+            lst[:] = [c for c in lst if id(c) not in gone]
+        for c in chunks:
+            native.soft_check(self.lib.mp4x_vmm_chunk_release(c.handle), "vmm_chunk_release")
+
     def import_fd(self, rank: int, cid: int, fd: int) -> int:
         h = ctypes.c_uint64()
         check(self.lib.mp4x_vmm_chunk_import(fd, ctypes.byref(h)), "vmm_chunk_import")

@@ -176,3 +176,74 @@ def test_chunk_pool_reuses_chunks_across_sizes_and_sends_only_new_ones(monkeypat
     assert len(set(lib.released)) == len(lib.released)          # nothing released twice
     assert len(lib.released) == lib.creates + lib.imports        # ... and everything once, at close
     assert set(lib.released) <= owned_handles
+
+
+def test_chunks_sent_by_a_failed_allocation_are_never_reused(monkeypatch):
+    """A peer fails to import a new chunk: memAlloc raises on every rank, the chunks that
+    allocation sent are released and dropped (a peer may not hold them), and the next memAlloc
+    of that size creates and sends new ones — it does not map a chunk some peer never got."""
+    p = 3
+    tls = threading.local()
+    lib = _VmmLib(tls)
+    orig_import = lib.mp4x_vmm_chunk_import
+    fail = {"on": False}
+
+    def flaky_import(fd, h):
+        if fail["on"] and tls.rank == 2:
+            return 1
+        return orig_import(fd, h)
+    lib.mp4x_vmm_chunk_import = flaky_import
+    monkeypatch.setattr(ipc_mod, "VMM_POLICY", "chunks")
+    monkeypatch.setattr(ipc_mod, "PUSH_ON", True)
+    monkeypatch.setattr(ipc_mod.native, "hip", lambda: lib)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
+    monkeypatch.setattr(ipc_mod.torch.cuda, "synchronize", lambda *a, **k: None)
+    monkeypatch.setattr(vmm, "tensor_at", lambda ptr, nb, dt, dev, owner=None: _T(ptr))
+    server = _Server(p)
+    out = [None] * p
+    errs = []
+
+    def run(r):
+        tls.rank = r
+        try:
+            inst = ipc_mod.IpcAllreduce(_Comm(server, r), nbytes=1 << 16)
+            t = inst.mem_alloc(10 * MiB, ipc_mod.torch.float32)
+            inst.mem_free(t)
+            server.call("barrier", r)
+            if r == 0:
+                fail["on"] = True
+            server.call("barrier", r)
+            raised = False
+            try:
+                inst.mem_alloc(12 * MiB, ipc_mod.torch.float32)      # a new 4 MiB chunk: import fails on rank 2
+            except Mp4jException:
+                raised = True
+            server.call("barrier", r)
+            if r == 0:
+                fail["on"] = False
+            server.call("barrier", r)
+            released_before = len(lib.released)
+            t = inst.mem_alloc(12 * MiB, ipc_mod.torch.float32)
+            reg = inst._regs[(t.data_ptr(), 12 * MiB)]
+            views = [lib.maps[v] for v in reg.peers]
+            inst.mem_free(t)
+            out[r] = (raised, views, sorted(c.size for c in inst._chunk_pool.owned), released_before, inst)
+        except Exception as e:   # noqa: BLE001
+            errs.append((r, repr(e)))
+            raise
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(p)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(60)
+    assert not any(t.is_alive() for t in threads) and not errs, errs
+    for r, (raised, views, owned, released_before, _) in enumerate(out):
+        assert raised                                             # every rank, together
+        for j in range(p):                                        # the retry maps real chunks everywhere
+            assert [int(tag.split(":")[0]) for tag in views[j]] == [j] * len(views[j])
+            assert views[j] == out[j][1][j]
+        assert owned.count(4 * MiB) == 1                          # the discarded 4 MiB chunk is gone
+        assert released_before >= p                               # ... released (one per rank at least)
+    for *_, inst in out:
+        inst.close(sync=False)
