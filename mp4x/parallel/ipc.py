@@ -283,6 +283,7 @@ class IpcAllreduce:
         self.sig_ptrs: List[int] = []
         err = None
         got = {}
+        got = {}
         if self._vmm_data:
             from . import vmm
             try:
@@ -300,11 +301,7 @@ class IpcAllreduce:
                 for i, lst in ((0, self.data_ptrs), (1, self.sig_ptrs)):
                     if i == 0 and self._vmm_data:
                         own = self._data_regions[0]
-                        try:
-                            pr = vmm.VmmRegion.import_fds(self.lib, got[r], own.chunk)
-                        finally:
-                            for fd in got[r]:
-                                os.close(fd)
+                        pr = vmm.VmmRegion.import_fds(self.lib, got[r], own.chunk)
                         self._data_regions.append(pr)
                         lst.append(pr.va)
                         continue
@@ -315,6 +312,10 @@ class IpcAllreduce:
                     lst.append(ptr.value)
         except Exception as e:   # decide collectively: every rank enables IPC or none does
             err = str(e)
+        finally:
+            for fl in got.values():             # every received fd, also after a failure midway
+                for fd in fl:
+                    os.close(fd)
         oks, anybad = _agree(comm, self.rank, b"" if err is None else err.encode(), bool)
         if anybad:
             self.close(sync=False)
@@ -844,19 +845,19 @@ class IpcAllreduce:
                     continue
                 chunk, n, schunk, sn = plans[r][0]
                 fds = got[r]
-                try:
-                    pr = vmm.VmmRegion.import_fds(self.lib, fds[:n], chunk)
-                    reg.vmm.append(pr)
-                    reg.peers.append(pr.va)
-                    if push:
-                        ps = vmm.VmmRegion.import_fds(self.lib, fds[n:n + sn], schunk)
-                        reg.vmm.append(ps)
-                        scratch.append(ps.va)
-                finally:
-                    for fd in fds:
-                        os.close(fd)
+                pr = vmm.VmmRegion.import_fds(self.lib, fds[:n], chunk)
+                reg.vmm.append(pr)
+                reg.peers.append(pr.va)
+                if push:
+                    ps = vmm.VmmRegion.import_fds(self.lib, fds[n:n + sn], schunk)
+                    reg.vmm.append(ps)
+                    scratch.append(ps.va)
         except Exception as e:   # noqa: BLE001
             err = f"{type(e).__name__}: {e}"
+        finally:
+            for fl in got.values():             # every received fd, also after a failure midway
+                for fd in fl:
+                    os.close(fd)
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
             self.comm.server.call("barrier", self.rank)
