@@ -134,6 +134,7 @@ class DeviceEngine(AutotuneMixin):
     hier_min_bytes = 1 << 20
     _probe_depth = 0
     _probe_s: Optional[float] = None      # explicit bound of the innermost probing(seconds) scope
+    _zc_vmm = True                        # memAlloc builds VMM tensors (False: registered plain ones)
     _ipc_obj = _ipc_large = _ipc_fp8_big = None
 
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
@@ -341,7 +342,16 @@ class DeviceEngine(AutotuneMixin):
                 self.ipc_enabled = False
                 return None
             bad = self._ipc_self_test(inst)
-            if bad and all(": zero_copy_" in b for b in bad):
+            if bad and all(": zero_copy_memalloc" in b for b in bad):
+                # only the memAlloc (VMM-imported) region failed: registered caching-allocator
+                # tensors keep the zero-copy forms; memAlloc hands out registered plain tensors
+                # (up to the IPC open limit) instead of VMM ones (the verdict is agreed)
+                LOG.warning("rank %d: IPC memAlloc zero-copy self-test failed (%s): memAlloc falls back to "
+                            "registered plain tensors on every rank", self.rank, bad)
+                self._zc_vmm = False
+                self.ipc_selftest = dict(self.ipc_selftest or {}, zero_copy_memalloc=False)
+                bad = None
+            elif bad and all(": zero_copy_" in b for b in bad):
                 # only the zero-copy forms failed (identically known on every rank: the verdict is
                 # agreed): keep the staged kernels, run registered / memAlloc tensors staged
                 LOG.warning("rank %d: IPC zero-copy self-test failed (%s): zero-copy forms disabled on every rank, "
@@ -527,6 +537,8 @@ class DeviceEngine(AutotuneMixin):
             fails.append(f"set_spin: {e}")
         if os.environ.get("MP4X_IPC_SELFTEST_INJECT", "").strip() == str(r):   # failure-path tests
             fails.append("injected failure (MP4X_IPC_SELFTEST_INJECT)")
+        if os.environ.get("MP4X_IPC_SELFTEST_INJECT_MEMALLOC", "").strip() == str(r):
+            fails.append("zero_copy_memalloc_1MiB: injected failure (MP4X_IPC_SELFTEST_INJECT_MEMALLOC)")
         allf = self.comm.server.call("allgather_obj", self.rank, fails)
         bad = [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
         self.ipc_selftest = {"ok": not bad, "failures": bad, "seconds": round(time.perf_counter() - t0, 3)}
@@ -811,16 +823,29 @@ class DeviceEngine(AutotuneMixin):
     def mem_alloc(self, n: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
         """Collective: an ``n``-element tensor mapped into every peer at any size (see
         ``IpcAllreduce.mem_alloc``), or None on every rank when there is no IPC mesh (the
-        caller then allocates a plain tensor: the staged kernels / RCCL serve it)."""
-        if not self._zc or self.p < 2 or self.device.type != "cuda" or self.ipc() is None:
+        caller then allocates a plain tensor: the staged kernels / RCCL serve it).  When only
+        the memAlloc self-test failed on this topology, a plain tensor registered with the peers
+        (hipIpc, up to the IPC open limit) stands in for the VMM one."""
+        if self.p < 2 or self.device.type != "cuda" or self.ipc() is None or not self._zc:
             return None
         es = torch.empty((), dtype=dtype).element_size()
+        if not self._zc_vmm:
+            from .ipc import IPC_OPEN_MAX
+            if n * es > IPC_OPEN_MAX:
+                return None
+            t = torch.empty(n, dtype=dtype, device=self.device)
+            self._ipc_obj.register(self._flat(t))         # collective; False = staged, still correct
+            return t
         return self._ipc_obj.mem_alloc(n * es, dtype)
 
     def mem_free(self, t: torch.Tensor) -> None:
-        if self._ipc_obj is not None and self._ipc_obj._find(t)[0] is not None \
-                and self._ipc_obj._find(t)[0].vmm:
+        if self._ipc_obj is None:
+            return
+        reg = self._ipc_obj._find(t)[0]
+        if reg is not None and reg.vmm:
             self._ipc_obj.mem_free(t)
+        elif reg is not None and not self._zc_vmm:
+            self._ipc_obj.deregister(self._flat(t))      # the registered stand-in of mem_alloc
 
     def _run_allreduce(self, algo: str, view: torch.Tensor, op, scale: float = 1.0,
                        capturing: Optional[bool] = None) -> bool:

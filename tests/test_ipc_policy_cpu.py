@@ -253,15 +253,18 @@ def test_process_barrier_and_close_surface_a_timed_out_collective():
     assert code == 1
 
 
-@pytest.mark.parametrize("fails,zc,enabled", [
-    (["rank 1: zero_copy_memalloc_1MiB: 12 wrong elements"], False, True),      # zero-copy only: staged kept
+@pytest.mark.parametrize("fails,zc,enabled,zc_vmm", [
+    (["rank 1: zero_copy_memalloc_1MiB: 12 wrong elements"], True, True, False),   # memAlloc only
+    (["rank 0: zero_copy_twoshot_and_plans_4MiB: 5 wrong elements",
+      "rank 1: zero_copy_memalloc_1MiB: 12 wrong elements"], False, True, True),   # zero-copy: staged kept
     (["rank 0: zero_copy_twoshot_and_plans_4MiB: barrier timeout 2", "rank 1: twoshot_4MiB: 3 wrong elements"],
-     True, False),                                                              # a core family: IPC off
-    (None, True, True)])
-def test_self_test_failure_scope(monkeypatch, fails, zc, enabled):
-    """A failed zero-copy self-test drops only the zero-copy forms on every rank (registered /
-    memAlloc tensors then run staged); any other failure disables IPC (the verdict is agreed, so
-    every rank takes the same branch)."""
+     True, False, True),                                                            # a core family: IPC off
+    (None, True, True, True)])
+def test_self_test_failure_scope(monkeypatch, fails, zc, enabled, zc_vmm):
+    """A failed memAlloc self-test alone drops only the VMM-built memAlloc (registered plain
+    tensors stand in); a failed zero-copy self-test drops the zero-copy forms on every rank
+    (registered / memAlloc tensors then run staged); any other failure disables IPC (the verdict
+    is agreed, so every rank takes the same branch)."""
     import mp4x.parallel.ipc as ipcm
 
     class _FakeInst:
@@ -278,5 +281,5 @@ def test_self_test_failure_scope(monkeypatch, fails, zc, enabled):
     e.comm, e.rank = object(), 0
     e._ipc_self_test = lambda inst: fails
     got = e.ipc()
-    assert e._zc is zc and e.ipc_enabled is enabled
+    assert e._zc is zc and e.ipc_enabled is enabled and e._zc_vmm is zc_vmm
     assert (got is not None) is enabled and _FakeInst.closed is (not enabled)

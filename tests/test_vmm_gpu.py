@@ -139,3 +139,34 @@ def test_fp8_whole_tensor_staging_built_from_vmm():
         assert nbad == 0, (r, nbad)
         assert stats.get("allreduce.fp8.ipc", 0) == 1, stats
         assert is_vmm and nb >= n * 260 // 256, (is_vmm, nb)
+
+
+def _standin_fn(comm, n):
+    from mp4x import Operands, Operators
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    t = comm.memAlloc(n, torch.float32)
+    reg = eng._ipc_obj._find(t)[0]
+    kind = (reg is not None, bool(reg.vmm) if reg is not None else None)
+    i = torch.arange(n, device="cuda", dtype=torch.int32) % 13
+    t.copy_(i + r)
+    before = dict(eng.stats)
+    comm.allreduceArray(t, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
+    torch.cuda.synchronize()
+    bad = int((t != (i * p + p * (p - 1) // 2).float()).sum())
+    used = {k: v - before.get(k, 0) for k, v in eng.stats.items() if v != before.get(k, 0)}
+    comm.memFree(t)
+    return kind, bad, used, eng._zc, eng._zc_vmm, eng._ipc_obj._find(t)[0] is None
+
+
+def test_memalloc_falls_back_to_registered_plain_tensors_when_only_its_self_test_fails():
+    """The memAlloc (VMM) self-test fails on one rank (injected): every rank keeps the zero-copy
+    forms for registered tensors, memAlloc hands out a registered plain tensor, the allreduce on
+    it is the zero-copy two-shot and exact, memFree deregisters it."""
+    n = (8 << 20) // 4
+    out = run_spawn(2, _standin_fn, args=(n,), env={"MP4X_IPC_SELFTEST_INJECT_MEMALLOC": "1"})
+    for r, (kind, bad, used, zc, zc_vmm, gone) in out.items():
+        assert zc and not zc_vmm, (r, zc, zc_vmm)
+        assert kind == (True, False), kind                  # registered, not VMM-built
+        assert bad == 0 and used.get("allreduce.ipc2z", 0) + used.get("allreduce.ipc2w", 0) == 1, used
+        assert gone
