@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Diagnose the rooted autotune probe at 1 MiB (broadcast / gather / scatter 'ipc' ruled out in
+the 4-rank bench rehearsal): p ranks on one GPU, the agreement values of every probe recorded per
+rank.  python tools/diag/rooted_probe.py [p]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def fn(comm, sizes):
+    import torch
+    eng = comm.device
+    eng.ipc()
+    log = []
+    orig = eng._agree
+
+    def agree(flags):
+        out = orig(flags)
+        log.append((list(flags), out))
+        return out
+    eng._agree = agree
+    res = {}
+    for nb in sizes:
+        like = torch.empty(nb // 4, device="cuda")
+        for kind in ("reduce", "broadcast", "gather", "scatter"):
+            mark = len(log)
+            from mp4x import Operators
+            r = getattr(eng, "autotune_" + kind)(like, Operators.Float.SUM) if kind == "reduce" else \
+                getattr(eng, "autotune_" + kind)(like)
+            res[f"{nb}:{kind}"] = {"times": r, "agree": log[mark:]}
+    return res
+
+
+if __name__ == "__main__":
+    from spawn_ranks import run_spawn
+    p = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    out = run_spawn(p, fn, args=([1 << 20, 16 << 20],), timeout=300)
+    for r in sorted(out):
+        print(json.dumps({"rank": r, "res": out[r]}, default=str))
