@@ -11,10 +11,24 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def fn(comm, sizes):
+def fn(comm, sizes, pre=""):
     import torch
+    from mp4x import Operands, Operators
     eng = comm.device
     eng.ipc()
+    op = Operators.Float.SUM
+    if "head" in pre:            # bench.py's sequence before its rooted sweep
+        n = 250_000_000
+        buf = torch.randn(n, device="cuda")
+        comm.registerBuffer(buf)
+        if "tune1g" in pre:
+            eng.autotune_allreduce(buf, op, iters=5)
+        for _ in range(5):
+            comm.allreduceArray(buf, Operands.FLOAT_OPERAND(), op, 0, n, scale=0.25)
+        torch.cuda.synchronize()
+    if "tiers" in pre:
+        for nb in (65536, 4194304):
+            eng.autotune_allreduce(torch.empty(nb // 4, device="cuda"), op, iters=3)
     log = []
     orig = eng._agree
 
@@ -38,6 +52,7 @@ def fn(comm, sizes):
 if __name__ == "__main__":
     from spawn_ranks import run_spawn
     p = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    out = run_spawn(p, fn, args=([1 << 20, 16 << 20],), timeout=300)
+    pre = sys.argv[2] if len(sys.argv) > 2 else ""
+    out = run_spawn(p, fn, args=([1 << 20, 16 << 20], pre), timeout=300)
     for r in sorted(out):
         print(json.dumps({"rank": r, "res": out[r]}, default=str))
