@@ -43,8 +43,9 @@ def fn(comm, sizes, pre=""):
         for kind in ("reduce", "broadcast", "gather", "scatter"):
             mark = len(log)
             from mp4x import Operators
-            r = getattr(eng, "autotune_" + kind)(like, Operators.Float.SUM) if kind == "reduce" else \
-                getattr(eng, "autotune_" + kind)(like)
+            root = int(os.environ.get("DIAG_ROOT", comm.getSlaveNum() - 1))     # bench.py uses p - 1
+            r = getattr(eng, "autotune_" + kind)(like, Operators.Float.SUM, root=root) if kind == "reduce" else \
+                getattr(eng, "autotune_" + kind)(like, root=root)
             res[f"{nb}:{kind}"] = {"times": r, "agree": log[mark:]}
     return res
 
