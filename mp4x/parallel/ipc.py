@@ -86,9 +86,9 @@ DATA_COARSE = os.environ.get("MP4X_IPC_DATA_MEM", "uncached").lower() == "coarse
 # registration refuses such allocations (every rank alike): the staged kernels run instead.
 IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 # Memory lifetime (diagnosed with tools/repro/ipc_lifetime_repro.hip):
-# CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' TENSOR allocations
-#   (refcounted per allocation) instead of caching every mapping until close(); push scratches are
-#   pooled per power-of-two size class and their peer mappings kept (see _alloc_scratch);
+# CLOSE_PEERS — a deregistration closes this rank's mappings of the peers' allocations (refcounted
+#   per allocation) and frees its push scratch, instead of caching every mapping and pooling every
+#   scratch until close();
 # VMM_POLICY — how memAlloc / memFree manage memory (tests/test_vmm_policy_gpu.py measures every
 #   one for exactness and device-memory growth; tools/repro/ipc_lifetime_repro.hip shows, in plain
 #   HIP, why only the first and "fresh_va" / "pool" are exact on this runtime):
@@ -174,7 +174,7 @@ def _agree(comm, rank, obj, is_bad):
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "scratch_keys", "chunks")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "chunks")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
@@ -183,8 +183,7 @@ class _Reg:
         self.scratch_alloc = None        # own push scratch: (allocation, IPC handle bytes)
         self.vmm: list = []              # memAlloc: own regions first (nown of them), then imported
         self.nown = 0
-        self.peer_keys: list = []        # (rank, handle bytes) of every peer tensor mapping this one uses
-        self.scratch_keys: list = []     # ... and of the peers' push scratches (pooled: kept mapped)
+        self.peer_keys: list = []        # (rank, handle bytes) of every peer mapping this one uses
         self.chunks = None               # memAlloc under the chunk pool: this rank's chunks
 
 
@@ -630,7 +629,7 @@ class IpcAllreduce:
                 if push:
                     sk = (r, bytes(b[4]))
                     scr.append(self._open_peer_base(sk, hs))
-                    reg.scratch_keys.append(sk)
+                    reg.peer_keys.append(sk)
         except Exception as e:   # noqa: BLE001
             err = str(e)
         reg.scratch = scr if push else None
@@ -659,16 +658,15 @@ class IpcAllreduce:
         self._peer_refs[hk] = self._peer_refs.get(hk, 0) + 1
         return ent.value
 
-    def _close_peer(self, hk, close: bool = True) -> None:
+    def _close_peer(self, hk) -> None:
         """Drop one registration's use of peer mapping ``hk``; the last one closes it
-        (``CLOSE_PEERS`` and ``close``; otherwise it stays cached until close() — the mappings of
-        the peers' pooled push scratches always do, see :meth:`_free_scratch`)."""
+        (``CLOSE_PEERS``; otherwise it stays cached until close())."""
         n = self._peer_refs.get(hk, 0) - 1
         if n > 0:
             self._peer_refs[hk] = n
             return
         self._peer_refs.pop(hk, None)
-        if CLOSE_PEERS and close:
+        if CLOSE_PEERS:
             ptr = self._peer_bases.pop(hk, None)
             if ptr is not None:
                 native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
@@ -677,17 +675,12 @@ class IpcAllreduce:
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
         slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
         (allocation, IPC handle), or (None, None): the registration then has no push form.
-        Sizes are rounded up to a power of two (64 KiB at least) and a scratch an earlier
-        deregistration returned is reused: scratches are pooled, never freed before close()
-        (the peers keep their mappings of them), so the pool is bounded by the size classes in
-        use.  Freeing a scratch that peers had mapped and opening the next fine-grained
-        allocations corrupted later collectives on this runtime (4-rank bench rehearsal, round 4:
-        ruled out by the rooted probes only with the scratch freed and the mappings closed)."""
+        Without ``CLOSE_PEERS``, a scratch of the same size that an earlier deregistration
+        returned is reused (the peers' mappings of it stay cached by handle)."""
         chunk = -(-(nbytes // 16) // self.p)
-        need = max(16, (self.p - 1) * chunk * 16)
-        size = max(64 << 10, 1 << (need - 1).bit_length())
+        size = max(16, (self.p - 1) * chunk * 16)
         pooled = self._scratch_pool.get(size)
-        if pooled:
+        if pooled and not CLOSE_PEERS:
             return pooled.pop()
         ptr = c_void_p()
         try:
@@ -704,10 +697,15 @@ class IpcAllreduce:
         return ptr, h.raw
 
     def _free_scratch(self, scr) -> None:
-        """Park a push scratch in the per-size-class pool (freed at close(); see
-        :meth:`_alloc_scratch`)."""
+        """Free a push scratch (``CLOSE_PEERS``: its peers close their mappings at their own
+        deregistration; until then the driver keeps the memory alive for them), or park it in
+        the per-size pool (freed at close())."""
         if scr and scr[0]:
-            self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
+            if CLOSE_PEERS:
+                self._scratch_size.pop(scr[0].value, None)
+                native.soft_check(self.lib.mp4x_ipc_free(scr[0]), "ipc_free", LOG)
+            else:
+                self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
     def _release(self, reg: "_Reg") -> None:
         """Release what ``reg`` holds on this rank: its scratch, its uses of the peer mappings
@@ -718,9 +716,6 @@ class IpcAllreduce:
         for hk in reg.peer_keys:
             self._close_peer(hk)
         reg.peer_keys = []
-        for hk in reg.scratch_keys:           # the peers' pooled scratches: mappings stay cached
-            self._close_peer(hk, close=False)
-        reg.scratch_keys = []
         for i in reversed(range(len(reg.vmm))):   # the peers' imported views first, own memory last
             reg.vmm[i].free(self._keep_va(own=i < reg.nown))
         reg.vmm = []
