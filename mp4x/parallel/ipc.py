@@ -605,6 +605,9 @@ class IpcAllreduce:
         allb = self.comm.server.call("allgather_obj", self.rank, (blob, err))
         errs = [(i, e) for i, (_, e) in enumerate(allb) if e]
         if errs or len({b[2] for b, _ in allb}) != 1:
+            if self.rank == 0:            # agreed: every rank returns False; say why once
+                LOG.warning("registerBuffer(%d bytes) refused: %s", key[1],
+                            errs or f"sizes differ across ranks {[b[2] for b, _ in allb]}")
             self._free_scratch(scr_alloc)
             return False
         if all(b[3] for b, _ in allb):
@@ -636,6 +639,9 @@ class IpcAllreduce:
         reg.scratch_alloc = scr_alloc
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
+            if self.rank == 0:
+                LOG.warning("registerBuffer(%d bytes): peer mapping failed on ranks %s", key[1],
+                            [(i, o) for i, o in enumerate(oks) if o])
             self._release(reg)
             return False
         old = self._regs.get(key)
