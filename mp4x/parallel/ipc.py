@@ -106,11 +106,6 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 #   "pool":           park the allocation in a per-size pool that the next memAlloc of that size
 #                     reuses (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
-# Diagnostic split of CLOSE_PEERS for the push scratches (profiles/r4/rooted/: a freed scratch and
-# closed scratch mappings preceded wrong rooted results in the 4-rank rehearsal): with either set
-# to 0 the scratches are pooled / their peer mappings kept.  Defaults = the CLOSE_PEERS policy.
-SCRATCH_FREE = os.environ.get("MP4X_IPC_SCRATCH_FREE", "1") == "1"
-SCRATCH_CLOSE = os.environ.get("MP4X_IPC_SCRATCH_CLOSE", "1") == "1"
 VMM_POLICIES = ("chunks", "fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
 VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
     "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "chunks")
@@ -179,7 +174,7 @@ def _agree(comm, rank, obj, is_bad):
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "scratch_keys", "chunks")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "chunks")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
@@ -188,8 +183,7 @@ class _Reg:
         self.scratch_alloc = None        # own push scratch: (allocation, IPC handle bytes)
         self.vmm: list = []              # memAlloc: own regions first (nown of them), then imported
         self.nown = 0
-        self.peer_keys: list = []        # (rank, handle bytes) of every peer tensor mapping this one uses
-        self.scratch_keys: list = []     # ... and of the peers' push scratches
+        self.peer_keys: list = []        # (rank, handle bytes) of every peer mapping this one uses
         self.chunks = None               # memAlloc under the chunk pool: this rank's chunks
 
 
@@ -638,7 +632,7 @@ class IpcAllreduce:
                 if push:
                     sk = (r, bytes(b[4]))
                     scr.append(self._open_peer_base(sk, hs))
-                    reg.scratch_keys.append(sk)
+                    reg.peer_keys.append(sk)
         except Exception as e:   # noqa: BLE001
             err = str(e)
         reg.scratch = scr if push else None
@@ -670,15 +664,15 @@ class IpcAllreduce:
         self._peer_refs[hk] = self._peer_refs.get(hk, 0) + 1
         return ent.value
 
-    def _close_peer(self, hk, close: bool = True) -> None:
+    def _close_peer(self, hk) -> None:
         """Drop one registration's use of peer mapping ``hk``; the last one closes it
-        (``CLOSE_PEERS`` and ``close``; otherwise it stays cached until close())."""
+        (``CLOSE_PEERS``; otherwise it stays cached until close())."""
         n = self._peer_refs.get(hk, 0) - 1
         if n > 0:
             self._peer_refs[hk] = n
             return
         self._peer_refs.pop(hk, None)
-        if CLOSE_PEERS and close:
+        if CLOSE_PEERS:
             ptr = self._peer_bases.pop(hk, None)
             if ptr is not None:
                 native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
@@ -692,7 +686,7 @@ class IpcAllreduce:
         chunk = -(-(nbytes // 16) // self.p)
         size = max(16, (self.p - 1) * chunk * 16)
         pooled = self._scratch_pool.get(size)
-        if pooled and not (CLOSE_PEERS and SCRATCH_FREE):
+        if pooled and not CLOSE_PEERS:
             return pooled.pop()
         ptr = c_void_p()
         try:
@@ -713,7 +707,7 @@ class IpcAllreduce:
         deregistration; until then the driver keeps the memory alive for them), or park it in
         the per-size pool (freed at close())."""
         if scr and scr[0]:
-            if CLOSE_PEERS and SCRATCH_FREE:
+            if CLOSE_PEERS:
                 self._scratch_size.pop(scr[0].value, None)
                 native.soft_check(self.lib.mp4x_ipc_free(scr[0]), "ipc_free", LOG)
             else:
@@ -728,9 +722,6 @@ class IpcAllreduce:
         for hk in reg.peer_keys:
             self._close_peer(hk)
         reg.peer_keys = []
-        for hk in reg.scratch_keys:           # the peers' push scratches
-            self._close_peer(hk, close=SCRATCH_CLOSE)
-        reg.scratch_keys = []
         for i in reversed(range(len(reg.vmm))):   # the peers' imported views first, own memory last
             reg.vmm[i].free(self._keep_va(own=i < reg.nown))
         reg.vmm = []
