@@ -102,7 +102,7 @@ def _timed_p50(torch, fn, iters, sync):
     return sorted(ts)[len(ts) // 2]
 
 
-def _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev):
+def _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev, may_start=lambda name: True):
     """BASELINE configs 3 / 4 / 5 on this job (evidence; each bounded, failures recorded, every
     rank stops together).  Exact checks for 3 and 4, the fp64 error bound for 5."""
     from mp4x import CommUtils, Operands, Operators
@@ -187,6 +187,8 @@ def _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev):
 
     for name, fn in (("config3_rs_ag_4gb_bf16", cfg3), ("config4_sparse_200k_x64", cfg4),
                      ("config5_fp8_8gb", cfg5)):
+        if not may_start(name):          # the extras' wall-time budget is spent (agreed)
+            continue
         failed = 0.0
         try:
             out[name] = fn()
@@ -367,59 +369,6 @@ def main():
         finally:
             eng.algo = saved
 
-    # after the timed steps (never inside them): measure every schedule at the size classes
-    # the IPC tiers are chosen for, so a multi-GPU run records the tier boundaries on real links
-    tiers = None
-    if p > 1 and not args.cpu and not args.no_tier_sweep and not (args.algo or args.codec):
-        tiers = {}
-        for nb in [int(x) for x in args.sweep_sizes.split(",") if x.strip()]:
-            failed = 0.0
-            try:
-                res = comm.device.autotune_allreduce(torch.empty(nb // 4, device=dev), op, iters=3)
-                tiers[str(nb)] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in res.items()}
-            except Exception as e:   # noqa: BLE001 — evidence only; the headline is already measured
-                tiers[str(nb)] = {"error": str(e)[:200]}
-                failed = 1.0
-            # every rank stops together (a rank-local failure must not leave the others waiting
-            # in the next size's collectives)
-            flag = torch.tensor([failed], dtype=torch.float64, device=agree_dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            if flag.item() > 0:
-                break
-        # the rooted collectives' schedules (RCCL vs IPC copy plans / two-shot vs composites)
-        # at sizes on both sides of the IPC direct tier, recorded the same way
-        rooted = {}
-        for nb in () if args.no_rooted_sweep else (1 << 20, 16 << 20, 128 << 20):
-            failed = 0.0
-            like = torch.empty(nb // 4, device=dev)
-            row = {}
-            try:
-                for kind, fn in (("reduce", lambda: comm.device.autotune_reduce(like, op, root=p - 1)),
-                                 ("broadcast", lambda: comm.device.autotune_broadcast(like, root=p - 1)),
-                                 ("gather", lambda: comm.device.autotune_gather(like, root=p - 1)),
-                                 ("scatter", lambda: comm.device.autotune_scatter(like, root=p - 1))):
-                    row[kind] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in fn().items()}
-            except Exception as e:   # noqa: BLE001 — evidence only
-                row["error"] = str(e)[:200]
-                failed = 1.0
-            rooted[str(nb)] = row
-            flag = torch.tensor([failed], dtype=torch.float64, device=agree_dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-            if flag.item() > 0:
-                break
-        tiers["rooted"] = rooted
-
-    # the other BASELINE.json configs at this rank count, after everything above (never timed with
-    # the headline): config 3 (RS + AG of a 4 GB bf16 memAlloc tensor), config 4 (sparse rows,
-    # 200k keys x float[64] per rank, half shared), config 5 (8 GB f32 allreduce, fp8 wire codec)
-    configs = None
-    if p > 1 and not args.cpu and not args.no_configs and not (args.algo or args.codec):
-        # a bounded IPC spin (60 s) for these evidence runs: a kernel that cannot complete raises
-        # (recorded, every rank stops together) long before the watchdog's 600 s would end the
-        # whole job and lose the headline line
-        with comm.device.probing(float(os.environ.get("MP4X_BENCH_CONFIG_SPIN_S", 60))):
-            configs = _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev)
-
     ref = REF_BUSBW_MBPS.get(p)
     topo = None
     if rank == 0 and not args.cpu:
@@ -438,9 +387,12 @@ def main():
     ipc_inst = None if (p == 1 or args.cpu) else comm.device._ipc_obj
     ipc_info = None if ipc_inst is None else {"spin_s": ipc_inst.spin_s, "share": ipc_inst.share,
                                               "grid_caps": ipc_inst.grid_caps_summary()}
-    stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items() if k.startswith("allreduce")}
-    if rank == 0:
-        rec = {
+
+    def record(phase, tiers=None, configs=None, extras=None):
+        stats = None if (p == 1 or args.cpu) else {k: v for k, v in comm.device.stats.items()
+                                                   if k.startswith("allreduce")}
+        probes = None if (p == 1 or args.cpu) else list(comm.device.probe_failures)
+        return {
             "metric": METRIC,
             "value": round(busbw, 3),
             "unit": "GB/s",
@@ -459,7 +411,8 @@ def main():
                        "alloc": args.alloc if p > 1 else "n/a", "registered": registered if p > 1 else "n/a",
                        "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
                        "autotune_iters": args.autotune_iters, "ipc_selftest": selftest, "ipc": ipc_info,
-                       "calls": stats, "tier_sweep_ms": tiers, "baseline_configs": configs, "topology": topo},
+                       "probe_failures": probes, "calls": stats, "tier_sweep_ms": tiers,
+                       "baseline_configs": configs, "extras": extras, "topology": topo},
             "verified": verified,
             "max_abs_err": max_err,
             "busbw_gbps_per_rank": round(busbw, 3),
@@ -471,13 +424,98 @@ def main():
             "rccl_p50_ms": rccl["rccl_p50_ms"] if rccl else None,
             "rccl_baseline": rccl,
             "busbw_factor": factor,
+            "phase": phase,
             "note": ("p=1: nothing crosses a link (nccl-tests busbw factor 2(p-1)/p = 0), so this is "
                      "busbw := algbw of the out-of-place single-rank allreduce, a 1 GB HBM copy through K1; "
                      "N>=2 values are xGMI-link-bound and not comparable to N=1 as a scaling base"
                      if p == 1 else "value = busbw = algbw * 2(p-1)/p (nccl-tests convention, per rank); "
                                     "aggregate_busbw_gbps = p * busbw; rccl_* = the same call with RCCL forced"),
         }
-        print(json.dumps(rec), flush=True)
+
+    # ---- the headline is measured, verified and next to RCCL: print it NOW, so nothing that runs
+    # after it (sweeps, baseline configs) can lose it by hanging or overrunning the driver's timeout
+    if rank == 0:
+        print(json.dumps(record("headline")), flush=True)
+
+    # ---- evidence after the headline, under ONE wall-time budget (MP4X_BENCH_EXTRA_S, default
+    # 240 s): each stage starts only while the budget lasts (decided on the MAX elapsed over ranks,
+    # so every rank starts or skips the same stages); what was skipped is recorded
+    budget = float(os.environ.get("MP4X_BENCH_EXTRA_S", 240))
+    t_extra = time.perf_counter()
+    extras = {"budget_s": budget, "skipped": [], "seconds": None}
+    if os.environ.get("MP4X_BENCH_TEST_HANG") == "extras" and rank == 0:
+        time.sleep(3600)             # test hook: a stage that never returns (tests/test_launch_cpu.py)
+
+    def budget_left(stage) -> bool:
+        if budget <= 0:
+            extras["skipped"].append(stage)
+            return False
+        el = max_over_ranks([time.perf_counter() - t_extra])[0]
+        if el >= budget:
+            extras["skipped"].append(stage)
+            return False
+        return True
+
+    def agreed_failure(failed) -> bool:
+        # every rank stops together (a rank-local failure must not leave the others waiting in the
+        # next stage's collectives)
+        return max_over_ranks([failed])[0] > 0
+
+    # measure every schedule at the size classes the IPC tiers are chosen for, so a multi-GPU run
+    # records the tier boundaries on real links
+    tiers = None
+    gpu_extras = p > 1 and not args.cpu and not (args.algo or args.codec)
+    if gpu_extras and not args.no_tier_sweep:
+        tiers = {}
+        for nb in [int(x) for x in args.sweep_sizes.split(",") if x.strip()]:
+            if not budget_left(f"tier_sweep:{nb}"):
+                continue
+            failed = 0.0
+            try:
+                res = comm.device.autotune_allreduce(torch.empty(nb // 4, device=dev), op, iters=3)
+                tiers[str(nb)] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in res.items()}
+            except Exception as e:   # noqa: BLE001 — evidence only; the headline is already printed
+                tiers[str(nb)] = {"error": str(e)[:200]}
+                failed = 1.0
+            if agreed_failure(failed):
+                break
+        # the rooted collectives' schedules (RCCL vs IPC copy plans / two-shot) at sizes on both
+        # sides of the IPC direct tier, recorded the same way
+        rooted = {}
+        for nb in () if args.no_rooted_sweep else (1 << 20, 16 << 20, 128 << 20):
+            if not budget_left(f"rooted_sweep:{nb}"):
+                continue
+            failed = 0.0
+            like = torch.empty(nb // 4, device=dev)
+            row = {}
+            try:
+                for kind, fn in (("reduce", lambda: comm.device.autotune_reduce(like, op, root=p - 1)),
+                                 ("broadcast", lambda: comm.device.autotune_broadcast(like, root=p - 1)),
+                                 ("gather", lambda: comm.device.autotune_gather(like, root=p - 1)),
+                                 ("scatter", lambda: comm.device.autotune_scatter(like, root=p - 1))):
+                    row[kind] = {k: (round(v * 1e3, 4) if v != float("inf") else None) for k, v in fn().items()}
+            except Exception as e:   # noqa: BLE001 — evidence only
+                row["error"] = str(e)[:200]
+                failed = 1.0
+            rooted[str(nb)] = row
+            if agreed_failure(failed):
+                break
+        tiers["rooted"] = rooted
+
+    # the other BASELINE.json configs at this rank count (never timed with the headline): config 3
+    # (RS + AG of a 4 GB bf16 memAlloc tensor), config 4 (sparse rows, 200k keys x float[64] per
+    # rank, half shared), config 5 (8 GB f32 allreduce, fp8 wire codec)
+    configs = None
+    if gpu_extras and not args.no_configs:
+        if budget_left("baseline_configs"):
+            # a bounded IPC spin (60 s) for these evidence runs: a kernel that cannot complete raises
+            # (recorded, every rank stops together) long before the watchdog's 600 s would end the job
+            with comm.device.probing(float(os.environ.get("MP4X_BENCH_CONFIG_SPIN_S", 60))):
+                configs = _baseline_configs(comm, torch, dist, p, rank, dev, agree_dev,
+                                            lambda name: budget_left(name))
+    extras["seconds"] = round(time.perf_counter() - t_extra, 3)
+    if rank == 0:
+        print(json.dumps(record("final", tiers, configs, extras)), flush=True)
     if args.alloc == "memalloc" and p > 1 and not args.cpu:
         comm.memFree(buf)
     comm.close(0)

@@ -90,7 +90,40 @@ struct alignas(128) Signal {
   // barrier spin bound of this instance's kernels, s_memrealtime ticks (100 MHz); 0 = the
   // built-in 600 s.  Set from the host (mp4x_ipc_set_spin); only the owning rank reads it.
   uint64_t spin_ticks;
+  // DEBUG BUILD ONLY (MP4X_DEBUG; the release kernels never read it): kDbgNoRelease /
+  // kDbgNoAcquire remove block_barrier's system-scope release / acquire, so a test can show that
+  // the coherence probes detect a missing fence (tests/test_coherence_gpu.py).  mp4x_ipc_set_debug.
+  uint32_t dbg_flags;
 };
+
+constexpr uint32_t kDbgNoRelease = 1u;
+constexpr uint32_t kDbgNoAcquire = 2u;
+
+// The two halves of every cross-agent hand-off of these kernels (MI355X_MICROARCH "inter-workgroup
+// visibility": per-XCD L2s are not coherent with each other, a CU's L1 is never refreshed by
+// another CU's stores).  Release: write back the dirty lines of this XCD's L2, and WAIT for the
+// write-back before the flag store (an inline-asm wait: the compiler may drop its own after
+// buffer_wbl2).  Acquire: invalidate this CU's L1 / the non-coherent L2 lines, and WAIT for the
+// invalidate, which completes asynchronously — the block's other waves load right after the
+// __syncthreads that follows, so without this wait they could still hit stale lines.
+__device__ __forceinline__ void sys_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // system scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void sys_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");        // system scope
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// The debug flags of `self` (0 in release builds: the fences are unconditional there).
+__device__ __forceinline__ uint32_t dbg_flags_of(const Signal* self) {
+#ifdef MP4X_DEBUG
+  return __hip_atomic_load(&self->dbg_flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  (void)self;
+  return 0u;
+#endif
+}
 
 constexpr uint64_t kDefaultSpinTicks = 600ull * 100000000ull;   // 600 s at 100 MHz
 
@@ -134,8 +167,9 @@ __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int r
   __syncthreads();
   const int t = threadIdx.x;
   if (t < p) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");      // system scope
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t dbg = dbg_flags_of(self);
+    if (!(dbg & kDbgNoRelease)) sys_release();
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     Signal* peer = sig_of(P, t);
     uint32_t* slot = which == 0 ? &peer->start[blockIdx.x][rank]
                    : which == 1 ? &peer->mid[blockIdx.x][rank] : &peer->end[blockIdx.x][rank];
@@ -164,7 +198,7 @@ __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int r
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (!(dbg & kDbgNoAcquire)) sys_acquire();
   }
   __syncthreads();
   return s_fail == 0;

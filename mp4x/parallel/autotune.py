@@ -107,30 +107,44 @@ class AutotuneMixin:
         return self.backend == "gloo" and self.device.type == "cuda" and self.ipc_enabled and \
             os.environ.get("MP4X_AUTOTUNE_GLOO", "0") != "1"
 
+    @staticmethod
+    def _extra_schedules() -> bool:
+        """``MP4X_AUTOTUNE_EXTRA=1``: the opt-in schedules join the autotune candidates (RCCL with
+        pinned channel counts, the pipelined staged two-shot, the zero-copy grid variants, rhd,
+        the composite broadcast).  Off by default: every schedule tried on first contact with a
+        topology is a risk and costs tuning time; each stays reachable by
+        name (``MP4X_DEVICE_ALGO``, ``MP4X_AUTOTUNE_CANDIDATES``, a tune file)."""
+        return os.environ.get("MP4X_AUTOTUNE_EXTRA", "0") == "1"
+
     def allreduce_candidates(self, nbytes: int, op, dtype) -> List[str]:
+        """The default decision tree's allreduce candidates (DESIGN.md "Default schedules"): at
+        most six — ``rccl``, ``ipc1`` (<= 4 MiB), ``ipc2``, ``ipc2z``, ``ipc2w``, ``a2a`` (``hier``
+        replaces the IPC forms on a multi-node job).  The rest only with :meth:`_extra_schedules`."""
         c = []
+        extra = self._extra_schedules()
         if self._stand_in() and self._ipc_ok(op, dtype, nbytes):
             return (["ipc1"] if nbytes <= (4 << 20) else []) + ["ipc2"] + \
-                (["ipc2p"] if nbytes > self.ipc_twoshot_max else []) + (["ipc2z", "ipc2w"] if self._zc else [])
+                (["ipc2p"] if extra and nbytes > self.ipc_twoshot_max else []) + \
+                (["ipc2z", "ipc2w"] if self._zc else [])
         if self.rccl_ok(op, dtype):
             c.append("rccl")
-            if self.backend == "nccl" and nbytes >= (64 << 20):
+            if extra and self.backend == "nccl" and nbytes >= (64 << 20):
                 c += [f"rccl_c{n}" for n in self.RCCL_CTA_VARIANTS]
         if self._ipc_ok(op, dtype, nbytes) and self.device.type == "cuda":
             if nbytes <= (4 << 20):
                 c.append("ipc1")
             c.append("ipc2")
-            if nbytes > self.ipc_twoshot_max:
+            if extra and nbytes > self.ipc_twoshot_max:
                 c.append("ipc2p")     # pipelined pieces: input copies overlap the xGMI-bound kernel
             if self._zc:
                 c.append("ipc2z")     # zero-copy two-shot on a registered tensor (one kernel)
                 c.append("ipc2w")     # ... its push form: every xGMI transfer a posted write
-                if nbytes >= (64 << 20) and not getattr(self._ipc_obj, "shared_gpu", True):
+                if extra and nbytes >= (64 << 20) and not getattr(self._ipc_obj, "shared_gpu", True):
                     c += [f"ipc2z_b{g}" for g in ZC_GRIDS]     # ... with fewer, longer-lived blocks
         if self._hier_ok(op, dtype, nbytes):
             c.append("hier")
         c.append("a2a")
-        if nbytes <= (64 << 20):
+        if extra and nbytes <= (64 << 20):
             c.append("rhd")
         return c
 
@@ -155,23 +169,23 @@ class AutotuneMixin:
         if self.watchdog is not None:
             self.watchdog.paused += 1     # IPC timeouts here are expected probe results, not failures
         registered = False
-        probe = self.probing()
-        probe.__enter__()
         try:
-            if any(zc_grid(c)[0] in ("ipc2z", "ipc2w") for c in cands):
-                registered = self.register_buffer(view)     # collective; False on every rank alike
-                if not registered or (self._ipc_obj.scratch_of(view) is None and "ipc2w" in cands):
-                    # (the push form needs every rank's scratch: agreed inside register)
-                    cands[:] = [c for c in cands if c != "ipc2w" or registered and
-                                self._ipc_obj.scratch_of(view) is not None]
-                if not registered:
-                    cands[:] = [c for c in cands if zc_grid(c)[0] not in ("ipc2z", "ipc2w")]
-            for c in cands:
-                times.append(self._time_candidate(c, view, op, iters))
+            with self.probing():
+                try:
+                    if any(zc_grid(c)[0] in ("ipc2z", "ipc2w") for c in cands):
+                        registered = self.register_buffer(view)     # collective; False on every rank alike
+                        if not registered or (self._ipc_obj.scratch_of(view) is None and "ipc2w" in cands):
+                            # (the push form needs every rank's scratch: agreed inside register)
+                            cands[:] = [c for c in cands if c != "ipc2w" or registered and
+                                        self._ipc_obj.scratch_of(view) is not None]
+                        if not registered:
+                            cands[:] = [c for c in cands if zc_grid(c)[0] not in ("ipc2z", "ipc2w")]
+                    for c in cands:
+                        times.append(self._time_candidate(c, view, op, iters))
+                finally:
+                    if registered:
+                        self.deregister_buffer(view)        # collective, ordered (ipc.deregister)
         finally:
-            if registered:
-                self.deregister_buffer(view)
-            probe.__exit__(None, None, None)
             if self.watchdog is not None:
                 self.watchdog.paused -= 1
         tt = torch.tensor(times, dtype=torch.float64, device=self.device if self.backend == "nccl" else "cpu")
@@ -320,7 +334,8 @@ class AutotuneMixin:
         reference's van de Geijn schedule, ProcessCommSlave.java:750-775).  Collective."""
         view = torch.zeros(like.numel(), dtype=like.dtype, device=like.device)
         n = view.numel()
-        cands = ["rccl", "composite"] + (["ipc"] if self.ipc_enabled and view.is_cuda else [])
+        cands = ["rccl"] + (["composite"] if self._extra_schedules() else []) + \
+            (["ipc"] if self.ipc_enabled and view.is_cuda else [])
         if self._stand_in():
             cands = ["ipc"]
 

@@ -188,6 +188,7 @@ class DeviceEngine(AutotuneMixin):
         self._ipc_large_failed = False   # set on every rank together (setup failure is collective)
         self._ipc_fp8_big = None         # whole-tensor fp8 staging (see _ipc_fp8_whole)
         self._ipc_fp8_big_failed = False
+        self.probe_failures: List[dict] = []   # first-use probe failures of lazily made instances
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
         self._tuned: Dict[tuple, str] = _TunedTable()
@@ -362,10 +363,7 @@ class DeviceEngine(AutotuneMixin):
             if bad:
                 LOG.warning("rank %d: IPC self-test failed (%s): IPC tiers disabled on every rank, RCCL used",
                             self.rank, bad)
-                try:
-                    inst.close()
-                except Exception:   # noqa: BLE001
-                    pass
+                self._drop_instance(inst)                # agreed: every rank is here
                 self.ipc_enabled = False
                 self.ipc_selftest = {"ok": False, "failures": bad}
                 return None
@@ -570,16 +568,36 @@ class DeviceEngine(AutotuneMixin):
         if self._ipc_large is None and not self._ipc_large_failed and self.ipc() is not None:
             try:
                 from .ipc import IpcAllreduce
-                self._ipc_large = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
-                                               tag="large")
-                self._probe_spin(self._ipc_large)
-                if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
-                    self._ipc_large.prepare_graph()   # a capture is being prepared: same epoch mode
+                inst = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
+                                    tag="large")
             except Exception as e:
                 LOG.warning("large-message IPC allreduce disabled: %s", e)
                 self._ipc_large_failed = True
                 return self._ipc_obj
+            # first use of a fresh mesh: every form this instance serves, exact, agreed
+            bad = self._probe_instance(inst, large_forms=True)
+            if bad:
+                LOG.warning("rank %d: large-message IPC instance failed its first-use probe (%s): dropped on "
+                            "every rank, the default instance serves those calls", self.rank, bad)
+                self._drop_instance(inst)
+                self._ipc_large_failed = True
+                self.probe_failures.append({"instance": "large", "failures": bad})
+                return self._ipc_obj
+            self._ipc_large = inst
+            self._probe_spin(inst)
+            if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
+                inst.prepare_graph()   # a capture is being prepared: same epoch mode
         return self._ipc_large or self._ipc_obj
+
+    probe_failures: list = []      # (class default; the engine's own list is made in __init__)
+
+    def _drop_instance(self, inst) -> None:
+        """Collective: close an IPC instance every rank agreed to drop (ordered: every importer
+        unmaps before any owner frees, ``IpcAllreduce.close(collective=True)``)."""
+        try:
+            inst.close(collective=True)
+        except Exception as e:   # noqa: BLE001 — a teardown error must not hide the fallback
+            LOG.warning("rank %d: closing a dropped IPC instance: %s", self.rank, e)
 
     def hier(self):
         """The node-aware allreduce (parallel/hier.py) of a job spanning >= 2 nodes of equal size,
@@ -950,13 +968,15 @@ class DeviceEngine(AutotuneMixin):
             return self.ipc_large()
         try:
             if inst is not None:
-                inst.close()
+                self._ipc_fp8_big = None
+                inst.close(collective=True)       # re-grow mid-job: ordered, every rank here
             from .ipc import IpcAllreduce
             inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8")
-            bad = self._probe_staging(inst)
+            bad = self._probe_instance(inst, large_forms=False, fp8=True)
             if bad:
-                inst.close()
-                raise Mp4jException(f"staging self-test failed: {bad}")
+                self._drop_instance(inst)
+                self.probe_failures.append({"instance": "fp8", "failures": bad})
+                raise Mp4jException(f"first-use probe failed: {bad}")
             self._probe_spin(inst)
             if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
                 inst.prepare_graph()
@@ -968,31 +988,75 @@ class DeviceEngine(AutotuneMixin):
         self._ipc_fp8_big = inst
         return inst
 
-    def _probe_staging(self, inst) -> list:
-        """Collective first-contact check of a NEW instance's staging buffer (the whole-tensor fp8
-        one is VMM-built, coarse-grained, above 2 GiB): the staged two-shot twice on the same
-        tensor (the second call reduces the first call's result, so a stale line on either side of
-        a link shows as a wrong element), exact, short spin bound.  Returns every rank's failures
-        (agreed through the control plane; empty = fine)."""
+    def _probe_instance(self, inst, large_forms: bool = False, fp8: bool = False) -> list:
+        """Collective first-use check of a NEW IPC instance (lazily created instances
+        were never verified; a mesh built after a bad teardown read and wrote the wrong memory).
+        Exact patterns, short spin bound, nothing else in flight:
+
+        * the staged two-shot twice on the same tensor (the second call reduces the first call's
+          result, so a stale line on either side of a link shows as a wrong element);
+        * ``large_forms`` (the large-message instance): the piecewise broadcast / scatter /
+          gather copy plans and reduce-scatter / all-gather, the forms the rooted and RS / AG
+          schedules send to it;
+        * ``fp8``: the fused fp8 two-shot within its codec bound (garbage, not rounding, fails).
+
+        Returns every rank's failures, agreed through the control plane (empty = fine).
+        ``MP4X_IPC_PROBE_INJECT=<rank>`` injects a failure on that rank (failure-path tests)."""
         from . import ipc as ipcm
         from ..operators import Operators
         fails = []
+        p, r = self.p, self.rank
         try:
             inst.set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2")))
             op = for_dtype(Operators.Float.SUM, DType.F32)
             n = min(inst.nbytes // 4, 1 << 20)
+            n -= n % (4 * p)                                # 16-byte segments for every rank
             t = torch.empty(n, dtype=torch.float32, device=self.device)
+
+            def check(name, bad_fn):
+                torch.cuda.synchronize(self.device)
+                inst.raise_if_failed()
+                nbad = int(bad_fn())
+                if nbad:
+                    fails.append(f"{name}: {nbad} wrong elements")
+
             exp = self._fill_probe(t, op)
             for rep in range(2):
                 inst.allreduce(t, op, algo=ipcm.TWOSHOT)
-                torch.cuda.synchronize(self.device)
-                inst.raise_if_failed()
-                nbad = int((t != exp * (self.p ** rep)).sum())
-                if nbad:
-                    fails.append(f"staged_twoshot_{rep}: {nbad} wrong elements")
+                check(f"staged_twoshot_{rep}", lambda: (t != exp * (p ** rep)).sum())
+            if large_forms:
+                root = p - 1
+                froms, tos, _ = CommUtils.even_split(0, n, p)
+                segs = [(froms[j], tos[j], j) for j in range(p)]
+                mine = slice(froms[r], tos[r])
+                ex = self._copy_probe(t, [(0, n, root)])
+                t.copy_(ex) if r == root else t.fill_(-1)
+                inst.broadcast_large(t, 0, n, root)
+                check("broadcast_large", lambda: (t != ex).sum())
+                ex = self._copy_probe(t, segs)
+                t.copy_(ex) if r == root else t.fill_(-1)
+                inst.scatter_large(t, froms, tos, root)
+                check("scatter_large", lambda: (t[mine] != ex[mine]).sum())
+                t.fill_(-1)
+                t[mine] = ex[mine]
+                inst.gather_large(t, froms, tos, root)
+                check("gather_large", lambda: (t != ex).sum() if r == root else 0)
+                exp = self._fill_probe(t, op, salt=3)
+                inst.reduce_scatter_large(t, froms, tos, op)
+                check("reduce_scatter_large", lambda: (t[mine] != exp[mine]).sum())
+                inst.allgather_large(t, froms, tos)
+                check("allgather_large", lambda: (t != exp).sum())
+            if fp8 and inst.fp8_ok(t):
+                exp = self._fill_probe(t, op, salt=5)
+                inst.allreduce_fp8(t)
+                tol = 0.25 * float(exp.abs().max())
+                check("fp8_twoshot", lambda: ((t - exp).abs() > tol).sum())
+            del t
             inst.set_spin(ipcm.spin_default())
         except Exception as e:   # noqa: BLE001
             fails.append(f"{type(e).__name__}: {e}")
+        if os.environ.get("MP4X_IPC_PROBE_INJECT", "").strip() == str(r):
+            fails.append("injected failure (MP4X_IPC_PROBE_INJECT)")
         allf = self.comm.server.call("allgather_obj", self.rank, fails)
         return [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
 

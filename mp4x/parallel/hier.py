@@ -207,11 +207,16 @@ class HierAllreduce:
         self.selftest = {"ok": not fails, "failures": fails, "ipc_nodes": None}
         if fails:
             LOG.warning("rank %d: hierarchical IPC self-test failed (%s): local process groups used", eng.rank, fails)
+            # agreed job-wide: every rank is here.  Ordered teardown (every importer unmaps
+            # before any owner frees, IpcAllreduce.close(collective=True)); a rank without a
+            # sub-mesh joins the same global barrier
             if self.ipc is not None:
                 try:
-                    self.ipc.close()
-                except Exception:   # noqa: BLE001
-                    pass
+                    self.ipc.close(collective=True)
+                except Exception as e:   # noqa: BLE001
+                    LOG.warning("rank %d: closing the dropped sub-mesh: %s", eng.rank, e)
+            else:
+                eng.comm.server.call("barrier", eng.rank)
             self.ipc = None
         self.selftest["ipc_nodes"] = sum(1 for x in eng.comm.server.call("allgather_obj", eng.rank,
                                                                           self.ipc is not None) if x) // self.L

@@ -106,6 +106,14 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 #   "pool":           park the allocation in a per-size pool that the next memAlloc of that size
 #                     reuses (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
+# Release ORDER of everything a peer maps (push scratches at deregistration, self-test buffers, the
+# staging buffers of an instance closed mid-job): every importer closes its mappings, a control-
+# plane barrier, and only then does each owner free its memory — the order mem_free always used.
+# Round 4 freed a push scratch while the peers still had it mapped, then made new fine-grained
+# exports: later instances' collectives read and wrote the wrong memory (profiles/r4/rooted/).
+# MP4X_TEST_UNORDERED_RELEASE=1 restores that order (owner frees first, no barrier) — for the
+# regression test that shows the first-use probes catch it; never for a job.
+UNORDERED_RELEASE = os.environ.get("MP4X_TEST_UNORDERED_RELEASE", "0") == "1"
 VMM_POLICIES = ("chunks", "fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
 VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
     "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "chunks")
@@ -282,7 +290,6 @@ class IpcAllreduce:
         self.data_ptrs: List[int] = []
         self.sig_ptrs: List[int] = []
         err = None
-        got = {}
         got = {}
         if self._vmm_data:
             from . import vmm
@@ -642,7 +649,7 @@ class IpcAllreduce:
             if self.rank == 0:
                 LOG.warning("registerBuffer(%d bytes): peer mapping failed on ranks %s", key[1],
                             [(i, o) for i, o in enumerate(oks) if o])
-            self._release(reg)
+            self._release_ordered(reg)                # agreed: every rank is here
             return False
         old = self._regs.get(key)
         if old is not None:
@@ -713,22 +720,38 @@ class IpcAllreduce:
             else:
                 self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
-    def _release(self, reg: "_Reg") -> None:
-        """Release what ``reg`` holds on this rank: its scratch, its uses of the peer mappings
-        (:meth:`_close_peer`) and its tensor reference; memAlloc regions are unmapped and released,
-        imported views first (the collective, ordered release is :meth:`mem_free`)."""
-        self._free_scratch(reg.scratch_alloc)
-        reg.scratch_alloc = None
+    def _release_imports(self, reg: "_Reg") -> None:
+        """The importer half of a release: this rank's uses of the peers' mappings
+        (:meth:`_close_peer`) and its imported memAlloc views."""
         for hk in reg.peer_keys:
             self._close_peer(hk)
         reg.peer_keys = []
-        for i in reversed(range(len(reg.vmm))):   # the peers' imported views first, own memory last
-            reg.vmm[i].free(self._keep_va(own=i < reg.nown))
+        for i in reversed(range(reg.nown, len(reg.vmm))):
+            reg.vmm[i].free(self._keep_va(own=False))
+        del reg.vmm[reg.nown:]
+
+    def _release_own(self, reg: "_Reg") -> None:
+        """The owner half: this rank's push scratch, own memAlloc regions / chunks, tensor reference."""
+        self._free_scratch(reg.scratch_alloc)
+        reg.scratch_alloc = None
+        for i in reversed(range(len(reg.vmm))):
+            reg.vmm[i].free(self._keep_va(own=True))
         reg.vmm = []
+        reg.nown = 0
         reg.keep = None
         if reg.chunks is not None and self._chunk_pool is not None:
             self._chunk_pool.give(reg.chunks)
             reg.chunks = []
+
+    def _release(self, reg: "_Reg") -> None:
+        """Rank-local release of ``reg``: the importer half, then the owner half.  The collective,
+        ordered form (no owner frees before every importer closed) is :meth:`_release_ordered`;
+        this one serves close() and the memAlloc paths that order themselves."""
+        if UNORDERED_RELEASE:           # test knob: round 4's order (own scratch freed first)
+            self._free_scratch(reg.scratch_alloc)
+            reg.scratch_alloc = None
+        self._release_imports(reg)
+        self._release_own(reg)
 
     @staticmethod
     def _keep_va(own: bool = True):
@@ -739,20 +762,36 @@ class IpcAllreduce:
             VMM_POLICY == ("keep_owner_va" if own else "keep_import_va")
         return vmm.va_quarantine() if keep else None
 
+    def _release_ordered(self, reg: Optional["_Reg"]) -> None:
+        """Collective release of a registration (``reg`` may be None on a rank that has none: it
+        still joins the barrier).  Every rank drains its stream, closes ITS mappings of the
+        peers' tensors and push scratches, a control-plane barrier, then each owner frees its
+        own push scratch — no memory is freed while a peer still maps it (the order of
+        :meth:`mem_free`; ``_release`` alone is the rank-local teardown used at close)."""
+        torch.cuda.synchronize(self.device)
+        if UNORDERED_RELEASE:           # test knob: round 4's order (owner first, nothing agreed)
+            if reg is not None:
+                self._release(reg)
+            return
+        if reg is not None:
+            self._release_imports(reg)
+        self.comm.server.call("barrier", self.rank)         # every importer closed its mappings
+        if reg is not None:
+            self._release_own(reg)
+
     def deregister(self, t: torch.Tensor) -> None:
-        """Forget ``t``: once this rank's stream drained, its mappings of the peers' tensors and
-        scratches are closed (when no other registration uses them), its push scratch is freed
-        and the reference to ``t`` is dropped.  Every peer deregisters its tensor at the same
-        point (the registration contract): each closes its own mappings, and the memory a rank
-        frees stays alive in the driver until the last peer mapping of it is closed.  A memAlloc
-        tensor stays registered until memFree."""
+        """Collective: forget ``t`` on every rank (the registration contract: every rank
+        deregisters its tensor at the same point).  Ordered like :meth:`mem_free` — every rank
+        drains its stream and closes its mappings of the peers' tensors and scratches, a
+        barrier, and only then does each owner free its push scratch (:meth:`_release_ordered`).
+        A memAlloc tensor stays registered until memFree (a collective fact: no barrier then)."""
         key = (t.data_ptr(), t.numel() * t.element_size())
         reg = self._regs.get(key)
-        if reg is None or reg.vmm:
+        if reg is not None and reg.vmm:
             return
-        del self._regs[key]
-        torch.cuda.synchronize(self.device)
-        self._release(reg)
+        if reg is not None:
+            del self._regs[key]
+        self._release_ordered(reg)
 
     def _find(self, view: torch.Tensor):
         """(registration, byte offset of ``view`` in it) or (None, 0)."""
@@ -1112,6 +1151,8 @@ class IpcAllreduce:
         self.comm.server.call("barrier", self.rank)         # every peer is done before unmapping
         for q in opened:
             native.soft_check(self.lib.mp4x_ipc_close_handle(q), "ipc_close_handle", LOG)
+        if not UNORDERED_RELEASE:
+            self.comm.server.call("barrier", self.rank)     # every importer unmapped before the owners free
         if ptr:
             native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)
         if scr:
@@ -1796,20 +1837,48 @@ class IpcAllreduce:
             ctypes.c_uint32.from_address(self._herr.value).value = 0
         return int(v.value)
 
-    def close(self, sync: bool = True):
+    def close(self, sync: bool = True, collective: bool = False):
+        """Tear the instance down: every mapping of the peers' memory first, then this rank's own
+        memory.  ``collective`` (every rank closes this instance at the same point, e.g. a mid-job
+        re-grow or an instance dropped after a failed first-use probe): a control-plane barrier
+        between the two halves, so no owner frees what a peer still maps — the process goes on
+        allocating and exporting afterwards.  Without it (process teardown, failure paths that
+        cannot agree) the halves run back to back."""
         if self.lib is None:
             return
         if sync:
             torch.cuda.synchronize()
         if self._sig and self._herr:
             self.lib.mp4x_ipc_set_host_error(self._sig, None)
+        # ---- importer half: the peers' staging / signal buffers, registered tensors, scratches
         for ptr in self._opened:
             native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
         self._opened = []
+        regions = getattr(self, "_data_regions", [])
+        for region in reversed(regions[1:]):               # imported views of the peers' data
+            try:
+                region.free(self._keep_va(own=False))
+            except Exception:   # noqa: BLE001 — best effort at teardown
+                pass
+        del regions[1:]
+        pooled = [r for lst in getattr(self, "_vmm_pool", {}).values() for r in lst]
+        regs = list(getattr(self, "_regs", {}).values()) + pooled
+        for reg in regs:
+            try:
+                self._release_imports(reg)
+            except Exception:   # noqa: BLE001 — best effort at teardown
+                pass
+        for ptr in getattr(self, "_peer_bases", {}).values():
+            native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
+        self._peer_bases = {}
+        self._peer_refs = {}
+        if collective and not UNORDERED_RELEASE:
+            self.comm.server.call("barrier", self.rank)     # every importer unmapped before the owners free
+        # ---- owner half
         if self._data and not getattr(self, "_vmm_data", False):
             native.soft_check(self.lib.mp4x_ipc_free(self._data), "ipc_free", LOG)
         self._data = c_void_p()
-        for region in reversed(getattr(self, "_data_regions", [])):   # imported views first
+        for region in regions:
             try:
                 region.free(self._keep_va())
             except Exception:   # noqa: BLE001 — best effort at teardown
@@ -1822,13 +1891,9 @@ class IpcAllreduce:
             self._herr_word = None
             self.lib.mp4x_host_word_free(self._herr)
             self._herr = c_void_p()
-        for ptr in getattr(self, "_peer_bases", {}).values():
-            native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
-        self._peer_bases = {}
-        pooled = [r for lst in getattr(self, "_vmm_pool", {}).values() for r in lst]
-        for reg in list(getattr(self, "_regs", {}).values()) + pooled:
+        for reg in regs:
             try:
-                self._release(reg)
+                self._release_own(reg)
             except Exception:   # noqa: BLE001 — best effort at teardown
                 pass
         self._regs = {}

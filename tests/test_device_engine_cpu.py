@@ -173,6 +173,10 @@ def test_sparse_engine_gloo(p):
     run_ranks(p, sparse_engine, timeout=120)
 
 
+# rhd is an opt-in schedule (MP4X_AUTOTUNE_EXTRA=1): these tests use it as the odd candidate
+EXTRA = {"MP4X_AUTOTUNE_EXTRA": "1"}
+
+
 def autotune_job(comm):
     eng = comm.device
     assert eng.algo == "auto"
@@ -190,7 +194,7 @@ def autotune_job(comm):
 
 @pytest.mark.parametrize("p", [2, 3])
 def test_autotune_pins_fastest_schedule_consistently(p):
-    res, code, _ = run_ranks(p, autotune_job, timeout=120)
+    res, code, _ = run_ranks(p, autotune_job, timeout=120, env=EXTRA)
     assert code == 0
     bests = {b for b, _ in res.values()}
     assert len(bests) == 1                      # every rank made the same decision
@@ -217,7 +221,7 @@ def broken_candidate_job(comm, dtype_name, opname):
 
 @pytest.mark.parametrize("dtype_name,opname", [("float32", "SUM"), ("bfloat16", "MAX"), ("float32", "MIN")])
 def test_autotune_probe_rejects_a_wrong_schedule(dtype_name, opname):
-    res, code, _ = run_ranks(3, broken_candidate_job, (dtype_name, opname), timeout=120)
+    res, code, _ = run_ranks(3, broken_candidate_job, (dtype_name, opname), timeout=120, env=EXTRA)
     assert code == 0
     for r in res.values():
         assert r["a2a"] == float("inf") and len(r) >= 2
@@ -374,7 +378,7 @@ def one_rank_raises_job(comm):
 
 
 def test_autotune_local_failure_is_agreed():
-    res, code, _ = run_ranks(3, one_rank_raises_job, timeout=120)
+    res, code, _ = run_ranks(3, one_rank_raises_job, timeout=120, env=EXTRA)
     assert code == 0
     for r in res.values():
         assert r["rhd"] == float("inf") and all(v < float("inf") for c, v in r.items() if c != "rhd")
@@ -400,7 +404,7 @@ def capped_job(comm):
 
 
 def test_autotune_wall_cap(monkeypatch):
-    res, code, _ = run_ranks(2, capped_job, timeout=120, env={"MP4X_AUTOTUNE_CAP_S": "0.1"})
+    res, code, _ = run_ranks(2, capped_job, timeout=120, env={"MP4X_AUTOTUNE_CAP_S": "0.1", **EXTRA})
     assert code == 0
     for r, n in res.values():
         assert n == 2 and r["rhd"] >= 0.3, (r, n)    # warm-up + second probe call, no timed calls
@@ -461,7 +465,7 @@ def rooted_autotune_job(comm):
 
 
 def test_rooted_autotuners_pin_and_apply():
-    res, code, _ = run_ranks(3, rooted_autotune_job, timeout=120)
+    res, code, _ = run_ranks(3, rooted_autotune_job, timeout=120, env=EXTRA)   # composite is opt-in
     assert code == 0
     assert len({tuple(sorted(pin.items())) for pin, _, _ in res.values()}) == 1     # agreed
     for pin, ok, st in res.values():
@@ -471,10 +475,11 @@ def test_rooted_autotuners_pin_and_apply():
         assert st.get("broadcast" if pin["broadcast"] == "rccl" else "broadcast.composite") == 1, st
 
 
-def test_zero_copy_grid_variants_are_candidates_on_a_gpu_of_their_own():
+def test_zero_copy_grid_variants_are_candidates_on_a_gpu_of_their_own(monkeypatch):
     """``ipc2z_b<N>`` (the zero-copy two-shot on N blocks) is tried for large messages when
-    every rank has a GPU of its own; never on a shared GPU (its grid is capped there anyway)
-    or under the gloo stand-in."""
+    every rank has a GPU of its own (opt-in: MP4X_AUTOTUNE_EXTRA=1); never on a shared GPU (its
+    grid is capped there anyway) or under the gloo stand-in."""
+    monkeypatch.setenv("MP4X_AUTOTUNE_EXTRA", "1")
     from mp4x import Operators
     from mp4x.parallel.device_engine import ZC_GRIDS, DeviceEngine, zc_grid
     assert zc_grid("ipc2z_b64") == ("ipc2z", 64) and zc_grid("ipc2z") == ("ipc2z", 0)

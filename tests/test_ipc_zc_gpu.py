@@ -172,7 +172,10 @@ def _mismatch_fn(comm):
     buf = _pattern(n, r)
     assert comm.registerBuffer(buf)
     if r == 1:
-        comm.deregisterBuffer(buf)      # rank 1 now runs the staged protocol, rank 0 zero-copy
+        # a rank-local registration difference (deregisterBuffer itself is collective and ordered
+        # now, so the misuse is simulated by rank 1 forgetting the registration on its own): rank 1
+        # now runs the staged protocol, rank 0 zero-copy
+        inst._regs.clear()
     t0 = time.perf_counter()
     eng._run_allreduce("ipc2z", buf, eng._op(Operators.Float.SUM, buf))
     torch.cuda.synchronize()

@@ -32,8 +32,10 @@ def _run(tmp_path, nproc=4, extra_env=None, steps=3):
 def test_torchrun_bench_dry_run_all_ranks_exit_clean(tmp_path):
     r, lines = _run(tmp_path)
     assert r.returncode == 0, r.stdout[-3000:]
-    assert len(lines) == 1
-    rec = lines[0]
+    # the verified headline right after its measurement, then the enriched final line (same numbers)
+    assert [x["phase"] for x in lines] == ["headline", "final"], lines
+    assert lines[0]["value"] == lines[1]["value"] and lines[0]["verified"] is True
+    rec = lines[-1]
     assert rec["n_gpus"] == 4 and rec["steps"] == 3 and rec["value"] > 0
     # value is the per-rank nccl-tests busbw (BASELINE metric), not the whole-job sum
     assert rec["value"] == rec["busbw_gbps_per_rank"]
@@ -59,4 +61,33 @@ def test_bench_wrong_result_fails_the_run(tmp_path):
     # a wrong element on one rank (test hook standing in for a broken kernel): verified false, rc != 0
     r, lines = _run(tmp_path, nproc=2, extra_env={"MP4X_BENCH_CORRUPT": "1"})
     assert r.returncode != 0, r.stdout[-3000:]
-    assert len(lines) == 1 and lines[0]["verified"] is False and lines[0]["max_abs_err"] >= 1.0, lines
+    assert len(lines) == 2 and all(x["verified"] is False and x["max_abs_err"] >= 1.0 for x in lines), lines
+
+
+def test_headline_survives_a_hang_after_it(tmp_path):
+    """VERDICT r4 Next #3: the headline line is printed right after its measurement; a stage after
+    it that never returns (test hook in the extras) and the driver's kill cannot lose it."""
+    import signal
+    import time
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--cpu", "--gpus", "2", "--steps", "3", "--warmup", "1", "--bytes", "4000000"]
+    pr = subprocess.Popen(cmd, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                          env=dict(os.environ, PYTHONPATH=ROOT, MP4X_BENCH_TEST_HANG="extras"),
+                          start_new_session=True)
+    got = None
+    t0 = time.monotonic()
+    try:
+        for line in pr.stdout:
+            if line.startswith('{"metric"'):
+                got = json.loads(line)
+                break
+            if time.monotonic() - t0 > 240:
+                break
+        time.sleep(1.0)
+        assert pr.poll() is None, "the hook should hang the run after the headline"
+    finally:
+        os.killpg(pr.pid, signal.SIGKILL)          # what the driver's timeout does
+        pr.wait(30)
+    assert got is not None and got["phase"] == "headline" and got["verified"] is True, got
+    assert got["value"] > 0 and got["n_gpus"] == 2

@@ -64,3 +64,39 @@ def test_universe_is_not_trivially_small():
     assert {"allreduce:rccl", "allreduce:ipc2z", "allreduce:hier", "allreduce:rccl_c112", "allreduce:zs",
             "broadcast:composite", "gather:p2p", "reduce_scatter:ipc"} <= uni
     assert len(uni) >= 25
+
+
+# Opt-in schedules (MP4X_AUTOTUNE_EXTRA=1, MP4X_DEVICE_ALGO, MP4X_AUTOTUNE_CANDIDATES or a tune
+# file): never autotune candidates by default, still covered by the cross-GPU module above.
+OPT_IN = {"rccl_c64", "rccl_c112", "ipc2p", "ipc2z_b64", "ipc2z_b128", "rhd"}
+
+
+def _engine(hier=False):
+    e = object.__new__(DeviceEngine)
+    e.backend, e.device, e.ipc_enabled, e._zc, e.p = "nccl", torch.device("cuda", 0), True, True, 8
+    e.ipc_twoshot_max, e.ipc_oneshot_max = 16 << 20, 256 << 10
+
+    class _Ipc:
+        shared_gpu = False
+    e._ipc_obj = _Ipc()
+    e._hier_ok = lambda op, dt, nb: hier
+    return e
+
+
+def test_default_decision_tree_has_at_most_six_schedules_per_size(monkeypatch):
+    """VERDICT r4 Next #6: the 8-GPU default decision tree tries <= 6 allreduce schedules per size
+    class, none of them opt-in; the opt-in ones return only when asked for."""
+    monkeypatch.delenv("MP4X_AUTOTUNE_EXTRA", raising=False)
+    e = _engine()
+    seen = set()
+    for nb in (4096, 1 << 20, 16 << 20, 64 << 20, 1 << 30, 4 << 30):
+        c = e.allreduce_candidates(nb, Operators.Float.SUM, torch.float32)
+        assert len(c) <= 6, (nb, c)
+        seen |= set(c)
+    assert not seen & OPT_IN, seen & OPT_IN
+    assert seen == {"rccl", "ipc1", "ipc2", "ipc2z", "ipc2w", "a2a"}, seen
+    monkeypatch.setenv("MP4X_AUTOTUNE_EXTRA", "1")
+    extra = set()
+    for nb in (4096, 1 << 20, 64 << 20, 1 << 30):
+        extra |= set(e.allreduce_candidates(nb, Operators.Float.SUM, torch.float32))
+    assert OPT_IN <= extra, OPT_IN - extra
