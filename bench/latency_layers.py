@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Where the host time of a small device allreduce goes: p processes on GPU 0, the same 4 KiB
-f32 SUM issued through each layer in turn (public API -> DeviceEngine -> IpcAllreduce ->
-the bare ctypes launch), wall time per call (MAX over ranks).  Rehearsal numbers: protocol
+f32 SUM issued through each layer in turn (public API with its native latency fast path ->
+the public API's full Python path -> DeviceEngine -> IpcAllreduce -> the bare ctypes launch),
+wall time per call (MAX over ranks).  Rehearsal numbers: protocol
 and host overhead, not xGMI latency.
 
     python bench/latency_layers.py --procs 2 --iters 3000 [--bytes 4096]
@@ -41,7 +42,16 @@ def worker(port, q, nbytes, iters):
         lib.mp4x_ipc_allreduce_ex(ipcm.ONESHOT, dt, int(fop.code), inst._pp_data[0], inst._pp_sig[0], inst.rank,
                                   inst.p, nbytes, x.data_ptr(), x.data_ptr(), inst.epoch, 8 if inst.shared_gpu else 0,
                                   None, 1.0, st)
+    fast_memo = comm._fast_ar
+
+    def api_full():            # the public call with the latency fast path disarmed
+        comm._fast_ar = None
+        try:
+            comm.allreduceArray(x, opnd, op, 0, n)
+        finally:
+            comm._fast_ar = fast_memo
     layers = {"api": lambda: comm.allreduceArray(x, opnd, op, 0, n),
+              "api_full_path": api_full,
               "engine": lambda: eng.allreduce(x, 0, n, op, opnd),
               "ipc": lambda: inst.allreduce(x, fop, algo=ipcm.ONESHOT),
               "raw_launch": raw}
@@ -77,8 +87,9 @@ def main():
     res = dict(q.get(timeout=600) for _ in range(a.procs))
     [p.join(timeout=30) for p in ps]
     m.stop(timeout=5)
+    us = {k: round(max(res[r][k] for r in res), 2) for k in res[0]}
     print(json.dumps({"procs_on_one_gpu": a.procs, "bytes": a.bytes, "watchdog": os.environ.get("MP4X_WATCHDOG", "1"),
-                      "us_per_call_max_rank": {k: round(max(res[r][k] for r in res), 2) for k in res[0]}}))
+                      "us_per_call_max_rank": us, "api_minus_raw_launch_us": round(us["api"] - us["raw_launch"], 2)}))
 
 
 if __name__ == "__main__":

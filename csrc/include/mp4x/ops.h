@@ -28,7 +28,10 @@ enum mp4x_op {
   MP4X_FIRST = 11,                      // keep the first value (K8 map merge / dedupe-by-key; sparse only)
 };
 
-enum { MP4X_E_BADARG = 1001, MP4X_E_UNSUPPORTED = 1002 };
+enum { MP4X_E_BADARG = 1001, MP4X_E_UNSUPPORTED = 1002,
+       // latency fast path (mp4x_ipc_fast_allreduce): not launched, the caller takes the full path
+       MP4X_E_FAILED_EARLIER = 1003,   // an IPC collective of this engine timed out earlier
+       MP4X_E_CAPTURING = 1004 };      // the stream is being captured into a hipGraph
 
 #define MP4X_MAX_NIN 8
 

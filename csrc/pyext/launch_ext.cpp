@@ -19,6 +19,12 @@ using AllreduceEx = int (*)(int algo, int dtype, int op, void* const* data_ptrs,
 
 AllreduceEx g_allreduce_ex = nullptr;
 
+// mp4x_ipc_fast_allreduce(state, algo, dtype, op, buf, nbytes, blocks, scale, stream): the latency
+// tier's whole per-call path (error words, capture check, epoch, launch) in libmp4x_hip.so.
+using FastAllreduce = int (*)(const void* state, int algo, int dtype, int op, void* buf, int64_t nbytes, int blocks,
+                              float scale, void* stream);
+FastAllreduce g_fast = nullptr;
+
 void* as_ptr(PyObject* o) {   // int address, or None -> NULL
   if (o == Py_None) return nullptr;
   return PyLong_AsVoidPtr(o);
@@ -65,7 +71,47 @@ PyObject* allreduce_ex(PyObject*, PyObject* const* a, Py_ssize_t na) {
   return PyLong_FromLong(rc);
 }
 
+PyObject* bind_fast(PyObject*, PyObject* addr) {
+  void* f = PyLong_AsVoidPtr(addr);
+  if (!f && PyErr_Occurred()) return nullptr;
+  g_fast = reinterpret_cast<FastAllreduce>(f);
+  Py_RETURN_NONE;
+}
+
+// fast_allreduce(entry, stream) -> rc.  `entry` is the engine's memoised launch tuple
+// (state address, algo, dtype, op, buffer address, nbytes, blocks, scale); rc 1003 / 1004 = not
+// launched (an earlier collective failed / the stream is capturing): the caller takes the full path.
+PyObject* fast_allreduce(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 2 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) < 8) {
+    PyErr_SetString(PyExc_TypeError, "fast_allreduce(entry: tuple of 8, stream)");
+    return nullptr;
+  }
+  if (!g_fast) {
+    PyErr_SetString(PyExc_RuntimeError, "_mp4x_launch: bind_fast() was not called");
+    return nullptr;
+  }
+  PyObject* const* t = &PyTuple_GET_ITEM(a[0], 0);
+  const void* state = PyLong_AsVoidPtr(t[0]);
+  const int algo = (int)PyLong_AsLong(t[1]);
+  const int dtype = (int)PyLong_AsLong(t[2]);
+  const int op = (int)PyLong_AsLong(t[3]);
+  void* buf = PyLong_AsVoidPtr(t[4]);
+  const int64_t nbytes = PyLong_AsLongLong(t[5]);
+  const int blocks = (int)PyLong_AsLong(t[6]);
+  const float scale = (float)PyFloat_AsDouble(t[7]);
+  void* stream = as_ptr(a[1]);
+  if (PyErr_Occurred()) return nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = g_fast(state, algo, dtype, op, buf, nbytes, blocks, scale, stream);
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 PyMethodDef kMethods[] = {
+    {"bind_fast", bind_fast, METH_O, "bind_fast(address of mp4x_ipc_fast_allreduce in the loaded libmp4x_hip.so)"},
+    {"fast_allreduce", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_allreduce)), METH_FASTCALL,
+     "fast_allreduce(entry, stream) -> rc"},
     {"bind", bind, METH_O, "bind(address of mp4x_ipc_allreduce_ex in the loaded libmp4x_hip.so)"},
     {"allreduce_ex", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(allreduce_ex)), METH_FASTCALL,
      "allreduce_ex(algo, dtype, op, data_pp, sig_pp, rank, p, nbytes, src, out, epoch, blocks, epoch_dev, scale, "

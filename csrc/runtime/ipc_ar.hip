@@ -131,6 +131,40 @@ extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* d
   });
 }
 
+// The latency tier's whole per-call host path in ONE native call (VERDICT r4 Next #5: 4.7 us of a
+// 10 us 4 KiB allreduce was interpreter time above the bare launch).  The Python entry
+// (ProcessCommSlave.allreduceArray) looks its call shape up in the engine's memo and hands over
+// the memoised launch; everything the Python path did per call happens here:
+//   * the fail-stop check: every IPC instance's pinned host error word (an earlier collective
+//     that timed out fails the next call: MP4X_E_FAILED_EARLIER, the caller raises);
+//   * the capture check: a stream being captured needs the device-epoch form (MP4X_E_CAPTURING);
+//   * the epoch bump, in the instance's epoch box (the same word IpcAllreduce.epoch reads);
+//   * the launch (mp4x_ipc_allreduce_ex: fused copy-in, in place, fused scale).
+struct FastAr {
+  const uint32_t* herr[8];   // pinned host error words of the engine's instances (nullptr ends the list)
+  uint32_t* epoch;           // the instance's epoch box
+  void* const* data_ptrs;    // every rank's staging buffer
+  void* const* signal_ptrs;  // every rank's signal block
+  int32_t rank, p;
+};
+
+extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int op, void* buf, int64_t nbytes,
+                                       int blocks, float scale, void* stream) {
+  for (int i = 0; i < 8 && s->herr[i]; ++i)
+    if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return MP4X_E_CAPTURING;
+  }
+  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  uint32_t e = (*s->epoch + 1u) & 0x3FFFFFFFu;
+  if (!e) e = 1u;
+  *s->epoch = e;
+  return mp4x_ipc_allreduce_ex(algo, dtype, op, s->data_ptrs, s->signal_ptrs, s->rank, s->p, nbytes, buf, buf, e, blocks,
+                               nullptr, scale, stream);
+}
+
 // The pre-staged form (no fused copy-in, no scale).
 extern "C" int mp4x_ipc_allreduce(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                   int rank, int p, int64_t nbytes, void* out, uint32_t epoch, int blocks,

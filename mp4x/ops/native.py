@@ -33,7 +33,7 @@ class NativeUnavailable(Mp4jException):
     pass
 
 
-_lock = threading.Lock()
+_lock = threading.RLock()    # launch_ext() calls hip() under it
 _hip = None
 _host = None
 
@@ -228,6 +228,9 @@ def launch_ext():
                         lib = hip()
                         mod = _load_ext("_mp4x_launch")
                         mod.bind(ctypes.cast(lib.mp4x_ipc_allreduce_ex, ctypes.c_void_p).value)
+                        fast = getattr(lib, "mp4x_ipc_fast_allreduce", None)
+                        if fast is not None and hasattr(mod, "bind_fast"):
+                            mod.bind_fast(ctypes.cast(fast, ctypes.c_void_p).value)
                     except Exception:   # noqa: BLE001 — ctypes path stays
                         mod = False
                 _launch_ext = mod

@@ -48,9 +48,12 @@ class _TunedTable(dict):
     """The pinned-schedule table; ``gen`` counts its mutations, so :meth:`DeviceEngine.select`
     can memoise its decisions and still see every re-tune, table load or clear."""
     gen = 0
+    on_change = None          # the engine's latency-memo invalidation
 
     def _bump(self):
         self.gen += 1
+        if self.on_change is not None:
+            self.on_change()
 
     def __setitem__(self, k, v):
         self._bump()

@@ -136,6 +136,7 @@ class DeviceEngine(AutotuneMixin):
     _probe_s: Optional[float] = None      # explicit bound of the innermost probing(seconds) scope
     _zc_vmm = True                        # memAlloc builds VMM tensors (False: registered plain ones)
     _ipc_obj = _ipc_large = _ipc_fp8_big = None
+    _fast_ar = None                       # (engines assembled without __init__: no fast path)
 
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
@@ -191,7 +192,9 @@ class DeviceEngine(AutotuneMixin):
         self.probe_failures: List[dict] = []   # first-use probe failures of lazily made instances
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
+        self._fast_ar: Dict[tuple, tuple] = {}        # latency fast path: call shape -> native launch
         self._tuned: Dict[tuple, str] = _TunedTable()
+        self._tuned.on_change = self._invalidate_fast
         self._sel_memo: Dict[tuple, tuple] = {}       # select() decisions of repeated call shapes
         self._dm_large = os.environ.get("MP4X_DM_LARGE", "auto")
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
@@ -268,6 +271,7 @@ class DeviceEngine(AutotuneMixin):
         """Fail-stop teardown (``ncclCommAbort``): a rank blocked in a collective with a dead
         peer returns instead of hanging.  Called by ``ProcessCommSlave.close(code != 0)``."""
         self._stop_watchdog()
+        self._invalidate_fast()
         for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big", "_hier"):
             setattr(self, name, None)          # peers may be gone: no synchronising close
         if self._owns_pg and dist.is_initialized():
@@ -291,6 +295,7 @@ class DeviceEngine(AutotuneMixin):
 
     def shutdown(self):
         self._stop_watchdog()
+        self._invalidate_fast()
         for name in ("_ipc_obj", "_ipc_large", "_ipc_fp8_big", "_hier"):
             obj = getattr(self, name)
             if obj is not None:
@@ -368,6 +373,8 @@ class DeviceEngine(AutotuneMixin):
                 self.ipc_selftest = {"ok": False, "failures": bad}
                 return None
             self._ipc_obj = inst
+            inst.on_change = self._invalidate_fast
+            self._invalidate_fast()
             self._probe_spin(inst)
         return self._ipc_obj
 
@@ -392,6 +399,52 @@ class DeviceEngine(AutotuneMixin):
         h = self._hier
         if h is not None and h.ipc is not None:
             h.ipc.raise_if_failed()
+
+    # ------------------------------------------------------------------ latency fast path
+    def _invalidate_fast(self) -> None:
+        """Forget every memoised latency-tier launch (any input of the decision changed: the pinned
+        table, a tier attribute, a registration, an instance, the epoch mode)."""
+        fa = self.__dict__.get("_fast_ar")
+        if fa:
+            fa.clear()
+
+    _FAST_MAX = 256
+
+    def _fast_remember(self, arr, frm, to, operator, operand, scale, view, op, algo: str) -> None:
+        """Memoise the native launch of a call that just took the staged latency tier (one-/two-
+        shot on the default instance, one piece, fused copy-in, in place, host epochs), keyed by
+        everything that decided it, so the next call of that shape runs ``mp4x_ipc_fast_allreduce``
+        from the public API's first lines (ProcessCommSlave.allreduceArray)."""
+        fa = self.__dict__.get("_fast_ar")
+        inst = self._ipc_obj
+        if fa is None or inst is None or inst._epoch_dev is not None or not inst._fuse_copy or \
+                self._probe_depth or os.environ.get("MP4X_FAST_PATH", "1") != "1":
+            return
+        from ..ops import native
+        lx = native.launch_ext()
+        if lx is None or not hasattr(lx, "fast_allreduce"):
+            return
+        total = view.numel() * view.element_size()
+        ptr = view.data_ptr()
+        if total % 16 or ptr % 16 or total > inst.nbytes or total > self.ipc_twoshot_max or \
+                not view.is_contiguous() or capturing_now():
+            return
+        from .ipc import ONESHOT, TWOSHOT
+        h = self._hier
+        words = [i._herr.value for i in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big,
+                                         h.ipc if h is not None else None) if i is not None and i._herr]
+        state = inst.fast_state(words)
+        if state is None:
+            return
+        a = ONESHOT if algo == "ipc1" else TWOSHOT
+        from ..operators import dtype_of_torch
+        key = (arr.data_ptr(), arr.numel(), frm, to, arr.dtype, operator, getattr(operand, "codec", None),
+               getattr(operand, "compress", False), scale)
+        if len(fa) >= self._FAST_MAX:
+            fa.clear()
+        fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr, total,
+                   inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
+                   "allreduce." + algo, inst)
 
     def _probe_spin(self, inst) -> None:
         if self._probe_depth and inst is not None:
@@ -584,6 +637,8 @@ class DeviceEngine(AutotuneMixin):
                 self.probe_failures.append({"instance": "large", "failures": bad})
                 return self._ipc_obj
             self._ipc_large = inst
+            inst.on_change = self._invalidate_fast
+            self._invalidate_fast()                # its error word joins the fast path's check
             self._probe_spin(inst)
             if self._ipc_obj is not None and self._ipc_obj._epoch_dev is not None:
                 inst.prepare_graph()   # a capture is being prepared: same epoch mode
@@ -603,6 +658,7 @@ class DeviceEngine(AutotuneMixin):
         """The node-aware allreduce (parallel/hier.py) of a job spanning >= 2 nodes of equal size,
         or None.  Collective, lazily created; a setup failure is agreed (every rank gets None)."""
         if self._hier is None and not self._hier_failed and self.layout.hier_ok():
+            self._invalidate_fast()
             from .hier import HierAllreduce
             try:
                 self._hier = HierAllreduce(self, self.layout)
@@ -724,6 +780,7 @@ class DeviceEngine(AutotuneMixin):
         pipelined pieces / sparse)."""
         if self.device.type != "cuda":
             raise Mp4jException("capture needs a GPU device engine")
+        self._invalidate_fast()
         for inst in (self.ipc(), self._ipc_large, self._ipc_fp8_big):
             if inst is not None:
                 inst.prepare_graph()
@@ -808,6 +865,9 @@ class DeviceEngine(AutotuneMixin):
         self._count("allreduce." + algo)
         fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view), capturing=capturing)
         self._post_scale(view, scale, fused)
+        if (algo == "ipc1" or algo == "ipc2") and out is None and not capturing and self._fast_ar is not None \
+                and view.is_cuda:
+            self._fast_remember(arr, frm, to, operator, operand, scale, view, op, algo)
         return arr
 
     @staticmethod
@@ -986,6 +1046,8 @@ class DeviceEngine(AutotuneMixin):
             self._ipc_fp8_big = None
             return self.ipc_large()
         self._ipc_fp8_big = inst
+        inst.on_change = self._invalidate_fast
+        self._invalidate_fast()
         return inst
 
     def _probe_instance(self, inst, large_forms: bool = False, fp8: bool = False) -> list:
@@ -1728,6 +1790,9 @@ def _tier_attr(name, default):
         d = self.__dict__
         d[slot] = v
         d["_state_ver"] = d.get("_state_ver", 0) + 1
+        fa = d.get("_fast_ar")
+        if fa:
+            fa.clear()
 
     return property(get, put, doc=f"tier input {name!r} (assignments invalidate the select memo)")
 

@@ -333,7 +333,9 @@ class IpcAllreduce:
         # integer addresses of the two pointer arrays, for the ctypes-free launcher
         self._pp_data_addr = ctypes.addressof(self._pp_data[1])
         self._pp_sig_addr = ctypes.addressof(self._pp_sig[1])
-        self.epoch = 0
+        self._epoch_box = (ctypes.c_uint32 * 1)()     # host epoch (also bumped by the native fast path)
+        self._fast_state = None    # native latency fast path state (fast_state())
+        self.on_change = None      # callback of the owning engine: registrations / epoch mode changed
         self._pp_hi = None         # peer pointers of the upper half-buffers (pipelined large path)
         self._copy_stream = None
         self._epoch_dev = None     # device epoch counter for graph-captured calls (lazy)
@@ -351,6 +353,58 @@ class IpcAllreduce:
         self._chunk_pool = None     # memAlloc chunk pool (VMM_POLICY "chunks", vmm.ChunkPool)
         # all ranks mapped before anyone launches
         comm.server.call("barrier", self.rank)
+
+    # ---------------------------------------------------------------- host epoch
+    @property
+    def epoch(self) -> int:
+        """The host-side epoch of the staged / zero-copy protocols (low 30 bits; graph mode uses
+        the device counter instead).  Kept in a native word (``_epoch_box``) that the latency fast
+        path (``mp4x_ipc_fast_allreduce``) bumps too, so both paths draw from ONE sequence."""
+        box = self.__dict__.get("_epoch_box")
+        return int(box[0]) if box is not None else 0
+
+    @epoch.setter
+    def epoch(self, v: int) -> None:
+        box = self.__dict__.get("_epoch_box")
+        if box is None:
+            box = self.__dict__["_epoch_box"] = (ctypes.c_uint32 * 1)()
+        box[0] = int(v)
+
+    def _changed(self) -> None:
+        cb = self.__dict__.get("on_change")
+        if cb is not None:
+            cb()
+
+    def fast_state(self, herr_words) -> Optional[int]:
+        """Address of the native latency fast path's state for this instance (csrc/runtime/ipc_ar.hip
+        ``FastAr``): ``herr_words`` = the pinned host error words of every IPC instance of the
+        engine (the fail-stop check of every call).  Rebuilt when the list changes."""
+        if self._epoch_dev is not None or not self._herr:
+            return None
+        words = tuple(int(w) for w in herr_words if w)[:8]
+        st = self._fast_state
+        if st is None or st[1] != words:
+            class _FastAr(ctypes.Structure):
+                _fields_ = [("herr", c_void_p * 8), ("epoch", c_void_p), ("data_ptrs", c_void_p),
+                            ("signal_ptrs", c_void_p), ("rank", ctypes.c_int32), ("p", ctypes.c_int32)]
+            s = _FastAr()
+            for i, w in enumerate(words):
+                s.herr[i] = w
+            s.epoch = ctypes.addressof(self._epoch_box)
+            s.data_ptrs = self._pp_data_addr
+            s.signal_ptrs = self._pp_sig_addr
+            s.rank, s.p = self.rank, self.p
+            st = self._fast_state = (s, words)
+        return ctypes.addressof(st[0])
+
+    def latency_blocks(self, total: int, algo: int, dtype, op) -> int:
+        """Grid of a staged one-/two-shot of ``total`` bytes (0 = the kernel's own default): on a
+        GPU shared by the ranks, the co-residency cap of that kernel (:meth:`grid_cap`)."""
+        if not self.shared_gpu:
+            return 0
+        vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
+        cap = self.grid_cap("oneshot" if algo == ONESHOT else "twoshot", dtype, op)
+        return max(1, min(cap, -(-min(total, self.nbytes) // 16 // vec_per_block)))
 
     # ---------------------------------------------------------------- fail-stop
     def host_error(self) -> int:
@@ -479,9 +533,7 @@ class IpcAllreduce:
             return out
         dt = int(dtype_of_torch(view.dtype))
         if not blocks and self.shared_gpu:
-            vec_per_block = 512          # kIpcThreads 16-byte vectors per block and grid step
-            cap = self.grid_cap("oneshot" if algo == ONESHOT else "twoshot", view.dtype, op)
-            blocks = max(1, min(cap, -(-min(total, self.nbytes) // 16 // vec_per_block)))
+            blocks = self.latency_blocks(total, algo, view.dtype, op)
         if overlap is None:
             overlap = self._overlap_default
         if capturing is None:                      # the engine's latency path already knows
@@ -656,6 +708,7 @@ class IpcAllreduce:
             # registered on this rank already but not on every rank: the new entry replaces it
             self._release(old)
         self._regs[key] = reg
+        self._changed()
         return True
 
     def _open_peer_base(self, hk, hs: int) -> int:
@@ -791,6 +844,7 @@ class IpcAllreduce:
             return
         if reg is not None:
             del self._regs[key]
+            self._changed()
         self._release_ordered(reg)
 
     def _find(self, view: torch.Tensor):
@@ -842,6 +896,7 @@ class IpcAllreduce:
             reg = pooled.pop()
             own_va = reg.vmm[0].va
             self._regs[(own_va, nb16)] = reg
+            self._changed()
             t = vmm.tensor_at(own_va, nb16, torch.uint8, torch.device("cuda", self.device))
             return t[:nbytes // es * es].view(dtype)
         own = scr = None
@@ -912,6 +967,7 @@ class IpcAllreduce:
         reg.scratch = scratch if push else None
         t = vmm.tensor_at(own.va, nb16, torch.uint8, torch.device("cuda", self.device))
         self._regs[(own.va, nb16)] = reg
+        self._changed()
         return t[:nbytes // es * es].view(dtype)
 
     def _mem_alloc_chunks(self, nbytes: int, nb16: int, es: int, dtype: torch.dtype) -> torch.Tensor:
@@ -1003,6 +1059,7 @@ class IpcAllreduce:
         reg.scratch = scratch if push else None
         t = vmm.tensor_at(maps[0].va, nb16, torch.uint8, torch.device("cuda", self.device))
         self._regs[(maps[0].va, nb16)] = reg
+        self._changed()
         return t[:nbytes // es * es].view(dtype)
 
     def mem_free(self, t: torch.Tensor) -> None:
@@ -1018,6 +1075,7 @@ class IpcAllreduce:
         torch.cuda.synchronize(self.device)
         self.comm.server.call("barrier", self.rank)     # no peer kernel still reads or writes it
         reg = self._regs.pop(key)
+        self._changed()
         if reg.chunks is not None:
             # chunk pool: unmap every view (own + peers', VA ranges stay reserved) and return this
             # rank's chunks to its pool; nothing is released (csrc/runtime/vmm.hip says why)
@@ -1819,6 +1877,8 @@ class IpcAllreduce:
         if self._epoch_dev is None:
             torch.cuda.synchronize()
             self._epoch_dev = torch.full((1,), self.epoch, dtype=torch.int32, device="cuda")
+            self._fast_state = None
+            self._changed()
         return self
 
     def error_word(self, clear: bool = False) -> int:
@@ -1846,6 +1906,8 @@ class IpcAllreduce:
         cannot agree) the halves run back to back."""
         if self.lib is None:
             return
+        self._fast_state = None
+        self._changed()
         if sync:
             torch.cuda.synchronize()
         if self._sig and self._herr:

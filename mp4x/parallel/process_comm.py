@@ -113,6 +113,7 @@ class ProcessCommSlave:
         self.loginName = loginName or os.environ.get("USER", "mp4x")
         self.closed = False
         self._device_engine = None
+        self._fast_ar = None       # the device engine's latency memo (allreduceArray fast path)
         self._device_index = device
         self._shm = None
         LOG.info("master host:%s, master port:%s", masterHost, masterPort)
@@ -277,7 +278,41 @@ class ProcessCommSlave:
         if self._device_engine is None:
             from .device_engine import DeviceEngine
             self._device_engine = DeviceEngine(self, self._device_index)
+            self._enable_fast_path()
         return self._device_engine
+
+    def _enable_fast_path(self) -> None:
+        """Arm the allreduceArray latency fast path (VERDICT r4 Next #5): a call whose shape the
+        device engine memoised (staged one-/two-shot on the default IPC instance) goes from the
+        API's first lines to ONE native call, ``mp4x_ipc_fast_allreduce`` (error words, capture
+        check, epoch, launch).  Off with fault injection (it counts every API call) or
+        ``MP4X_FAST_PATH=0``."""
+        eng = self._device_engine
+        from ..ops import native
+        if eng is None or self._fault.active or self.slaveNum < 2 or os.environ.get("MP4X_FAST_PATH", "1") != "1" \
+                or getattr(eng.device, "type", None) != "cuda":
+            return
+        lx = native.launch_ext()
+        if lx is None or not hasattr(lx, "fast_allreduce") or eng._fast_ar is None:
+            return
+        import torch
+        self._fast_lx = lx.fast_allreduce
+        self._fast_stream = native.stream_ptr
+        self._fast_tensor = torch.Tensor
+        self._fast_calls = self.stats["calls"]
+        self._fast_ar = eng._fast_ar
+
+    def _fast_after(self, ent) -> None:
+        """Book-keeping of a fast-path call: the API and engine call counts, and the watchdog's
+        device-side coverage (an event when none is outstanding, as ``CollectiveWatchdog.end``)."""
+        c = self._fast_calls
+        c["allreduceArray"] = c.get("allreduceArray", 0) + 1
+        eng = self._device_engine
+        st = eng.stats
+        st[ent[8]] = st.get(ent[8], 0) + 1
+        wd = eng.watchdog
+        if wd is not None and not wd._npending:
+            wd.end(wd.begin("allreduce"), eng.device)
 
     def registerBuffer(self, tensor) -> bool:
         """Collective (extension, like ``ncclCommRegister``): map a device tensor into every peer
@@ -779,6 +814,15 @@ class ProcessCommSlave:
         ``scale`` (extension, float data): the result is multiplied by it — e.g. ``1/p`` for a
         gradient average; on the device it is fused into the collective's final write.
         """
+        fast = self._fast_ar
+        if fast and out is None and type(arrData) is self._fast_tensor and arrData.is_contiguous():
+            ent = fast.get((arrData.data_ptr(), arrData.numel(), frm, to, arrData.dtype, operator, operand.codec,
+                            operand.compress, scale))
+            if ent is not None and self._fast_lx(ent, self._fast_stream()) == 0:
+                self._fast_after(ent)
+                return arrData
+            # not memoised, or not launched (rc 1003: an earlier collective failed; 1004: the stream
+            # is being captured): the full path decides, raises or records
         self._tick("allreduceArray")
         if scale != 1.0:
             if _is_device_tensor(arrData) and self.slaveNum > 1:

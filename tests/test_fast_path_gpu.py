@@ -1,0 +1,83 @@
+"""The allreduceArray latency fast path (VERDICT r4 Next #5): a repeated small device allreduce
+goes from the public API's first lines to ONE native call (mp4x_ipc_fast_allreduce: error words,
+capture check, epoch, launch) — exact every call, counted like the full path, invalidated when
+anything that decided it changes, and failing loudly when an earlier collective timed out.
+Two ranks share GPU 0 (the IPC kernels run for real)."""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from spawn_ranks import run_spawn  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _pat(n, r, k):
+    return ((torch.arange(n, device="cuda", dtype=torch.int32) + k) % 13 + r).float()
+
+
+def _exp(n, p, k):
+    i = (torch.arange(n, device="cuda", dtype=torch.int32) + k) % 13
+    return (i * p + p * (p - 1) // 2).float()
+
+
+def _fast_fn(comm):
+    import ctypes
+    from mp4x import Operands, Operators
+    from mp4x.exceptions import Mp4jException
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    eng.ipc()
+    F, SUM = Operands.FLOAT_OPERAND(), Operators.Float.SUM
+    out = {}
+    for n, tag in ((1024, "4KiB"), ((1 << 20) // 4, "1MiB")):
+        x = torch.empty(n, device="cuda")
+        bad = 0
+        for k in range(40):
+            x.copy_(_pat(n, r, k))
+            comm.allreduceArray(x, Operands.FLOAT_OPERAND(), SUM, 0, n)   # a fresh operand object each call
+            torch.cuda.synchronize()
+            bad += int((x != _exp(n, p, k)).sum())
+        out[tag] = {"bad": bad, "memo": len(eng._fast_ar)}
+        # fused scale through the fast path (the DP average)
+        x.copy_(_pat(n, r, 3))
+        for _ in range(3):
+            comm.allreduceArray(x, F, SUM, 0, n, scale=1.0 / p)
+        torch.cuda.synchronize()
+        out[tag]["scale_bad"] = int((x != _exp(n, p, 3) / p).sum())
+    calls = comm.stats["calls"].get("allreduceArray", 0)
+    eng_calls = sum(v for k, v in eng.stats.items() if k in ("allreduce.ipc1", "allreduce.ipc2"))
+    # an earlier collective that timed out fails the next call (no launch), then the job goes on
+    x = torch.empty(1024, device="cuda")
+    comm.barrier()
+    ctypes.c_uint32.from_address(eng._ipc_obj._herr.value).value = 1
+    raised = None
+    try:
+        comm.allreduceArray(x, F, SUM, 0, 1024)
+    except Mp4jException as e:
+        raised = str(e)
+    comm.barrier()
+    x.copy_(_pat(1024, r, 5))
+    comm.allreduceArray(x, F, SUM, 0, 1024)
+    torch.cuda.synchronize()
+    after_fail_bad = int((x != _exp(1024, p, 5)).sum())
+    # a registration (an input of the decision) clears the memo
+    before = len(eng._fast_ar)
+    y = torch.empty(1 << 20, device="cuda")
+    comm.registerBuffer(y)
+    cleared = len(eng._fast_ar) == 0 and before > 0
+    comm.deregisterBuffer(y)
+    return {"sizes": out, "calls": calls, "eng_calls": eng_calls, "raised": raised,
+            "after_fail_bad": after_fail_bad, "cleared": cleared}
+
+
+def test_fast_path_is_exact_counted_invalidated_and_fail_stop():
+    out = run_spawn(2, _fast_fn, timeout=240)
+    for r, o in out.items():
+        for tag, v in o["sizes"].items():
+            assert v["bad"] == 0 and v["scale_bad"] == 0, (r, tag, v)
+            assert v["memo"] >= 1, (r, tag, v)          # the shape was memoised
+        assert o["calls"] == 2 * 43, o                   # every API call counted, fast or not
+        assert o["eng_calls"] == 2 * 43, o
+        assert o["raised"] and "timed out" in o["raised"], o
+        assert o["after_fail_bad"] == 0 and o["cleared"], o

@@ -73,7 +73,8 @@ def test_headline_survives_a_hang_after_it(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--cpu", "--gpus", "2", "--steps", "3", "--warmup", "1", "--bytes", "4000000"]
     pr = subprocess.Popen(cmd, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                          env=dict(os.environ, PYTHONPATH=ROOT, MP4X_BENCH_TEST_HANG="extras"),
+                          env=dict(os.environ, PYTHONPATH=ROOT, MP4X_BENCH_TEST_HANG="extras",
+                                   MP4X_BENCH_TEST_HANG_S="60"),
                           start_new_session=True)
     got = None
     t0 = time.monotonic()
@@ -87,7 +88,20 @@ def test_headline_survives_a_hang_after_it(tmp_path):
         time.sleep(1.0)
         assert pr.poll() is None, "the hook should hang the run after the headline"
     finally:
-        os.killpg(pr.pid, signal.SIGKILL)          # what the driver's timeout does
+        # what the driver's timeout does: the launcher and every rank it started (the ranks lead
+        # process groups of their own, so each is killed by its exact pid)
+        import psutil
+        try:
+            kids = psutil.Process(pr.pid).children(recursive=True)
+        except psutil.NoSuchProcess:
+            kids = []
+        for k in kids:
+            try:
+                k.kill()
+            except psutil.NoSuchProcess:
+                pass
+        os.killpg(pr.pid, signal.SIGKILL)
         pr.wait(30)
+        psutil.wait_procs(kids, timeout=30)
     assert got is not None and got["phase"] == "headline" and got["verified"] is True, got
     assert got["value"] > 0 and got["n_gpus"] == 2
