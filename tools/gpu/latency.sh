@@ -1,5 +1,5 @@
-export OUT=r5c
-source tools/gpu/steps.sh
+export OUT=${OUT:-latency}
+source "$(dirname "$0")/steps.sh"
 export TMPDIR=/tmp
 PYT="python -u -m pytest -v --timeout 300 --timeout-method thread -p no:cacheprovider -m gpu"
 step fast_tests 600 $PYT tests/test_fast_path_gpu.py tests/test_ipc_straggler_gpu.py tests/test_graph_gpu.py tests/test_ipc_gpu.py
