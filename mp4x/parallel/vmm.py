@@ -251,8 +251,9 @@ class VmmRegion:
     def free(self, keep_va: Optional[List] = None) -> None:
         """Unmap + release the chunks and free the VA range — or, with ``keep_va`` (a list),
         keep the range reserved and append ``(va, bytes)`` to it: the physical memory goes back
-        to the device but no later reservation of this process lands on these addresses
-        (:func:`free_ranges` releases them at communicator close)."""
+        to the device but no later reservation of this process lands on these addresses.  Kept
+        ranges stay reserved for the life of the PROCESS (:data:`_QUARANTINE`, also across
+        communicators): a VA free breaks later exports on this runtime (csrc/runtime/vmm.hip)."""
         self.close_fds()
         if self.va:
             if keep_va is not None:
@@ -267,7 +268,12 @@ class VmmRegion:
 class _VaQuarantine(list):
     """Process-wide record of the VA ranges this process keeps reserved instead of freeing
     (hipMemAddressFree breaks later exports on this runtime, see csrc/runtime/vmm.hip): they
-    hold no physical memory, only address space (the GPU VA space is 2^48 bytes)."""
+    hold no physical memory, only address space.  Nothing releases them before the process
+    exits.  Growth: one memAlloc / memFree cycle of B bytes at p ranks keeps about
+    p * (B + B * (p - 1) / p) bytes of VA per process (the own range, p - 1 imported views, and
+    the push scratch's ranges); against the 2^48-byte GPU VA space that is ~16,000 cycles of 1 GB
+    tensors at p = 8 — fine for long-lived arenas (DDP buckets, ZeRO shards), not for a memAlloc
+    per step.  ``quarantined_bytes()`` reports it (tests/test_vmm_chunks_cpu.py)."""
 
 
 _QUARANTINE = _VaQuarantine()

@@ -128,6 +128,7 @@ def test_chunk_pool_reuses_chunks_across_sizes_and_sends_only_new_ones(monkeypat
     server = _Server(p)
     out = [None] * p
     errs = []
+    q0 = vmm.quarantined_bytes()
 
     def run(r):
         tls.rank = r
@@ -170,6 +171,12 @@ def test_chunk_pool_reuses_chunks_across_sizes_and_sends_only_new_ones(monkeypat
         assert rows[1][3] == (1, 2 * 1)
         assert rows[2][3] == (0, 0) and rows[3][3] == (0, 0)
         assert owned == [2 * MiB, 4 * MiB, 8 * MiB, 8 * MiB]
+    # the VA the cycles keep reserved (documented growth, vmm._VaQuarantine): per rank and cycle,
+    # its own range and p - 1 imported views of the tensor and of the push scratch
+    def span(nbytes):
+        return sum(chunk_sizes(nbytes, 2 * MiB))
+    per_cycle = {mb: p * (span(mb * MiB) + span((p - 1) * (-(-(mb * MiB // 16) // p)) * 16)) for mb in (10, 12, 3)}
+    assert vmm.quarantined_bytes() - q0 == p * sum(per_cycle[mb] for mb in (10, 12, 10, 3))
     for _, _, inst in out:
         inst.close(sync=False)
     owned_handles = {h for h, tag in lib.tags.items()}
