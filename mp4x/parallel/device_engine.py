@@ -568,9 +568,10 @@ class DeviceEngine(AutotuneMixin):
         step("broadcast_1MiB", bcast)
         if self._zc:
             # on a dedicated plain allocation (a tensor from the caching allocator may sit in a
-            # segment too large to map, see ipc.IPC_OPEN_MAX), then on a memAlloc (VMM) tensor
-            for name, fn in (("zero_copy_twoshot_and_plans_4MiB", lambda: inst.selftest_zero_copy(n4m)),
-                             ("zero_copy_memalloc_1MiB", lambda: inst.selftest_memalloc(min(cap, 1 << 18)))):
+            # segment too large to map, see ipc.IPC_OPEN_MAX).  The memAlloc (VMM-imported) region
+            # is checked at the first memAlloc instead (_memalloc_self_test): a job that never
+            # calls it never maps a VMM import across GPUs (first contact keeps to hipIpc).
+            for name, fn in (("zero_copy_twoshot_and_plans_4MiB", lambda: inst.selftest_zero_copy(n4m)),):
                 try:
                     nbad = fn()
                     if nbad:
@@ -588,8 +589,6 @@ class DeviceEngine(AutotuneMixin):
             fails.append(f"set_spin: {e}")
         if os.environ.get("MP4X_IPC_SELFTEST_INJECT", "").strip() == str(r):   # failure-path tests
             fails.append("injected failure (MP4X_IPC_SELFTEST_INJECT)")
-        if os.environ.get("MP4X_IPC_SELFTEST_INJECT_MEMALLOC", "").strip() == str(r):
-            fails.append("zero_copy_memalloc_1MiB: injected failure (MP4X_IPC_SELFTEST_INJECT_MEMALLOC)")
         allf = self.comm.server.call("allgather_obj", self.rank, fails)
         bad = [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
         self.ipc_selftest = {"ok": not bad, "failures": bad, "seconds": round(time.perf_counter() - t0, 3)}
@@ -898,6 +897,45 @@ class DeviceEngine(AutotuneMixin):
         if self._ipc_obj is not None:
             self._ipc_obj.deregister(self._flat(t))
 
+    _memalloc_checked = False
+
+    def _memalloc_self_test(self) -> None:
+        """Collective, once, at the first memAlloc: the VMM-imported region through the zero-copy
+        two-shot, pull and push, twice on the same memory, in two alloc / free cycles
+        (``IpcAllreduce.selftest_memalloc``), exact, agreed.  On failure memAlloc hands out
+        registered plain tensors on every rank (``_zc_vmm`` False); the zero-copy forms on
+        registered tensors stay.  ``MP4X_IPC_SELFTEST_INJECT_MEMALLOC=<rank>`` rehearses it."""
+        self._memalloc_checked = True
+        inst = self._ipc_obj
+        fails = []
+        try:
+            inst.set_spin(float(os.environ.get("MP4X_IPC_SELFTEST_SPIN_S", "2")))
+            nbad = inst.selftest_memalloc(min(inst.nbytes // 4, 1 << 18))
+            if nbad:
+                fails.append(f"zero_copy_memalloc_1MiB: {'setup failed' if nbad < 0 else f'{nbad} wrong elements'}")
+            torch.cuda.synchronize(self.device)
+            code = inst.host_error()
+            inst.raise_if_failed()
+            if code:
+                fails.append(f"zero_copy_memalloc_1MiB: barrier timeout {code}")
+        except Exception as e:   # noqa: BLE001
+            fails.append(f"zero_copy_memalloc_1MiB: {type(e).__name__}: {e}")
+        try:
+            from .ipc import probe_spin, spin_default
+            inst.set_spin(probe_spin() if self._probe_depth else spin_default())
+        except Exception as e:   # noqa: BLE001
+            fails.append(f"set_spin: {e}")
+        if os.environ.get("MP4X_IPC_SELFTEST_INJECT_MEMALLOC", "").strip() == str(self.rank):
+            fails.append("zero_copy_memalloc_1MiB: injected failure (MP4X_IPC_SELFTEST_INJECT_MEMALLOC)")
+        allf = self.comm.server.call("allgather_obj", self.rank, fails)
+        bad = [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
+        self.ipc_selftest = dict(self.ipc_selftest or {}, zero_copy_memalloc=not bad)
+        if bad:
+            LOG.warning("rank %d: IPC memAlloc zero-copy self-test failed (%s): memAlloc falls back to "
+                        "registered plain tensors on every rank", self.rank, bad)
+            self._zc_vmm = False
+            self.ipc_selftest["memalloc_failures"] = bad
+
     def mem_alloc(self, n: int, dtype: torch.dtype) -> Optional[torch.Tensor]:
         """Collective: an ``n``-element tensor mapped into every peer at any size (see
         ``IpcAllreduce.mem_alloc``), or None on every rank when there is no IPC mesh (the
@@ -906,6 +944,8 @@ class DeviceEngine(AutotuneMixin):
         (hipIpc, up to the IPC open limit) stands in for the VMM one."""
         if self.p < 2 or self.device.type != "cuda" or self.ipc() is None or not self._zc:
             return None
+        if not self._memalloc_checked and self._zc_vmm and os.environ.get("MP4X_IPC_SELFTEST", "1") != "0":
+            self._memalloc_self_test()
         es = torch.empty((), dtype=dtype).element_size()
         if not self._zc_vmm:
             from .ipc import IPC_OPEN_MAX
