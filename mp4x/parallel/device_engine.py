@@ -818,14 +818,17 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
 
     # ================================================================== allreduce
     def allreduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand=None, small: bool = False,
-                  out: Optional[torch.Tensor] = None, scale: float = 1.0):
+                  out: Optional[torch.Tensor] = None, scale: float = 1.0, memo: bool = False):
         """In-place allreduce of ``arr[frm:to]``; with ``out`` the result goes to ``out[frm:to]``
         and ``arr`` is left untouched (the staged IPC kernels write ``out`` directly; other
         schedules copy into ``out`` first and run in place there).
 
         ``scale`` (float dtypes): the result is multiplied by it — the 1/p average of a DP
         gradient sync fused into the collective's own final write (IPC kernels, fp8 requantise)
-        or RCCL's ncclAvg, instead of a separate pass over the buffer."""
+        or RCCL's ncclAvg, instead of a separate pass over the buffer.
+
+        ``memo`` (the public API's full path): memoise this call shape's native launch when it took
+        the staged latency tier, for ProcessCommSlave.allreduceArray's fast path."""
         if frm == 0 and arr.dim() == 1 and to == arr.shape[0] and arr.is_contiguous():
             view = arr                    # the whole 1-D tensor: no view objects on the latency tier
         else:
@@ -866,8 +869,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         self._count("allreduce." + algo)
         fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view), capturing=capturing)
         self._post_scale(view, scale, fused)
-        if (algo == "ipc1" or algo == "ipc2") and out is None and not capturing and self._fast_ar is not None \
-                and view.is_cuda:
+        if memo and (algo == "ipc1" or algo == "ipc2") and out is None and not capturing and \
+                self._fast_ar is not None and view.is_cuda:
             self._fast_remember(arr, frm, to, operator, operand, scale, view, op, algo)
         return arr
 

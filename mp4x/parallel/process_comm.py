@@ -827,7 +827,8 @@ class ProcessCommSlave:
         if scale != 1.0:
             if _is_device_tensor(arrData) and self.slaveNum > 1:
                 CommUtils.isFromToLegal(frm, to)
-                return self.device.allreduce(arrData, frm, to, operator, operand, out=out, scale=scale)
+                return self.device.allreduce(arrData, frm, to, operator, operand, out=out, scale=scale,
+                                             memo=out is None)
             res = self.allreduceArray(arrData, operand, operator, frm, to, out=out)
             tgt = res.view(-1)[frm:to] if _is_torch(res) else res[frm:to]
             tgt *= scale
@@ -855,7 +856,7 @@ class ProcessCommSlave:
             return arrData
         CommUtils.isFromToLegal(frm, to)
         if _is_device_tensor(arrData):
-            return self.device.allreduce(arrData, frm, to, operator, operand)
+            return self.device.allreduce(arrData, frm, to, operator, operand, memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         shm = self._shm_engine(buf, operand, operator, to - frm)
         if shm is not None and buf.flags.c_contiguous:
