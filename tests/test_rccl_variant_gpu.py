@@ -23,9 +23,13 @@ def _job(port, q):
             eng.rccl_variant(ctas).all_reduce(t, 0)
         ok = bool(torch.all(t == 3.0).item())
         big = torch.ones(32 << 20, device="cuda:0")          # 128 MiB: variants are candidates
+        import os
+        os.environ.pop("MP4X_AUTOTUNE_EXTRA", None)
+        default = eng.autotune_allreduce(big, Operators.Float.SUM, iters=1)
+        os.environ["MP4X_AUTOTUNE_EXTRA"] = "1"               # the variants are opt-in schedules
         res = eng.autotune_allreduce(big, Operators.Float.SUM, iters=2)
         comm.close(0)
-        q.put(("ok", ok, res))
+        q.put(("ok", ok, (default, res)))
     except BaseException:
         q.put(("err", traceback.format_exc(), None))
 
@@ -41,6 +45,8 @@ def test_rccl_cta_variants_and_autotune():
         st, ok, res = q.get(timeout=300)
         assert st == "ok", ok
         assert ok
+        default, res = res
+        assert "rccl" in default and not any(k.startswith("rccl_c") for k in default), default
         assert {"rccl", "rccl_c64", "rccl_c112"} <= set(res), res
         assert all(v < float("inf") for k, v in res.items() if k.startswith("rccl")), res
     finally:
