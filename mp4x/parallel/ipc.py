@@ -324,7 +324,9 @@ class IpcAllreduce(IpcForms):
                     os.close(fd)
         oks, anybad = _agree(comm, self.rank, b"" if err is None else err.encode(), bool)
         if anybad:
-            self.close(sync=False)
+            # agreed on every rank (job-wide for a sub-mesh): some peers may have mapped this
+            # rank's buffers already, so the teardown is ordered like any other
+            self.close(sync=False, collective=True)
             bad = [(i, bytes(o).decode()) for i, o in enumerate(oks) if o]
             raise Mp4jException(f"IPC peer mapping failed on ranks {bad or 'of another node'}")
         self._pp_data = ptr_array(self.data_ptrs)
@@ -959,8 +961,7 @@ class IpcAllreduce(IpcForms):
                     os.close(fd)
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
-            self.comm.server.call("barrier", self.rank)
-            self._release(reg)
+            self._release_ordered(reg)          # agreed: every rank is here
             raise Mp4jException(f"memAlloc({nbytes}) peer mapping failed on ranks "
                                 f"{[(i, o) for i, o in enumerate(oks) if o]}")
         reg.scratch = scratch if push else None
@@ -1047,11 +1048,10 @@ class IpcAllreduce(IpcForms):
                     os.close(fd)
         oks = self.comm.server.call("allgather_obj", self.rank, err)
         if any(oks):
-            self.comm.server.call("barrier", self.rank)
             # a chunk sent in THIS call may be missing on some peer: never hand it out again
             sent = set(map(id, new_own))
             reg.chunks = [c for c in reg.chunks if id(c) not in sent]
-            self._release(reg)
+            self._release_ordered(reg)          # agreed: every rank is here
             pool.discard(new_own)
             raise Mp4jException(f"memAlloc({nbytes}) peer mapping failed on ranks "
                                 f"{[(i, o) for i, o in enumerate(oks) if o]}")
