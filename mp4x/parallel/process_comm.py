@@ -815,7 +815,7 @@ class ProcessCommSlave:
         gradient average; on the device it is fused into the collective's final write.
         """
         fast = self._fast_ar
-        if fast and out is None and type(arrData) is self._fast_tensor and arrData.is_contiguous():
+        if fast and out is None and type(arrData) is self._fast_tensor and arrData.is_cuda and arrData.is_contiguous():
             ent = fast.get((arrData.data_ptr(), arrData.numel(), frm, to, arrData.dtype, operator, operand.codec,
                             operand.compress, scale))
             if ent is not None and self._fast_lx(ent, self._fast_stream()) == 0:
