@@ -283,3 +283,50 @@ def test_self_test_failure_scope(monkeypatch, fails, zc, enabled, zc_vmm):
     got = e.ipc()
     assert e._zc is zc and e.ipc_enabled is enabled and e._zc_vmm is zc_vmm
     assert (got is not None) is enabled and _FakeInst.closed is (not enabled)
+
+
+def test_latency_fast_path_memo_is_invalidated_by_every_decision_input():
+    """The allreduceArray fast path replays a memoised native launch; every input of the decision
+    that produced it clears the memo: a tier attribute, the pinned table, an IPC instance's
+    registrations / epoch mode (its ``on_change`` callback), capture and teardown."""
+    from mp4x.parallel.autotune import _TunedTable
+    e = _engine()
+    e._fast_ar = {}
+    e._tuned = _TunedTable()
+    e._tuned.on_change = e._invalidate_fast
+
+    def fill():
+        e._fast_ar[("shape",)] = ("launch",)
+
+    fill()
+    e.algo = "auto"                      # a tier attribute (even re-assigned to the same value)
+    assert not e._fast_ar
+    fill()
+    e._tuned[("k",)] = "rccl"            # the pinned table
+    assert not e._fast_ar
+    fill()
+    e._tuned.clear()
+    assert not e._fast_ar
+
+    import mp4x.parallel.ipc as ipcm
+    inst = object.__new__(ipcm.IpcAllreduce)
+    inst.on_change = e._invalidate_fast
+    fill()
+    inst._changed()                      # register / deregister / memAlloc / prepare_graph / close
+    assert not e._fast_ar
+    e._stop_watchdog = lambda: None
+    e._owns_pg = False
+    fill()
+    e.abort()                            # teardown
+    assert not e._fast_ar
+
+
+def test_fast_path_memo_only_from_the_public_api(monkeypatch):
+    """Direct engine callers (DDP, ThreadComm internals) never pay the memo's bookkeeping: only the
+    public API's full path asks for it (``memo=True``)."""
+    import inspect
+    from mp4x.parallel import process_comm
+    from mp4x.parallel.device_engine import DeviceEngine
+    assert inspect.signature(DeviceEngine.allreduce.__wrapped__).parameters["memo"].default is False
+    src = inspect.getsource(process_comm.ProcessCommSlave.allreduceArray)
+    assert "memo=" in src and "self._fast_lx(ent, self._fast_stream())" in src
