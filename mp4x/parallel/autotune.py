@@ -84,6 +84,24 @@ class _TunedTable(dict):
         return super().setdefault(k, d)
 
 
+_DIAG = os.environ.get("MP4X_AUTOTUNE_DIAG", "0") == "1"
+
+
+def _diag_mismatch(rank: int, name: str, got: torch.Tensor, exp: torch.Tensor) -> None:
+    """``MP4X_AUTOTUNE_DIAG=1``: what a wrong probe result holds (stderr, one line per rank): the
+    count, the first mismatches (index, got, expected) and how many wrong elements are the probe's
+    fill (-1), zero, or another rank's pattern value."""
+    import sys
+    bad = (got != exp).nonzero().flatten()
+    if bad.numel() == 0:
+        return
+    g, e = got[bad], exp[bad]
+    first = [(int(i), float(a), float(b)) for i, a, b in zip(bad[:6].tolist(), g[:6].tolist(), e[:6].tolist())]
+    print(f"[autotune-diag] rank {rank} {name}: {bad.numel()} of {got.numel()} wrong; first {first}; "
+          f"fill(-1) {int((g == -1).sum())}, zero {int((g == 0).sum())}, "
+          f"span [{int(bad[0])}, {int(bad[-1])}]", file=sys.stderr, flush=True)
+
+
 class AutotuneMixin:
     """The tuners, probes and the persisted table; state lives on the engine."""
 
@@ -315,6 +333,8 @@ class AutotuneMixin:
 
             def check():
                 bad = int((view != exp).sum()) if self.rank == root else 0
+                if bad and _DIAG:
+                    _diag_mismatch(self.rank, "reduce", view, exp)
                 view.zero_()
                 return bad
             return check
@@ -348,6 +368,8 @@ class AutotuneMixin:
 
             def check():
                 bad = int((view != exp).sum())
+                if bad and _DIAG:
+                    _diag_mismatch(self.rank, "broadcast", view, exp)
                 view.zero_()
                 return bad
             return check
@@ -373,8 +395,12 @@ class AutotuneMixin:
             def check():
                 if kind == "gather":
                     bad = int((view != exp).sum()) if r == root else 0
+                    if bad and _DIAG:
+                        _diag_mismatch(r, "gather", view, exp)
                 else:
                     bad = int((view[froms[r]:tos[r]] != exp[froms[r]:tos[r]]).sum())
+                    if bad and _DIAG:
+                        _diag_mismatch(r, "scatter", view[froms[r]:tos[r]], exp[froms[r]:tos[r]])
                 view.zero_()
                 return bad
             return check
@@ -417,7 +443,12 @@ class AutotuneMixin:
             failed = 1
         timeout = self._ipc_error_flag() if uses_ipc else 0
         warm_us = int(min(warm, 1e9) * 1e6)
-        failed, timeout, nwrong, warm_us = self._agree([failed, timeout, wrong, warm_us])
+        local = [failed, timeout, wrong, warm_us]
+        failed, timeout, nwrong, warm_us = self._agree(local)
+        if _DIAG and (failed or timeout or nwrong):
+            import sys
+            print(f"[autotune-diag] rank {self.rank} {name}: local [failed, timeout, wrong, warm_us] {local} -> "
+                  f"agreed {[failed, timeout, nwrong, warm_us]}", file=sys.stderr, flush=True)
         second = getattr(check, "second", None) if not (failed or timeout or nwrong) else None
         if second is not None:     # agreed: every rank runs the second probe call together
             try:

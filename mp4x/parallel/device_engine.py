@@ -629,7 +629,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 self._ipc_large_failed = True
                 return self._ipc_obj
             # first use of a fresh mesh: every form this instance serves, exact, agreed
-            bad = self._probe_instance(inst, large_forms=True)
+            bad = self._probe_instance(inst, large_forms=True) \
+                if os.environ.get("MP4X_TEST_SKIP_FIRST_USE_PROBE", "0") != "1" else []
             if bad:
                 LOG.warning("rank %d: large-message IPC instance failed its first-use probe (%s): dropped on "
                             "every rank, the default instance serves those calls", self.rank, bad)

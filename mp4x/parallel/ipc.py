@@ -113,6 +113,10 @@ CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
 # MP4X_TEST_UNORDERED_RELEASE=1 restores that order (owner frees first, no barrier) — for the
 # regression test that shows the first-use probes catch it; never for a job.
 UNORDERED_RELEASE = os.environ.get("MP4X_TEST_UNORDERED_RELEASE", "0") == "1"
+# MP4X_TEST_FREE_SCRATCH=1: round 4's push-scratch handling (freed at deregistration, the peers'
+# mappings of it closed) instead of the pool — the trigger of round 4's corruption; diagnosis only
+# (tools/gpu/r4repro.sh, profiles/r5/rootcause/).
+FREE_SCRATCH = os.environ.get("MP4X_TEST_FREE_SCRATCH", "0") == "1"
 VMM_POLICIES = ("chunks", "fresh_va", "ordered", "hint", "keep_owner_va", "keep_import_va", "pool")
 VMM_POLICY = os.environ.get("MP4X_VMM_POLICY") or (
     "pool" if os.environ.get("MP4X_VMM_RELEASE") == "0" else "chunks")
@@ -181,7 +185,7 @@ def _agree(comm, rank, obj, is_bad):
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
-    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "chunks")
+    __slots__ = ("peers", "scratch", "keep", "scratch_alloc", "vmm", "nown", "peer_keys", "chunks", "scr_keys")
 
     def __init__(self, keep=None):
         self.peers: List[int] = []
@@ -192,6 +196,7 @@ class _Reg:
         self.nown = 0
         self.peer_keys: list = []        # (rank, handle bytes) of every peer mapping this one uses
         self.chunks = None               # memAlloc under the chunk pool: this rank's chunks
+        self.scr_keys: list = []         # the peer_keys that are push scratches
 
 
 class IpcAllreduce(IpcForms):
@@ -693,6 +698,7 @@ class IpcAllreduce(IpcForms):
                     sk = (r, bytes(b[4]))
                     scr.append(self._open_peer_base(sk, hs))
                     reg.peer_keys.append(sk)
+                    reg.scr_keys.append(sk)
         except Exception as e:   # noqa: BLE001
             err = str(e)
         reg.scratch = scr if push else None
@@ -725,29 +731,47 @@ class IpcAllreduce(IpcForms):
         self._peer_refs[hk] = self._peer_refs.get(hk, 0) + 1
         return ent.value
 
-    def _close_peer(self, hk) -> None:
+    def _close_peer(self, hk, keep: bool = False) -> None:
         """Drop one registration's use of peer mapping ``hk``; the last one closes it
-        (``CLOSE_PEERS``; otherwise it stays cached until close())."""
+        (``CLOSE_PEERS``; otherwise it stays cached until close()).  ``keep``: a peer's pooled
+        push scratch — its mapping stays open for the next registration the owner hands the
+        same scratch to (same handle bytes)."""
         n = self._peer_refs.get(hk, 0) - 1
         if n > 0:
             self._peer_refs[hk] = n
             return
         self._peer_refs.pop(hk, None)
-        if CLOSE_PEERS:
+        if CLOSE_PEERS and not keep:
             ptr = self._peer_bases.pop(hk, None)
             if ptr is not None:
                 native.soft_check(self.lib.mp4x_ipc_close_handle(ptr), "ipc_close_handle", LOG)
+
+    @staticmethod
+    def _scratch_class(size: int) -> int:
+        """Pool size class of a push scratch of ``size`` bytes: the next power of two (>= 64 KiB),
+        or the exact size where that power of two is above the IPC open limit."""
+        c = 1 << 16
+        while c < size:
+            c <<= 1
+        return c if c <= IPC_OPEN_MAX else size
 
     def _alloc_scratch(self, nbytes: int, hs: int):
         """Receive scratch of the push two-shot for a registered tensor of ``nbytes``: p-1 chunk
         slots, uncached (peers write it over xGMI, this rank reads it once per call).  Returns
         (allocation, IPC handle), or (None, None): the registration then has no push form.
-        Without ``CLOSE_PEERS``, a scratch of the same size that an earlier deregistration
-        returned is reused (the peers' mappings of it stay cached by handle)."""
+
+        Scratches are POOLED per power-of-two size class and never freed before close(); the
+        peers keep their mappings of them (``_close_peer(keep=True)``).  Round 4's corruption
+        (profiles/r5/rootcause/) needed a scratch to be RELEASED mid-job — the owner's free AND
+        every peer's close (keeping either one alive removed it; the order of the two did not
+        matter): the first kernels of the IPC instance created right afterwards stored their
+        barrier flags into the owner's newly allocated memory."""
         chunk = -(-(nbytes // 16) // self.p)
         size = max(16, (self.p - 1) * chunk * 16)
+        if not FREE_SCRATCH:                   # (the diagnosis knob keeps round 4's exact sizes)
+            size = self._scratch_class(size)
         pooled = self._scratch_pool.get(size)
-        if pooled and not CLOSE_PEERS:
+        if pooled:
             return pooled.pop()
         ptr = c_void_p()
         try:
@@ -764,25 +788,43 @@ class IpcAllreduce(IpcForms):
         return ptr, h.raw
 
     def _free_scratch(self, scr) -> None:
-        """Free a push scratch (``CLOSE_PEERS``: its peers close their mappings at their own
-        deregistration; until then the driver keeps the memory alive for them), or park it in
-        the per-size pool (freed at close())."""
+        """Return a push scratch to the per-size-class pool (freed at close(), see
+        :meth:`_alloc_scratch`)."""
         if scr and scr[0]:
-            if CLOSE_PEERS:
+            if FREE_SCRATCH:                  # diagnosis knob: round 4's release
                 self._scratch_size.pop(scr[0].value, None)
                 native.soft_check(self.lib.mp4x_ipc_free(scr[0]), "ipc_free", LOG)
-            else:
-                self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
+                return
+            self._scratch_pool.setdefault(self._scratch_size[scr[0].value], []).append(scr)
 
     def _release_imports(self, reg: "_Reg") -> None:
         """The importer half of a release: this rank's uses of the peers' mappings
         (:meth:`_close_peer`) and its imported memAlloc views."""
+        scr_keys = set(reg.scr_keys)
         for hk in reg.peer_keys:
-            self._close_peer(hk)
+            self._close_peer(hk, keep=hk in scr_keys and not FREE_SCRATCH)   # pooled scratches stay mapped
         reg.peer_keys = []
         for i in reversed(range(reg.nown, len(reg.vmm))):
             reg.vmm[i].free(self._keep_va(own=False))
         del reg.vmm[reg.nown:]
+
+    def _flush_translations(self) -> None:
+        """After this rank closed IPC mappings of peer memory: map and unmap one small buffer in
+        this process's GPU address space, then drain the device.  Round 5 found (profiles/r5/
+        rootcause/) that right after an importer closes a mapping and the owner releases the
+        memory, the importer's GPU can still reach the old pages through the closed mapping's
+        address for a short while; an IPC mapping opened at that address in that window sent the
+        first kernels' stores into pages the owner had already reused.  One map / unmap (or
+        ~100 ms) closed the window in every run; it costs ~0.1 ms per release.
+        ``MP4X_IPC_FLUSH_ON_CLOSE=0`` skips it (diagnosis)."""
+        if os.environ.get("MP4X_IPC_FLUSH_ON_CLOSE", "1") != "1" or self.lib is None:
+            return
+        ptr = c_void_p()
+        if self.lib.mp4x_ipc_alloc(2 << 20, ctypes.byref(ptr)) == 0:
+            native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)
+        else:
+            native.clear_hip_error()
+        torch.cuda.synchronize(self.device)
 
     def _release_own(self, reg: "_Reg") -> None:
         """The owner half: this rank's push scratch, own memAlloc regions / chunks, tensor reference."""
@@ -829,6 +871,7 @@ class IpcAllreduce(IpcForms):
             return
         if reg is not None:
             self._release_imports(reg)
+            self._flush_translations()
         self.comm.server.call("barrier", self.rank)         # every importer closed its mappings
         if reg is not None:
             self._release_own(reg)
@@ -1308,6 +1351,7 @@ class IpcAllreduce(IpcForms):
         self._peer_bases = {}
         self._peer_refs = {}
         if collective and not UNORDERED_RELEASE:
+            self._flush_translations()
             self.comm.server.call("barrier", self.rank)     # every importer unmapped before the owners free
         # ---- owner half
         if self._data and not getattr(self, "_vmm_data", False):

@@ -105,6 +105,7 @@ class IpcForms:
             native.soft_check(self.lib.mp4x_ipc_close_handle(q), "ipc_close_handle", LOG)
         from . import ipc as _ipc            # (the knob lives there; tests patch it)
         if not _ipc.UNORDERED_RELEASE:
+            self._flush_translations()
             self.comm.server.call("barrier", self.rank)     # every importer unmapped before the owners free
         if ptr:
             native.soft_check(self.lib.mp4x_ipc_free(ptr), "ipc_free", LOG)

@@ -189,21 +189,19 @@ def _after_push_deregistration(comm):
             "stats": {k: v for k, v in dev.stats.items() if "ipc_large" in k or "fp8" in k}}
 
 
-@pytest.mark.parametrize("unordered", [False, True], ids=["ordered", "unordered_knob"])
-def test_instances_created_after_a_push_deregistration_are_exact(unordered):
+@pytest.mark.parametrize("probe", [True, False], ids=["default", "no_first_use_probe"])
+def test_instances_created_after_a_push_deregistration_are_exact(probe):
     """VERDICT r4 Next #1 / #2 'done looks like': 4 ranks, default CLOSE_PEERS=1, no probe scopes
-    around the calls under test.  ``unordered_knob``: round 4's release order restored
-    (MP4X_TEST_UNORDERED_RELEASE=1) — results must STILL be exact: either the order does not
-    matter on this box, or the first-use probes catch the broken instance and the job falls back
-    (recorded in ``probe_failures``) instead of returning garbage."""
-    env = {"MP4X_TEST_UNORDERED_RELEASE": "1"} if unordered else None
+    around the calls under test.  ``no_first_use_probe``: the large instance's first-use probe is
+    skipped (MP4X_TEST_SKIP_FIRST_USE_PROBE=1) — round 5 found that the probe's own traffic hid
+    round 4's corruption, so the fix (pooled push scratches, ipc._alloc_scratch) has to hold
+    without it.  (MP4X_TEST_FREE_SCRATCH=1 brings round 4's trigger back: tools/gpu/r4repro.sh.)"""
+    env = None if probe else {"MP4X_TEST_SKIP_FIRST_USE_PROBE": "1"}
     out = run_spawn(4, _after_push_deregistration, env=env, timeout=300)
-    print("probe_failures:", {r: o["probe_failures"] for r, o in out.items()})
     for r, o in out.items():
         assert all(v == 0 for v in o["bad"].values()), (r, o)
         assert o["canary"] == 0, (r, o)
         assert o["fp8_rel"] < 0.1, (r, o)
         assert "ipc2w" in o["autotune"], (r, o)
-        if not unordered:
-            assert o["large"] and o["fp8_big"] and not o["probe_failures"], (r, o)
-            assert o["stats"].get("broadcast.ipc_large", 0) >= 2, (r, o)
+        assert o["large"] and o["fp8_big"] and not o["probe_failures"], (r, o)
+        assert o["stats"].get("broadcast.ipc_large", 0) >= 2, (r, o)

@@ -211,13 +211,15 @@ class _FakeTensor:
 
 @pytest.mark.parametrize("close_peers", [True, False])
 def test_registration_lifecycle(monkeypatch, close_peers):
-    """CLOSE_PEERS (default): deregister() closes this rank's mappings of the peers' allocations
-    once no registration uses them and frees the push scratch, so nothing accumulates per
-    registration.  Without it (the round-3 policy): scratch pooled per size, mappings cached until
+    """CLOSE_PEERS (default): deregister() closes this rank's mappings of the peers' tensors once
+    no registration uses them; push scratches are pooled per size class (never freed before
+    close(), the peers' mappings of them kept: releasing them was round 4's corruption trigger),
+    so nothing accumulates per registration.  Without it (the round-3 policy): scratch pooled per size, mappings cached until
     close().  Either way a registration holds its tensor and close() releases everything."""
     p = 2
     lib = _CountingLib()
     monkeypatch.setattr(ipc_mod, "CLOSE_PEERS", close_peers)
+    monkeypatch.setenv("MP4X_IPC_FLUSH_ON_CLOSE", "0")      # (its map / unmap would count as allocs)
     monkeypatch.setattr(ipc_mod.native, "hip", lambda: lib)
     monkeypatch.setattr(ipc_mod.torch.cuda, "current_device", lambda: 0)
     monkeypatch.setattr(ipc_mod.torch.cuda, "synchronize", lambda *a, **k: None)
@@ -255,9 +257,11 @@ def test_registration_lifecycle(monkeypatch, close_peers):
         assert ok1 and ok2 and ok3 and keeps
         assert opened == 2                           # the peer's tensor segment + its push scratch
         if close_peers:
-            assert after_dereg == (0, 0)             # mappings closed, scratch freed
-            assert not inst._peer_refs and not inst._peer_bases
-            assert allocs >= 3                       # one scratch per registration (freed at each)
+            # the tensor mapping closed; the push scratches pooled (never freed before close), the
+            # peer's pooled scratch still mapped for the next registration it serves
+            assert after_dereg == (1, 1)
+            assert not inst._peer_refs and len(inst._peer_bases) == 1
+            assert allocs <= p                       # one scratch per rank, reused by every registration
         else:
             assert after_dereg == (2, 1)             # cached mappings, pooled scratch
             assert allocs <= p                       # the pooled scratch came back
