@@ -105,13 +105,13 @@ IPC_OPEN_MAX = int(os.environ.get("MP4X_IPC_OPEN_MAX", (1 << 31) - 1))
 #   "pool":           park the allocation in a per-size pool that the next memAlloc of that size
 #                     reuses (round 3's behaviour; MP4X_VMM_RELEASE=0 still selects it).
 CLOSE_PEERS = os.environ.get("MP4X_IPC_CLOSE_PEERS", "1") == "1"
-# Release ORDER of everything a peer maps (push scratches at deregistration, self-test buffers, the
-# staging buffers of an instance closed mid-job): every importer closes its mappings, a control-
-# plane barrier, and only then does each owner free its memory — the order mem_free always used.
-# Round 4 freed a push scratch while the peers still had it mapped, then made new fine-grained
-# exports: later instances' collectives read and wrote the wrong memory (profiles/r4/rooted/).
-# MP4X_TEST_UNORDERED_RELEASE=1 restores that order (owner frees first, no barrier) — for the
-# regression test that shows the first-use probes catch it; never for a job.
+# Release ORDER of everything a peer maps (registered tensors at deregistration, self-test buffers,
+# the staging buffers of an instance closed mid-job): every importer closes its mappings (and
+# flushes, _flush_translations), a control-plane barrier, and only then does each owner free its
+# memory — the order mem_free always used.  (Round 4's corruption turned out to need a RELEASE of a
+# peer-mapped push scratch, whatever the order: push scratches are pooled now, see _alloc_scratch
+# and profiles/r5/rootcause/.)  MP4X_TEST_UNORDERED_RELEASE=1 restores round 4's order (owner frees
+# first, no barrier) for the release-order tests; never for a job.
 UNORDERED_RELEASE = os.environ.get("MP4X_TEST_UNORDERED_RELEASE", "0") == "1"
 # MP4X_TEST_FREE_SCRATCH=1: round 4's push-scratch handling (freed at deregistration, the peers'
 # mappings of it closed) instead of the pool — the trigger of round 4's corruption; diagnosis only
