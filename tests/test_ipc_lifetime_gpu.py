@@ -60,6 +60,10 @@ def _register_cycles(comm):
     from mp4x import Operands, Operators
     r, p = comm.getRank(), comm.getSlaveNum()
     comm.device.ipc()
+    # a canary allocated before any cycle: the segments released by empty_cache() below were
+    # mapped by the peers, so a store through a stale translation would land somewhere like it
+    canary = (torch.arange(1 << 20, device="cuda", dtype=torch.int32) * 3 + r).float()
+    keep = canary.clone()
     samples, bad, regs = [], 0, 0
     for k in range(CYCLES):
         n = (8 << 20) // 4 + k * (256 << 10)
@@ -74,6 +78,8 @@ def _register_cycles(comm):
         torch.cuda.empty_cache()                        # the segment really goes back to the device
         comm.barrier()
         samples.append(_used())
+    torch.cuda.synchronize()
+    bad += int((canary != keep).sum())
     return bad, samples, regs, dict(comm.device.stats)
 
 
