@@ -13,9 +13,11 @@
 
 namespace {
 
+// mp4x_ipc_allreduce_ex2 (the slot arguments last; 0 / 0 = the single-buffer form)
 using AllreduceEx = int (*)(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs, int rank,
                             int p, int64_t nbytes, const void* src, void* out, uint32_t epoch, int blocks,
-                            const uint32_t* epoch_dev, float scale, void* stream);
+                            const uint32_t* epoch_dev, float scale, void* stream, int64_t slot_base,
+                            int64_t slot_vecs);
 
 AllreduceEx g_allreduce_ex = nullptr;
 
@@ -40,8 +42,8 @@ PyObject* bind(PyObject*, PyObject* addr) {
 // allreduce_ex(algo, dtype, op, data_pp, sig_pp, rank, p, nbytes, src, out, epoch, blocks,
 //              epoch_dev, scale, stream) -> rc     (pointers as int addresses or None)
 PyObject* allreduce_ex(PyObject*, PyObject* const* a, Py_ssize_t na) {
-  if (na != 15) {
-    PyErr_SetString(PyExc_TypeError, "allreduce_ex takes 15 arguments");
+  if (na != 15 && na != 17) {
+    PyErr_SetString(PyExc_TypeError, "allreduce_ex takes 15 arguments (+ slot_base, slot_vecs)");
     return nullptr;
   }
   if (!g_allreduce_ex) {
@@ -63,10 +65,13 @@ PyObject* allreduce_ex(PyObject*, PyObject* const* a, Py_ssize_t na) {
   const uint32_t* edev = static_cast<const uint32_t*>(as_ptr(a[12]));
   const float scale = (float)PyFloat_AsDouble(a[13]);
   void* stream = as_ptr(a[14]);
+  const int64_t slot_base = na == 17 ? PyLong_AsLongLong(a[15]) : 0;
+  const int64_t slot_vecs = na == 17 ? PyLong_AsLongLong(a[16]) : 0;
   if (PyErr_Occurred()) return nullptr;
   int rc;
   Py_BEGIN_ALLOW_THREADS
-  rc = g_allreduce_ex(algo, dtype, op, data, sig, rank, p, nbytes, src, out, epoch, blocks, edev, scale, stream);
+  rc = g_allreduce_ex(algo, dtype, op, data, sig, rank, p, nbytes, src, out, epoch, blocks, edev, scale, stream,
+                      slot_base, slot_vecs);
   Py_END_ALLOW_THREADS
   return PyLong_FromLong(rc);
 }
@@ -112,7 +117,7 @@ PyMethodDef kMethods[] = {
     {"bind_fast", bind_fast, METH_O, "bind_fast(address of mp4x_ipc_fast_allreduce in the loaded libmp4x_hip.so)"},
     {"fast_allreduce", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_allreduce)), METH_FASTCALL,
      "fast_allreduce(entry, stream) -> rc"},
-    {"bind", bind, METH_O, "bind(address of mp4x_ipc_allreduce_ex in the loaded libmp4x_hip.so)"},
+    {"bind", bind, METH_O, "bind(address of mp4x_ipc_allreduce_ex2 in the loaded libmp4x_hip.so)"},
     {"allreduce_ex", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(allreduce_ex)), METH_FASTCALL,
      "allreduce_ex(algo, dtype, op, data_pp, sig_pp, rank, p, nbytes, src, out, epoch, blocks, epoch_dev, scale, "
      "stream) -> rc"},

@@ -12,8 +12,7 @@
 namespace mp4x {
 
 __global__ void k_ipc_bump_epoch(uint32_t* epoch_dev) {
-  uint32_t e = (*epoch_dev + 1) & ~kTagMask;
-  *epoch_dev = e ? e : 1;
+  *epoch_dev = next_epoch(*epoch_dev);      // (wraps to 2: consecutive epochs alternate parity)
 }
 
 // ---------------------------------------------------------------- direct all-gather

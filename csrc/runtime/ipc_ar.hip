@@ -8,22 +8,32 @@ namespace mp4x {
 // src != nullptr: the kernel stages its own input (fused copy-in, one launch instead of a
 // memcpy + kernel): block b copies exactly the vectors block b of every peer will read, then
 // meets them at the start barrier (whose release fence publishes the copies).
+//
+// slot_vecs > 0 (the latency tier, staged and fused): the staging area is one of TWO slots at
+// vector offset slot_base + (epoch & 1) * slot_vecs, chosen by the epoch's parity (consecutive
+// epochs alternate parity, next_epoch), and the kernel has NO end barrier — one cross-rank round
+// trip per call instead of two.  Safe: this rank writes a slot again only two calls later, after
+// the start barrier of the call in between, which every peer reaches only once it has finished
+// reading this call's slot (one stream: kernels complete in order); the other kernel families
+// stage below slot_base; a peer one call ahead at the start barrier is accepted there.
 template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_oneshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
                                                               const uint32_t* epoch_dev,
-                                                              const u32x4* __restrict__ src, float scale, int op) {
+                                                              const u32x4* __restrict__ src, float scale, int op,
+                                                              int64_t slot_base, int64_t slot_vecs) {
   constexpr int p = NR;
   epoch = resolve_epoch(epoch, epoch_dev);
+  const int64_t so = slot_vecs > 0 ? slot_base + (int64_t)(epoch & 1u) * slot_vecs : 0;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
   if (src) {
-    u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+    u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank])) + so;
     for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride) mine[v] = src[v];
   }
   if (!block_barrier(P, 0, rank, p, epoch, self)) return;
   for (int64_t v = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x; v < nvec; v += stride)
-    out[v] = reduce_vec<DT, OP, NR>(P, v, scale, op);
-  block_barrier(P, 2, rank, p, epoch, self);
+    out[v] = reduce_vec<DT, OP, NR>(P, v + so, scale, op);
+  if (slot_vecs <= 0) block_barrier(P, 2, rank, p, epoch, self);
 }
 
 // two-shot: direct reduce-scatter into own buffer chunk `rank`, then direct all-gather.
@@ -92,10 +102,15 @@ using namespace mp4x;
 // pointers are the registered caller tensors and out == data_ptrs[rank]).  scale != 1: the
 // reduced value is multiplied by it before it is stored (fused average; float dtypes only).
 // op: any operator of the reference table valid for dtype (MP4X_E_UNSUPPORTED otherwise).
-extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
-                                     int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
-                                     int blocks, const uint32_t* epoch_dev, float scale, void* stream) {
+// slot_base / slot_vecs (16-byte vectors, one-shot only): the double-buffered latency slots (see
+// k_ipc_oneshot); 0 = the single-buffer form with its end barrier.  A slotted call needs src (the
+// fused copy-in: the staging target depends on the device-side epoch) and nbytes <= a slot.
+extern "C" int mp4x_ipc_allreduce_ex2(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                      int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
+                                      int blocks, const uint32_t* epoch_dev, float scale, void* stream,
+                                      int64_t slot_base, int64_t slot_vecs) {
   if ((nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
+  if (slot_vecs > 0 && (algo != 0 || !src || nbytes / 16 > slot_vecs || slot_base < 0)) return MP4X_E_BADARG;
   if (((uintptr_t)out & 15) || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
   if (scale != 1.0f && !float_dtype(dtype)) return MP4X_E_BADARG;
   IpcPtrs P;
@@ -121,7 +136,7 @@ extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* d
         constexpr int NR = decltype(nrc)::value;
         if (algo == 0)
           hipLaunchKernelGGL((k_ipc_oneshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,
-                             nvec, outv, epoch, epoch_dev, srcv, scale, op);
+                             nvec, outv, epoch, epoch_dev, srcv, scale, op, slot_base, slot_vecs);
         else
           hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,
                              nvec, outv, epoch, epoch_dev, srcv, scale, op);
@@ -146,6 +161,7 @@ struct FastAr {
   void* const* data_ptrs;    // every rank's staging buffer
   void* const* signal_ptrs;  // every rank's signal block
   int32_t rank, p;
+  int64_t slot_base, slot_vecs;   // the one-shot's double-buffered slots (0: none)
 };
 
 extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int op, void* buf, int64_t nbytes,
@@ -158,11 +174,18 @@ extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int
     return MP4X_E_CAPTURING;
   }
   if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
-  uint32_t e = (*s->epoch + 1u) & 0x3FFFFFFFu;
-  if (!e) e = 1u;
+  const uint32_t e = next_epoch(*s->epoch);
   *s->epoch = e;
-  return mp4x_ipc_allreduce_ex(algo, dtype, op, s->data_ptrs, s->signal_ptrs, s->rank, s->p, nbytes, buf, buf, e, blocks,
-                               nullptr, scale, stream);
+  const bool slotted = algo == 0 && s->slot_vecs > 0 && nbytes / 16 <= s->slot_vecs;
+  return mp4x_ipc_allreduce_ex2(algo, dtype, op, s->data_ptrs, s->signal_ptrs, s->rank, s->p, nbytes, buf, buf, e,
+                                blocks, nullptr, scale, stream, slotted ? s->slot_base : 0, slotted ? s->slot_vecs : 0);
+}
+
+extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                     int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
+                                     int blocks, const uint32_t* epoch_dev, float scale, void* stream) {
+  return mp4x_ipc_allreduce_ex2(algo, dtype, op, data_ptrs, signal_ptrs, rank, p, nbytes, src, out, epoch, blocks,
+                                epoch_dev, scale, stream, 0, 0);
 }
 
 // The pre-staged form (no fused copy-in, no scale).

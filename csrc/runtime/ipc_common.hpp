@@ -158,6 +158,19 @@ __device__ __forceinline__ Signal* sig_of(const IpcPtrs& P, int t) {
   return reinterpret_cast<Signal*>(s);
 }
 
+// The epoch after `e` (low 30 bits; 0 is never used and the sequence wraps to 2, so consecutive
+// epochs always alternate parity — the one-shot's double-buffered slots are chosen by it).  Host
+// (IpcAllreduce._next_epoch, mp4x_ipc_fast_allreduce) and k_ipc_bump_epoch follow the same rule.
+__host__ __device__ __forceinline__ uint32_t next_epoch(uint32_t e) {
+  const uint32_t n = ((e & ~kTagMask) + 1u) & ~kTagMask;
+  return n ? n : 2u;
+}
+
+// `which`: 0 start, 1 mid, 2 end.  At the START barrier a peer may already be ONE call ahead: the
+// double-buffered one-shot (k_ipc_oneshot with slots) has no end barrier, so a peer that finished
+// call e can store call e+1's start flag before this rank saw its flag of call e.  Every other
+// kernel ends with an end barrier, so a peer is never further ahead; a start flag holding the next
+// epoch (any protocol tag) therefore means "arrived, and done with call e".
 __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int rank, int p, uint32_t epoch,
                                               Signal* self) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its stores
@@ -181,7 +194,9 @@ __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int r
     // pays one uncached round trip, not two (r4 latency: +4 us per kernel when it was read first)
     uint64_t spin = 0;
     uint32_t seen;
-    while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch) {
+    const uint32_t ahead = which == 0 ? next_epoch(epoch) : 0xFFFFFFFFu;   // (low bits never all ones)
+    while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch &&
+           (seen & ~kTagMask) != ahead) {
       if (spin == 0) {
         spin = __hip_atomic_load(&self->spin_ticks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (spin == 0) spin = kDefaultSpinTicks;

@@ -227,7 +227,7 @@ def launch_ext():
                     try:
                         lib = hip()
                         mod = _load_ext("_mp4x_launch")
-                        mod.bind(ctypes.cast(lib.mp4x_ipc_allreduce_ex, ctypes.c_void_p).value)
+                        mod.bind(ctypes.cast(lib.mp4x_ipc_allreduce_ex2, ctypes.c_void_p).value)
                         fast = getattr(lib, "mp4x_ipc_fast_allreduce", None)
                         if fast is not None and hasattr(mod, "bind_fast"):
                             mod.bind_fast(ctypes.cast(fast, ctypes.c_void_p).value)

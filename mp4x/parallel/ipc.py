@@ -60,6 +60,8 @@ native.register_signatures({
                                    c_int, c_void_p, c_void_p]),
     "mp4x_ipc_allreduce_ex": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
                                       ctypes.c_uint32, c_int, c_void_p, ctypes.c_float, c_void_p]),
+    "mp4x_ipc_allreduce_ex2": (c_int, [c_int, c_int, c_int, PP, PP, c_int, c_int, c_int64, c_void_p, c_void_p,
+                                       ctypes.c_uint32, c_int, c_void_p, ctypes.c_float, c_void_p, c_int64, c_int64]),
     "mp4x_ipc_reduce_scatter_from": (c_int, [c_int, c_int, PP, PP, c_int, c_int, ctypes.POINTER(c_int64),
                                              ctypes.POINTER(c_int64), c_void_p, c_void_p, ctypes.c_uint32, c_int,
                                              c_void_p, c_void_p]),
@@ -128,6 +130,19 @@ SUPPORTED_DTYPES = {torch.float32, torch.float64, torch.bfloat16, torch.float16,
 _FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
 
 _FP8_NARROW = os.environ.get("MP4X_FP8_NARROW") == "1"    # the r1 4-byte-lane fp8 kernel (A/B)
+
+
+def next_epoch(e: int) -> int:
+    """The host epoch after ``e`` (low 30 bits, never 0, wrapping to 2 so consecutive epochs always
+    alternate parity): csrc/runtime/ipc_common.hpp ``next_epoch`` — the one-shot's double-buffered
+    slots are chosen by the parity."""
+    return ((e + 1) & 0x3FFFFFFF) or 2
+
+
+# The one-shot's two double-buffered slots (csrc/runtime/ipc_ar.hip k_ipc_oneshot), appended to
+# every instance's staging buffer: the latency tier then has ONE cross-rank barrier per call
+# (no end barrier).  MP4X_IPC_SLOTS=0 turns them off (A/B); their size follows the one-shot tier.
+SLOTS_ON = os.environ.get("MP4X_IPC_SLOTS", "1") == "1"
 
 
 def ipc_op_ok(dtype, op) -> bool:
@@ -239,6 +254,12 @@ class IpcAllreduce(IpcForms):
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
+        # the one-shot's two slots live above self.nbytes (nothing else stages there)
+        slot = max(256 << 10, int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))) if SLOTS_ON else 0
+        self._slot_bytes = (slot + 4095) // 4096 * 4096
+        self._slot_base = self.nbytes // 16          # in 16-byte vectors
+        self._slot_vecs = self._slot_bytes // 16
+        alloc_bytes = self.nbytes + 2 * self._slot_bytes
         # a staging buffer above the IPC open limit is built like a memAlloc tensor (VMM chunks,
         # dmabuf fds to the peers): rank-independent (the size is the same on every rank)
         self._vmm_data = self.nbytes > IPC_OPEN_MAX
@@ -251,14 +272,14 @@ class IpcAllreduce(IpcForms):
                 from . import vmm
                 g = ctypes.c_size_t()
                 check(self.lib.mp4x_vmm_granularity(ctypes.byref(g)), "vmm_granularity")
-                chunk, nch = vmm.chunk_plan(self.nbytes, g.value)
+                chunk, nch = vmm.chunk_plan(alloc_bytes, g.value)
                 own = vmm.VmmRegion.create(self.lib, chunk, nch)
                 self._data_regions.append(own)
                 self._data = c_void_p(own.va)
-                check(self.lib.mp4x_memset_async(own.va, 0, self.nbytes, None), "vmm data zero")
+                check(self.lib.mp4x_memset_async(own.va, 0, alloc_bytes, None), "vmm data zero")
                 torch.cuda.synchronize()
             else:
-                check(self.lib.mp4x_ipc_alloc_data(self.nbytes, int(DATA_COARSE), ctypes.byref(self._data)),
+                check(self.lib.mp4x_ipc_alloc_data(alloc_bytes, int(DATA_COARSE), ctypes.byref(self._data)),
                       "ipc_alloc(data)")
             check(self.lib.mp4x_ipc_alloc(self.lib.mp4x_ipc_signal_bytes(), ctypes.byref(self._sig)),
                   "ipc_alloc(sig)")
@@ -392,7 +413,8 @@ class IpcAllreduce(IpcForms):
         if st is None or st[1] != words:
             class _FastAr(ctypes.Structure):
                 _fields_ = [("herr", c_void_p * 8), ("epoch", c_void_p), ("data_ptrs", c_void_p),
-                            ("signal_ptrs", c_void_p), ("rank", ctypes.c_int32), ("p", ctypes.c_int32)]
+                            ("signal_ptrs", c_void_p), ("rank", ctypes.c_int32), ("p", ctypes.c_int32),
+                            ("slot_base", ctypes.c_int64), ("slot_vecs", ctypes.c_int64)]
             s = _FastAr()
             for i, w in enumerate(words):
                 s.herr[i] = w
@@ -400,6 +422,7 @@ class IpcAllreduce(IpcForms):
             s.data_ptrs = self._pp_data_addr
             s.signal_ptrs = self._pp_sig_addr
             s.rank, s.p = self.rank, self.p
+            s.slot_base, s.slot_vecs = self._slot_base, self._slot_vecs
             st = self._fast_state = (s, words)
         return ctypes.addressof(st[0])
 
@@ -566,14 +589,17 @@ class IpcAllreduce(IpcForms):
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+                self.epoch = next_epoch(self.epoch)
+            # the latency tier: one-shot, one piece, fused copy-in -> the double-buffered slots
+            slotted = algo == ONESHOT and fused and m == total and m <= self._slot_bytes
+            sb, sv = (self._slot_base, self._slot_vecs) if slotted else (0, 0)
             if lx is not None:
                 rc = lx.allreduce_ex(algo, dt, code, self._pp_data_addr, self._pp_sig_addr, self.rank, self.p, m,
-                                     sp + off if fused else None, dp + off, self.epoch, blocks, edev, scale, st)
+                                     sp + off if fused else None, dp + off, self.epoch, blocks, edev, scale, st, sb, sv)
             else:
-                rc = self.lib.mp4x_ipc_allreduce_ex(algo, dt, code, self._pp_data[0], self._pp_sig[0], self.rank,
-                                                    self.p, m, sp + off if fused else None, dp + off, self.epoch,
-                                                    blocks, edev, scale, st)
+                rc = self.lib.mp4x_ipc_allreduce_ex2(algo, dt, code, self._pp_data[0], self._pp_sig[0], self.rank,
+                                                     self.p, m, sp + off if fused else None, dp + off, self.epoch,
+                                                     blocks, edev, scale, st, sb, sv)
             check(rc, "mp4x_ipc_allreduce")
             off += m
         return out
@@ -611,7 +637,7 @@ class IpcAllreduce(IpcForms):
             if edev is not None:
                 check(self.lib.mp4x_ipc_bump_epoch(edev, ms), "ipc_bump_epoch")
             else:
-                self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+                self.epoch = next_epoch(self.epoch)
             pp = self._pp_hi[0] if slot else self._pp_data[0]
             check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
                                                  None, dst.data_ptr() + off, self.epoch, blocks, edev, scale, ms),
@@ -1159,7 +1185,7 @@ class IpcAllreduce(IpcForms):
         if edev is not None:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
-            self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+            self.epoch = next_epoch(self.epoch)
         chunk = -(-(total // 16) // self.p)
         blocks = max(1, min(self.grid_cap("push", dtype, op), -(-chunk // 512))) if self.shared_gpu else 0
         pp = ptr_array(peers)
@@ -1191,7 +1217,7 @@ class IpcAllreduce(IpcForms):
         if edev is not None:
             check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
         else:
-            self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+            self.epoch = next_epoch(self.epoch)
         blocks = self._grid(total // 16, "twoshot", dtype, op)   # >= 8: every XCD passes the barriers
         if grid > 0:
             blocks = min(grid, self.grid_cap("twoshot", dtype, op))

@@ -313,7 +313,7 @@ class IpcForms:
             return self._epoch_dev.data_ptr()
         if torch.cuda.is_current_stream_capturing():
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
-        self.epoch = (self.epoch + 1) & 0x3FFFFFFF or 1
+        self.epoch = ((self.epoch + 1) & 0x3FFFFFFF) or 2   # (ipc.next_epoch)
         return None
 
     def _grid(self, nvec: int, family: str = "plan", dtype=None, op=None) -> int:

@@ -3,8 +3,10 @@
 p processes share GPU 0 and run the SAME seeded random sequence of calls: sizes from 16 B to
 3 MiB through a 1 MiB buffer (so some calls are piecewise, pipelined or serial), one-shot /
 two-shot, SUM / MAX, f32 / bf16 / f64 / i32, in place and out of place, back to back with no
-host synchronisation in between.  Every result is checked exactly (integers, small-integer
-floats) against a local recomputation; the barrier error word must stay 0.
+host synchronisation in between, each rank pausing at random points of its own (so ranks run
+ahead of each other, the case the one-shot's double-buffered slots and its start-barrier rule
+exist for).  Every result is checked exactly (integers, small-integer floats) against a local
+recomputation; the barrier error word must stay 0.
 """
 import multiprocessing as mp
 import tempfile
@@ -31,9 +33,16 @@ def _worker(port, q, seed):
         r, p = comm.getRank(), comm.getSlaveNum()
         ipc = IpcAllreduce(comm, nbytes=1 << 20)
         rng = random.Random(seed)
+        jitter = random.Random(seed * 31 + r)     # rank-dependent: ranks drift apart in time
         pending = []
         bad = []
         for it in range(ITERS):
+            if jitter.random() < 0.15:
+                # a late rank: the others run ahead — after a double-buffered one-shot (no end
+                # barrier) a peer may store the NEXT call's start flag before this rank saw the
+                # current one (csrc/runtime/ipc_common.hpp block_barrier)
+                import time
+                time.sleep(jitter.choice([0.0005, 0.002, 0.005]))
             dt = rng.choice([torch.float32, torch.bfloat16, torch.float64, torch.int32])
             es = torch.empty(0, dtype=dt).element_size()
             nbytes = rng.choice([16, 256, 4096, 65536, 300_000 // 16 * 16, (1 << 20) + 4096, 3 << 20])

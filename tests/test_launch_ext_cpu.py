@@ -1,6 +1,7 @@
 """The ctypes-free launcher (csrc/pyext/launch_ext.cpp) passes every argument of
-mp4x_ipc_allreduce_ex through unchanged: bound here to a ctypes callback with the same C
-signature (CPU, no HIP) that records what it receives."""
+mp4x_ipc_allreduce_ex2 through unchanged (the 15-argument form with slots 0 / 0, or the
+17-argument form with the one-shot's double-buffered slots): bound here to a ctypes callback with
+the same C signature (CPU, no HIP) that records what it receives."""
 import ctypes
 
 import pytest
@@ -9,7 +10,8 @@ from mp4x.ops import native
 
 PROTO = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
-                         ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p)
+                         ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p, ctypes.c_float, ctypes.c_void_p,
+                         ctypes.c_int64, ctypes.c_int64)
 
 
 def test_allreduce_ex_marshals_every_argument():
@@ -41,6 +43,8 @@ def _check(mod, seen):
     (a,) = seen
     assert a[:3] == (1, 2, 3) and a[3] == 0x1000 and a[4] == 0x2000 and a[5:8] == (5, 8, (5 << 32) + 16)
     assert a[8] is None and a[9] == 0x3000 and a[10] == 0xFFFFFFF0 and a[11] == 48 and a[12] is None
-    assert a[13] == pytest.approx(0.125) and a[14] == 0x4000
+    assert a[13] == pytest.approx(0.125) and a[14] == 0x4000 and a[15:] == (0, 0)
+    mod.allreduce_ex(0, 2, 0, 0x1000, 0x2000, 1, 2, 4096, 0x5000, 0x5000, 3, 0, None, 1.0, 0x4000, 1 << 22, 1 << 15)
+    assert seen[1][15:] == (1 << 22, 1 << 15)
     with pytest.raises(TypeError):
         mod.allreduce_ex(1, 2, 3)
