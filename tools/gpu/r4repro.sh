@@ -1,6 +1,10 @@
 #!/bin/bash
-# Round 4's rooted-probe failure, bisected on the round-4 tree (a git worktree of 586a5dd at
-# r4tree/, native libraries built there): the same 4-rank bench flow once per variant, each
+# Round 4's rooted-probe failure, bisected on the round-4 tree: the same 4-rank bench flow once
+# per variant.  Set the tree up first (on the CPU host; it travels with the snapshot, so take
+# ./r4tree out of .gpurunignore for these calls):
+#   git worktree add r4tree 586a5dd && (cd r4tree && git apply ../profiles/r5/rootcause/r4tree_bisect_knobs.patch
+#     && python tools/build_native.py)      # + the acquire-wait build as libmp4x_hip_debug.so, see the patch
+# Each
 # variant = one round-5 change switched on by an environment variable of the patched worktree
 # (R5_ORDERED, R5_LAZY_MEMALLOC, R5_PROBE_LARGE; MP4X_NATIVE_DEBUG=1 loads the build with the
 # block_barrier acquire wait).  Lines "ruled out" per variant -> ruled_out_<variant>.txt.
