@@ -330,3 +330,56 @@ def test_fast_path_memo_only_from_the_public_api(monkeypatch):
     assert inspect.signature(DeviceEngine.allreduce.__wrapped__).parameters["memo"].default is False
     src = inspect.getsource(process_comm.ProcessCommSlave.allreduceArray)
     assert "memo=" in src and "self._fast_lx(ent, self._fast_stream())" in src
+
+
+def test_epochs_alternate_parity_across_the_wrap():
+    """The one-shot's double-buffered slots are chosen by the epoch's parity: consecutive epochs
+    must always alternate parity, also where the 30-bit counter wraps (to 2, never 0 or 1 twice)."""
+    from mp4x.parallel.ipc import next_epoch
+    e = 0
+    seq = []
+    for _ in range(6):
+        e = next_epoch(e)
+        seq.append(e)
+    assert seq == [1, 2, 3, 4, 5, 6]
+    e = 0x3FFFFFFD
+    seq = []
+    for _ in range(5):
+        e = next_epoch(e)
+        seq.append(e)
+    assert seq == [0x3FFFFFFE, 0x3FFFFFFF, 2, 3, 4]
+    assert all((a ^ b) & 1 for a, b in zip(seq, seq[1:]))
+
+
+def test_oneshot_takes_the_slots_only_when_fused_and_small(monkeypatch):
+    """The staged allreduce passes the slot region (above the staging buffer) to the launcher for
+    a one-piece, fused one-shot that fits a slot, and the single-buffer form (0, 0) otherwise
+    (two-shot, a message larger than a slot, the unfused copy-in)."""
+    calls = []
+
+    class _Lx:
+        def allreduce_ex(self, *a):
+            calls.append(a)
+            return 0
+    monkeypatch.setattr(ipc_mod.native, "launch_ext", lambda: _Lx())
+    monkeypatch.setattr(ipc_mod, "stream_ptr", lambda *a: 0)
+    inst = object.__new__(ipc_mod.IpcAllreduce)
+    inst.raise_if_failed = lambda: None
+    inst.nbytes, inst._slot_bytes = 1 << 20, 256 << 10
+    inst._slot_base, inst._slot_vecs = (1 << 20) // 16, (256 << 10) // 16
+    inst.shared_gpu, inst._epoch_dev, inst._overlap_default = False, None, False
+    inst.rank, inst.p, inst._pp_data_addr, inst._pp_sig_addr = 0, 2, 0x1000, 0x2000
+    inst.lib = None
+    cases = ((1024, ipc_mod.ONESHOT, True, True), (65536, ipc_mod.ONESHOT, True, True),
+             (65540, ipc_mod.ONESHOT, True, False), (1024, ipc_mod.TWOSHOT, True, False),
+             (1024, ipc_mod.ONESHOT, False, False))
+    for n, algo, fuse, want in cases:
+        inst._fuse_copy = fuse
+        if not fuse:
+            inst._data = type("V", (), {"value": 0})()
+            inst.lib = type("L", (), {"mp4x_memcpy_async": staticmethod(lambda *a: 0)})()
+        calls.clear()
+        t = torch.zeros(n)
+        inst.allreduce(t, Operators.Float.SUM, algo=algo, capturing=False)
+        (a,) = calls
+        assert a[15:] == ((inst._slot_base, inst._slot_vecs) if want else (0, 0)), (n, algo, fuse, a[15:])
