@@ -41,14 +41,19 @@ template <int DT, int OP, int NR>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* self, int rank, int64_t nvec,
                                                               u32x4* __restrict__ out, uint32_t epoch,
                                                               const uint32_t* epoch_dev,
-                                                              const u32x4* __restrict__ src, float scale, int op) {
+                                                              const u32x4* __restrict__ src, float scale, int op,
+                                                              int64_t slot_base, int64_t slot_vecs) {
   constexpr int p = NR;
   MP4X_DASSERT(rank >= 0 && rank < NR && blockIdx.x < kIpcMaxBlocks);
   epoch = resolve_epoch(epoch, epoch_dev);
+  // slotted (staged, fused copy-in, one piece): the same double-buffered slots as the one-shot,
+  // so the end barrier goes — the all-gather's reads of a slot finish before the reader's next
+  // call starts, and this rank writes that slot again only two calls later (k_ipc_oneshot)
+  const int64_t so = slot_vecs > 0 ? slot_base + (int64_t)(epoch & 1u) * slot_vecs : 0;
   const int64_t chunk = (nvec + p - 1) / p;
   const int64_t stride = (int64_t)gridDim.x * kIpcThreads;
   const int64_t off0 = (int64_t)blockIdx.x * kIpcThreads + threadIdx.x;
-  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank]));
+  u32x4* mine = reinterpret_cast<u32x4*>(const_cast<void*>(P.data[rank])) + so;
   if (src) {   // fused copy-in: block b stages the chunk offsets block b of every peer reads
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
@@ -64,7 +69,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
     // zero-copy form: `out` IS this rank's registered buffer (== mine), one store per vector
     const bool zc = out == mine;
     for (int64_t v = b + off0; v < e; v += stride) {
-      u32x4 o = reduce_vec<DT, OP, NR>(P, v, scale, op);
+      u32x4 o = reduce_vec<DT, OP, NR>(P, v + so, scale, op);
       mine[v] = o;
       if (!zc) out[v] = o;
     }
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
       const int64_t idx = (int64_t)k * chunk + v;
-      if (k != rank && idx < nvec) x[k] = reinterpret_cast<const u32x4*>(P.data[k])[idx];
+      if (k != rank && idx < nvec) x[k] = reinterpret_cast<const u32x4*>(P.data[k])[so + idx];
     }
 #pragma unroll
     for (int k = 0; k < NR; ++k) {
@@ -86,7 +91,7 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_twoshot(IpcPtrs P, Signal* 
       if (k != rank && idx < nvec) out[idx] = x[k];
     }
   }
-  block_barrier(P, 2, rank, p, epoch, self);
+  if (slot_vecs <= 0) block_barrier(P, 2, rank, p, epoch, self);
 }
 
 }  // namespace mp4x
@@ -102,7 +107,7 @@ using namespace mp4x;
 // pointers are the registered caller tensors and out == data_ptrs[rank]).  scale != 1: the
 // reduced value is multiplied by it before it is stored (fused average; float dtypes only).
 // op: any operator of the reference table valid for dtype (MP4X_E_UNSUPPORTED otherwise).
-// slot_base / slot_vecs (16-byte vectors, one-shot only): the double-buffered latency slots (see
+// slot_base / slot_vecs (16-byte vectors; one- and two-shot): the double-buffered slots (see
 // k_ipc_oneshot); 0 = the single-buffer form with its end barrier.  A slotted call needs src (the
 // fused copy-in: the staging target depends on the device-side epoch) and nbytes <= a slot.
 extern "C" int mp4x_ipc_allreduce_ex2(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
@@ -110,7 +115,8 @@ extern "C" int mp4x_ipc_allreduce_ex2(int algo, int dtype, int op, void* const* 
                                       int blocks, const uint32_t* epoch_dev, float scale, void* stream,
                                       int64_t slot_base, int64_t slot_vecs) {
   if ((nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
-  if (slot_vecs > 0 && (algo != 0 || !src || nbytes / 16 > slot_vecs || slot_base < 0)) return MP4X_E_BADARG;
+  if (slot_vecs > 0 && (algo < 0 || algo > 1 || !src || nbytes / 16 > slot_vecs || slot_base < 0))
+    return MP4X_E_BADARG;
   if (((uintptr_t)out & 15) || ((uintptr_t)src & 15)) return MP4X_E_BADARG;
   if (scale != 1.0f && !float_dtype(dtype)) return MP4X_E_BADARG;
   IpcPtrs P;
@@ -139,7 +145,7 @@ extern "C" int mp4x_ipc_allreduce_ex2(int algo, int dtype, int op, void* const* 
                              nvec, outv, epoch, epoch_dev, srcv, scale, op, slot_base, slot_vecs);
         else
           hipLaunchKernelGGL((k_ipc_twoshot<DT, OP, NR>), dim3(blocks), dim3(kIpcThreads), 0, st, P, self, rank,
-                             nvec, outv, epoch, epoch_dev, srcv, scale, op);
+                             nvec, outv, epoch, epoch_dev, srcv, scale, op, slot_base, slot_vecs);
         return (int)hipGetLastError();
       });
     });
@@ -161,7 +167,7 @@ struct FastAr {
   void* const* data_ptrs;    // every rank's staging buffer
   void* const* signal_ptrs;  // every rank's signal block
   int32_t rank, p;
-  int64_t slot_base, slot_vecs;   // the one-shot's double-buffered slots (0: none)
+  int64_t slot_base, slot_vecs;   // the double-buffered slots of the one- / two-shot (0: none)
 };
 
 extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int op, void* buf, int64_t nbytes,
@@ -176,7 +182,7 @@ extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int
   if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
   const uint32_t e = next_epoch(*s->epoch);
   *s->epoch = e;
-  const bool slotted = algo == 0 && s->slot_vecs > 0 && nbytes / 16 <= s->slot_vecs;
+  const bool slotted = (algo == 0 || algo == 1) && s->slot_vecs > 0 && nbytes / 16 <= s->slot_vecs;
   return mp4x_ipc_allreduce_ex2(algo, dtype, op, s->data_ptrs, s->signal_ptrs, s->rank, s->p, nbytes, buf, buf, e,
                                 blocks, nullptr, scale, stream, slotted ? s->slot_base : 0, slotted ? s->slot_vecs : 0);
 }

@@ -139,10 +139,13 @@ def next_epoch(e: int) -> int:
     return ((e + 1) & 0x3FFFFFFF) or 2
 
 
-# The one-shot's two double-buffered slots (csrc/runtime/ipc_ar.hip k_ipc_oneshot), appended to
-# every instance's staging buffer: the latency tier then has ONE cross-rank barrier per call
-# (no end barrier).  MP4X_IPC_SLOTS=0 turns them off (A/B); their size follows the one-shot tier.
+# Two double-buffered slots (csrc/runtime/ipc_ar.hip k_ipc_oneshot / k_ipc_twoshot), appended to
+# every instance's staging buffer: a staged, fused, one-piece one-shot then has ONE cross-rank
+# barrier per call and a two-shot two (no end barrier).  MP4X_IPC_SLOTS=0 turns them off (A/B);
+# MP4X_IPC_SLOT_BYTES sizes them (4 MiB: the staged two-shot's range below the zero-copy sizes,
+# where a barrier round trip is a visible share of the call; at least the one-shot tier).
 SLOTS_ON = os.environ.get("MP4X_IPC_SLOTS", "1") == "1"
+SLOT_BYTES = int(os.environ.get("MP4X_IPC_SLOT_BYTES", 4 << 20))
 
 
 def ipc_op_ok(dtype, op) -> bool:
@@ -254,8 +257,8 @@ class IpcAllreduce(IpcForms):
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
-        # the one-shot's two slots live above self.nbytes (nothing else stages there)
-        slot = max(256 << 10, int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))) if SLOTS_ON else 0
+        # the two slots live above self.nbytes (nothing else stages there)
+        slot = max(SLOT_BYTES, int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))) if SLOTS_ON else 0
         self._slot_bytes = (slot + 4095) // 4096 * 4096
         self._slot_base = self.nbytes // 16          # in 16-byte vectors
         self._slot_vecs = self._slot_bytes // 16
@@ -590,8 +593,8 @@ class IpcAllreduce(IpcForms):
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = next_epoch(self.epoch)
-            # the latency tier: one-shot, one piece, fused copy-in -> the double-buffered slots
-            slotted = algo == ONESHOT and fused and m == total and m <= self._slot_bytes
+            # one piece, fused copy-in, fits a slot -> the double-buffered slots (no end barrier)
+            slotted = fused and m == total and m <= self._slot_bytes
             sb, sv = (self._slot_base, self._slot_vecs) if slotted else (0, 0)
             if lx is not None:
                 rc = lx.allreduce_ex(algo, dt, code, self._pp_data_addr, self._pp_sig_addr, self.rank, self.p, m,

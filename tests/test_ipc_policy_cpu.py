@@ -351,10 +351,10 @@ def test_epochs_alternate_parity_across_the_wrap():
     assert all((a ^ b) & 1 for a, b in zip(seq, seq[1:]))
 
 
-def test_oneshot_takes_the_slots_only_when_fused_and_small(monkeypatch):
+def test_staged_calls_take_the_slots_only_when_fused_one_piece_and_small(monkeypatch):
     """The staged allreduce passes the slot region (above the staging buffer) to the launcher for
-    a one-piece, fused one-shot that fits a slot, and the single-buffer form (0, 0) otherwise
-    (two-shot, a message larger than a slot, the unfused copy-in)."""
+    a one-piece, fused one- or two-shot that fits a slot, and the single-buffer form (0, 0)
+    otherwise (a message larger than a slot, the unfused copy-in)."""
     calls = []
 
     class _Lx:
@@ -371,7 +371,8 @@ def test_oneshot_takes_the_slots_only_when_fused_and_small(monkeypatch):
     inst.rank, inst.p, inst._pp_data_addr, inst._pp_sig_addr = 0, 2, 0x1000, 0x2000
     inst.lib = None
     cases = ((1024, ipc_mod.ONESHOT, True, True), (65536, ipc_mod.ONESHOT, True, True),
-             (65540, ipc_mod.ONESHOT, True, False), (1024, ipc_mod.TWOSHOT, True, False),
+             (65540, ipc_mod.ONESHOT, True, False), (1024, ipc_mod.TWOSHOT, True, True),
+             (65540, ipc_mod.TWOSHOT, True, False),
              (1024, ipc_mod.ONESHOT, False, False))
     for n, algo, fuse, want in cases:
         inst._fuse_copy = fuse
