@@ -83,12 +83,13 @@ PyObject* bind_fast(PyObject*, PyObject* addr) {
   Py_RETURN_NONE;
 }
 
-// fast_allreduce(entry, stream) -> rc.  `entry` is the engine's memoised launch tuple
-// (state address, algo, dtype, op, buffer address, nbytes, blocks, scale); rc 1003 / 1004 = not
-// launched (an earlier collective failed / the stream is capturing): the caller takes the full path.
+// fast_allreduce(entry, stream[, base]) -> rc.  `entry` is the engine's memoised launch tuple
+// (state address, algo, dtype, op, buffer address — or its offset from `base` when base is given —,
+// nbytes, blocks, scale); rc 1003 / 1004 / MP4X_E_BADARG = not launched (an earlier collective
+// failed / the stream is capturing / an unaligned buffer): the caller takes the full path.
 PyObject* fast_allreduce(PyObject*, PyObject* const* a, Py_ssize_t na) {
-  if (na != 2 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) < 8) {
-    PyErr_SetString(PyExc_TypeError, "fast_allreduce(entry: tuple of 8, stream)");
+  if ((na != 2 && na != 3) || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) < 8) {
+    PyErr_SetString(PyExc_TypeError, "fast_allreduce(entry: tuple of 8, stream[, base])");
     return nullptr;
   }
   if (!g_fast) {
@@ -100,7 +101,8 @@ PyObject* fast_allreduce(PyObject*, PyObject* const* a, Py_ssize_t na) {
   const int algo = (int)PyLong_AsLong(t[1]);
   const int dtype = (int)PyLong_AsLong(t[2]);
   const int op = (int)PyLong_AsLong(t[3]);
-  void* buf = PyLong_AsVoidPtr(t[4]);
+  char* buf = static_cast<char*>(PyLong_AsVoidPtr(t[4]));
+  if (na == 3) buf = static_cast<char*>(PyLong_AsVoidPtr(a[2])) + PyLong_AsLongLong(t[4]);
   const int64_t nbytes = PyLong_AsLongLong(t[5]);
   const int blocks = (int)PyLong_AsLong(t[6]);
   const float scale = (float)PyFloat_AsDouble(t[7]);

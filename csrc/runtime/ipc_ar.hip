@@ -180,6 +180,9 @@ extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int
     return MP4X_E_CAPTURING;
   }
   if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  // everything mp4x_ipc_allreduce_ex2 could refuse is refused HERE, before the epoch moves (a
+  // refused call must leave this rank's epoch where its peers expect it): the full path runs it
+  if (((uintptr_t)buf & 15) || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
   const uint32_t e = next_epoch(*s->epoch);
   *s->epoch = e;
   const bool slotted = (algo == 0 || algo == 1) && s->slot_vecs > 0 && nbytes / 16 <= s->slot_vecs;

@@ -127,6 +127,17 @@ def local_reduce(out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: i
     return out
 
 
+
+class _FastMemo(dict):
+    """The allreduceArray latency fast path's memo (call shape -> native launch entry).
+    ``by_ptr``: keys carry the tensor's address (some tensor is registered) or 0 (none is: the
+    staged launch of a shape does not depend on where the tensor lives)."""
+    __slots__ = ("by_ptr",)
+
+    def __init__(self):
+        super().__init__()
+        self.by_ptr = False
+
 class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
     # (class defaults: engines assembled without __init__ in unit tests see one node, no hier)
     layout = NodeLayout([])
@@ -194,7 +205,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         self.probe_failures: List[dict] = []   # first-use probe failures of lazily made instances
         self._rccl_variants: Dict[int, object] = {}   # min CTAs -> TorchColl on a dedicated communicator
         # (dtype, op code, log2 size class) -> algorithm measured fastest by autotune_allreduce
-        self._fast_ar: Dict[tuple, tuple] = {}        # latency fast path: call shape -> native launch
+        self._fast_ar = _FastMemo()                   # latency fast path: call shape -> native launch
         self._tuned: Dict[tuple, str] = _TunedTable()
         self._tuned.on_change = self._invalidate_fast
         self._sel_memo: Dict[tuple, tuple] = {}       # select() decisions of repeated call shapes
@@ -405,10 +416,16 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
     # ------------------------------------------------------------------ latency fast path
     def _invalidate_fast(self) -> None:
         """Forget every memoised latency-tier launch (any input of the decision changed: the pinned
-        table, a tier attribute, a registration, an instance, the epoch mode)."""
+        table, a tier attribute, a registration, an instance, the epoch mode).  While any tensor is
+        registered the memo keys on the buffer address too (an address inside a registered range
+        takes the zero-copy kernels instead); with none, one entry serves every buffer of a shape."""
         fa = self.__dict__.get("_fast_ar")
-        if fa:
-            fa.clear()
+        if fa is None:
+            return
+        fa.clear()
+        if isinstance(fa, _FastMemo):
+            inst = self.__dict__.get("_ipc_obj")
+            fa.by_ptr = bool(getattr(inst, "_regs", None))
 
     _FAST_MAX = 256
 
@@ -440,11 +457,14 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             return
         a = ONESHOT if algo == "ipc1" else TWOSHOT
         from ..operators import dtype_of_torch
-        key = (arr.data_ptr(), arr.numel(), frm, to, arr.dtype, operator, getattr(operand, "codec", None),
-               getattr(operand, "compress", False), scale)
+        base = arr.data_ptr()
+        key = (base if getattr(fa, "by_ptr", True) else 0, arr.get_device(), arr.numel(), frm, to, arr.dtype,
+               operator, getattr(operand, "codec", None), getattr(operand, "compress", False), scale)
         if len(fa) >= self._FAST_MAX:
             fa.clear()
-        fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr, total,
+        # the buffer as an offset from the tensor's address: the call passes its tensor's address
+        # (an unaligned one is refused natively before anything is launched: the full path runs)
+        fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr - base, total,
                    inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
                    "allreduce." + algo, inst)
 

@@ -582,6 +582,14 @@ class IpcAllreduce(IpcForms):
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
         sp, dp = view.data_ptr(), out.data_ptr()
+        # one piece that fits a slot -> the double-buffered slots (no end barrier).  The decision
+        # must be the same on every rank, so it never depends on this rank's input alignment: a
+        # slotted call needs the fused copy-in, and an unaligned input is first copied to an
+        # aligned temporary (rank-local, the protocol is unchanged)
+        slotted = self._fuse_copy and total <= piece and total <= self._slot_bytes
+        if slotted and sp % 16:
+            view = view.clone()
+            sp = view.data_ptr()
         fused = sp % 16 == 0 and self._fuse_copy   # copy-in inside the kernel: one launch
         lx = native.launch_ext()
         code = int(op.code)
@@ -593,8 +601,6 @@ class IpcAllreduce(IpcForms):
                 check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
             else:
                 self.epoch = next_epoch(self.epoch)
-            # one piece, fused copy-in, fits a slot -> the double-buffered slots (no end barrier)
-            slotted = fused and m == total and m <= self._slot_bytes
             sb, sv = (self._slot_base, self._slot_vecs) if slotted else (0, 0)
             if lx is not None:
                 rc = lx.allreduce_ex(algo, dt, code, self._pp_data_addr, self._pp_sig_addr, self.rank, self.p, m,

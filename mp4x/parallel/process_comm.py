@@ -293,7 +293,7 @@ class ProcessCommSlave:
                 or getattr(eng.device, "type", None) != "cuda":
             return
         lx = native.launch_ext()
-        if lx is None or not hasattr(lx, "fast_allreduce") or eng._fast_ar is None:
+        if lx is None or not hasattr(lx, "fast_allreduce") or getattr(eng._fast_ar, "by_ptr", None) is None:
             return
         import torch
         self._fast_lx = lx.fast_allreduce
@@ -816,13 +816,14 @@ class ProcessCommSlave:
         """
         fast = self._fast_ar
         if fast and out is None and type(arrData) is self._fast_tensor and arrData.is_cuda and arrData.is_contiguous():
-            ent = fast.get((arrData.data_ptr(), arrData.numel(), frm, to, arrData.dtype, operator, operand.codec,
-                            operand.compress, scale))
-            if ent is not None and self._fast_lx(ent, self._fast_stream()) == 0:
+            base = arrData.data_ptr()
+            ent = fast.get((base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
+                            arrData.dtype, operator, operand.codec, operand.compress, scale))
+            if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
                 self._fast_after(ent)
                 return arrData
             # not memoised, or not launched (rc 1003: an earlier collective failed; 1004: the stream
-            # is being captured): the full path decides, raises or records
+            # is being captured; an unaligned buffer): the full path decides, raises or records
         self._tick("allreduceArray")
         if scale != 1.0:
             if _is_device_tensor(arrData) and self.slaveNum > 1:

@@ -47,6 +47,45 @@ def _fast_fn(comm):
         out[tag]["scale_bad"] = int((x != _exp(n, p, 3) / p).sum())
     calls = comm.stats["calls"].get("allreduceArray", 0)
     eng_calls = sum(v for k, v in eng.stats.items() if k in ("allreduce.ipc1", "allreduce.ipc2"))
+    # one memo entry serves every tensor of the shape (nothing registered): fresh buffers at other
+    # addresses launch natively; an unaligned one is refused natively before its epoch moves and
+    # the full path runs it (exact)
+    launched = []
+    orig = comm._fast_lx
+
+    def spy(*a):
+        rc = orig(*a)
+        launched.append(rc)
+        return rc
+    comm._fast_lx = spy
+    n = 1024
+    pool = [torch.empty(n, device="cuda") for _ in range(3)]
+    big = torch.empty(n + 1, device="cuda")
+    fresh_bad = 0
+    for k in range(12):
+        x = big[1:] if k % 4 == 3 else pool[k % 3]
+        x.copy_(_pat(n, r, k))
+        comm.allreduceArray(x, F, SUM, 0, n)
+        torch.cuda.synchronize()
+        fresh_bad += int((x != _exp(n, p, k)).sum())
+    fresh = {"bad": fresh_bad, "launched": launched.count(0), "refused": len(launched) - launched.count(0),
+             "addrs": len({t.data_ptr() for t in pool}), "by_ptr": eng._fast_ar.by_ptr}
+    # with a registered tensor the memo keys on the address: the registered one runs zero-copy
+    y = torch.empty(1 << 18, device="cuda")      # 1 MiB: the two-shot tier, zero-copy when registered
+    comm.registerBuffer(y)
+    keyed = eng._fast_ar.by_ptr
+    zc_before = sum(v for k, v in eng.stats.items() if k.endswith("ipc2z") or k.endswith("ipc_zc"))
+    reg_bad = 0
+    for k in range(4):
+        for t in (y, pool[0]):
+            t.copy_(_pat(t.numel(), r, k))
+            comm.allreduceArray(t, F, SUM, 0, t.numel())
+            torch.cuda.synchronize()
+            reg_bad += int((t != _exp(t.numel(), p, k)).sum())
+    zc = sum(v for k, v in eng.stats.items() if k.endswith("ipc2z") or k.endswith("ipc_zc")) - zc_before
+    comm.deregisterBuffer(y)
+    fresh.update(reg_bad=reg_bad, keyed=keyed, zc_calls=zc, unkeyed_after=not eng._fast_ar.by_ptr)
+    comm._fast_lx = orig
     # an earlier collective that timed out fails the next call (no launch), then the job goes on
     x = torch.empty(1024, device="cuda")
     comm.barrier()
@@ -67,7 +106,7 @@ def _fast_fn(comm):
     comm.registerBuffer(y)
     cleared = len(eng._fast_ar) == 0 and before > 0
     comm.deregisterBuffer(y)
-    return {"sizes": out, "calls": calls, "eng_calls": eng_calls, "raised": raised,
+    return {"sizes": out, "calls": calls, "eng_calls": eng_calls, "raised": raised, "fresh": fresh,
             "after_fail_bad": after_fail_bad, "cleared": cleared}
 
 
@@ -81,3 +120,8 @@ def test_fast_path_is_exact_counted_invalidated_and_fail_stop():
         assert o["eng_calls"] == 2 * 43, o
         assert o["raised"] and "timed out" in o["raised"], o
         assert o["after_fail_bad"] == 0 and o["cleared"], o
+        f = o["fresh"]
+        assert f["bad"] == 0 and f["reg_bad"] == 0, f
+        assert f["addrs"] == 3 and f["by_ptr"] is False, f
+        assert f["launched"] >= 8 and f["refused"] == 3, f    # 9 aligned calls (1st may miss), 3 unaligned
+        assert f["keyed"] and f["zc_calls"] == 4 and f["unkeyed_after"], f

@@ -314,6 +314,19 @@ def test_latency_fast_path_memo_is_invalidated_by_every_decision_input():
     fill()
     inst._changed()                      # register / deregister / memAlloc / prepare_graph / close
     assert not e._fast_ar
+    # the memo keys on the tensor's address only while something is registered
+    from mp4x.parallel.device_engine import _FastMemo
+    e._fast_ar = _FastMemo()
+    e._ipc_obj = inst
+    inst._regs = {}
+    inst._changed()
+    assert e._fast_ar.by_ptr is False
+    inst._regs = {(4096, 1 << 20): object()}
+    inst._changed()
+    assert e._fast_ar.by_ptr is True
+    inst._regs = {}
+    inst._changed()
+    assert e._fast_ar.by_ptr is False
     e._stop_watchdog = lambda: None
     e._owns_pg = False
     fill()
@@ -329,7 +342,7 @@ def test_fast_path_memo_only_from_the_public_api(monkeypatch):
     from mp4x.parallel.device_engine import DeviceEngine
     assert inspect.signature(DeviceEngine.allreduce.__wrapped__).parameters["memo"].default is False
     src = inspect.getsource(process_comm.ProcessCommSlave.allreduceArray)
-    assert "memo=" in src and "self._fast_lx(ent, self._fast_stream())" in src
+    assert "memo=" in src and "self._fast_lx(ent, self._fast_stream(), base)" in src
 
 
 def test_epochs_alternate_parity_across_the_wrap():
@@ -374,13 +387,17 @@ def test_staged_calls_take_the_slots_only_when_fused_one_piece_and_small(monkeyp
              (65540, ipc_mod.ONESHOT, True, False), (1024, ipc_mod.TWOSHOT, True, True),
              (65540, ipc_mod.TWOSHOT, True, False),
              (1024, ipc_mod.ONESHOT, False, False))
-    for n, algo, fuse, want in cases:
+    # an unaligned input on ONE rank must not change the protocol: it is copied to an aligned
+    # temporary and still takes the slots (the decision is rank-independent)
+    cases += ((1024, ipc_mod.ONESHOT, True, True, 1), (1024, ipc_mod.TWOSHOT, True, True, 1))
+    for n, algo, fuse, want, *shift in cases:
         inst._fuse_copy = fuse
         if not fuse:
             inst._data = type("V", (), {"value": 0})()
             inst.lib = type("L", (), {"mp4x_memcpy_async": staticmethod(lambda *a: 0)})()
         calls.clear()
-        t = torch.zeros(n)
-        inst.allreduce(t, Operators.Float.SUM, algo=algo, capturing=False)
+        t = torch.zeros(n + 4)[shift[0]:shift[0] + n] if shift else torch.zeros(n)
+        inst.allreduce(t, Operators.Float.SUM, algo=algo, out=torch.zeros(n), capturing=False)
         (a,) = calls
+        assert not fuse or (a[8] is not None and a[8] % 16 == 0), a[8]    # the fused copy-in's source
         assert a[15:] == ((inst._slot_base, inst._slot_vecs) if want else (0, 0)), (n, algo, fuse, a[15:])
