@@ -5,7 +5,7 @@
 #   OUT=<dir> bash tools/gpu/round.sh
 source "$(dirname "$0")/steps.sh"
 export TMPDIR=/tmp
-step suite 1000 python -u -m pytest -v --timeout 400 --timeout-method thread -p no:cacheprovider -m gpu \
+step suite 1000 python -u -m pytest -v --timeout 170 --timeout-method thread -p no:cacheprovider -m gpu \
   --durations=25 tests
 step smoke 240 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_n1 240 python bench.py --steps 20 --warmup 5
