@@ -150,6 +150,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
     _zc_vmm = True                        # memAlloc builds VMM tensors (False: registered plain ones)
     _ipc_obj = _ipc_large = _ipc_fp8_big = None
     _fast_ar = None                       # (engines assembled without __init__: no fast path)
+    _oneshot_ar_max = 0                   # the staged allreduce's one-shot limit when it differs
 
     def __init__(self, comm, device_index: Optional[int] = None, backend: Optional[str] = None, coll=None,
                  device=None):
@@ -197,6 +198,12 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             and coll is None
         self.ipc_oneshot_max = int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))
         self.ipc_twoshot_max = int(os.environ.get("MP4X_IPC_TWOSHOT_MAX", 16 << 20))
+        # two ranks: the one-shot moves the same bytes over the one link as the two-shot with one
+        # barrier fewer, so the staged allreduce takes it for every size a slot holds (measured on
+        # one GPU: 1.7-2.2x faster than the two-shot at 256 KiB - 4 MiB, profiles/r5/tiers/)
+        from .ipc import SLOTS_ON, SLOT_BYTES
+        self._oneshot_ar_max = max(self.ipc_oneshot_max, SLOT_BYTES) if self.p == 2 and SLOTS_ON and \
+            "MP4X_IPC_ONESHOT_MAX" not in os.environ else 0
         self._ipc_obj = None
         self._ipc_large = None
         self._ipc_large_failed = False   # set on every rank together (setup failure is collective)
@@ -412,6 +419,11 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         h = self._hier
         if h is not None and h.ipc is not None:
             h.ipc.raise_if_failed()
+
+    def _oneshot_limit(self) -> int:
+        """Largest staged allreduce that runs the one-shot (the two-shot above): the latency tier's
+        ``ipc_oneshot_max``, or at two ranks the slot size (see __init__)."""
+        return max(self.ipc_oneshot_max, self._oneshot_ar_max)
 
     # ------------------------------------------------------------------ latency fast path
     def _invalidate_fast(self) -> None:
@@ -768,7 +780,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             # operator of the table in one fused kernel per call; a2a only without a mesh
             if kind in ("allreduce", "reduce") and forced in ("", "auto") and self._ipc_ok(op, dtype, nbytes) \
                     and self.device.type == "cuda":
-                return "ipc1" if kind == "allreduce" and nbytes <= self.ipc_oneshot_max else "ipc2"
+                return "ipc1" if kind == "allreduce" and nbytes <= self._oneshot_limit() else "ipc2"
             return "a2a"
         if forced in ("", "auto") and kind == "allreduce" and nbytes >= self.hier_min_bytes and \
                 self._hier_ok(op, dtype, nbytes):
@@ -779,7 +791,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 and self._algo_valid(forced, op, dtype, nbytes):
             return forced
         if kind == "allreduce" and self._ipc_ok(op, dtype, nbytes):
-            if nbytes <= self.ipc_oneshot_max:
+            if nbytes <= self._oneshot_limit():
                 return "ipc1"
             if nbytes <= self.ipc_twoshot_max or (self.backend != "nccl" and self.device.type == "cuda"
                                                   and self._dm_large != "rccl"):
@@ -1428,8 +1440,8 @@ def _watched(name, fn):
 
 # Attributes the schedule choice reads (DeviceEngine._select): properties whose setter bumps
 # ``_state_ver``, the select memo's view of them (class-level defaults kept).
-_TIER_ATTRS = ("algo", "ipc_enabled", "ipc_oneshot_max", "ipc_twoshot_max", "_hier_failed", "backend", "a2a_bytes",
-               "hier_min_bytes", "_dm_large", "layout", "device")
+_TIER_ATTRS = ("algo", "ipc_enabled", "ipc_oneshot_max", "_oneshot_ar_max", "ipc_twoshot_max", "_hier_failed", "backend",
+               "a2a_bytes", "hier_min_bytes", "_dm_large", "layout", "device")
 
 
 def _tier_attr(name, default):

@@ -71,7 +71,7 @@ def _fast_fn(comm):
     fresh = {"bad": fresh_bad, "launched": launched.count(0), "refused": len(launched) - launched.count(0),
              "addrs": len({t.data_ptr() for t in pool}), "by_ptr": eng._fast_ar.by_ptr}
     # with a registered tensor the memo keys on the address: the registered one runs zero-copy
-    y = torch.empty(1 << 18, device="cuda")      # 1 MiB: the two-shot tier, zero-copy when registered
+    y = torch.empty(1 << 21, device="cuda")      # 8 MiB: the two-shot tier, zero-copy when registered
     comm.registerBuffer(y)
     keyed = eng._fast_ar.by_ptr
     zc_before = sum(v for k, v in eng.stats.items() if k.endswith("ipc2z") or k.endswith("ipc_zc"))

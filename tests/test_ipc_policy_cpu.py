@@ -66,6 +66,22 @@ def test_select_never_returns_a2a_for_a_builtin_op_with_a_mesh():
     assert e.select("allreduce", 4096, CustomOperator(lambda a, b: a), torch.float32, opnd) == "a2a"
 
 
+def test_two_ranks_take_the_one_shot_up_to_the_slot_size(monkeypatch):
+    """At p = 2 the one-shot moves the same bytes as the two-shot with one barrier fewer: the
+    staged allreduce takes it up to the slot size (unless MP4X_IPC_ONESHOT_MAX pins the tier);
+    p > 2 keeps the 256 KiB crossover; the rooted forms' latency tier is unchanged."""
+    opnd = Operands.FLOAT_OPERAND()
+    SUM = Operators.Float.SUM
+    e = _engine()
+    e.p = 2
+    e._oneshot_ar_max = ipc_mod.SLOT_BYTES
+    got = {nb: e.select("allreduce", nb, SUM, torch.float32, opnd) for nb in (256 << 10, 1 << 20, 4 << 20, 8 << 20)}
+    assert got == {256 << 10: "ipc1", 1 << 20: "ipc1", 4 << 20: "ipc1", 8 << 20: "ipc2"}, got
+    assert e.ipc_oneshot_max == 256 << 10
+    e._oneshot_ar_max = 0               # a tier attribute: the select memo follows it
+    assert e.select("allreduce", 1 << 20, SUM, torch.float32, opnd) == "ipc2"
+
+
 def test_select_memo_key_covers_every_tier_input():
     """a2a_bytes, hier_min_bytes, the large-data mode, the layout and the device type
     all feed _select; changing any of them must not return a stale memoised decision."""

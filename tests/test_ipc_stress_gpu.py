@@ -31,7 +31,7 @@ def _worker(port, q, seed):
         torch.cuda.set_device(0)
         comm = ProcessCommSlave("s", "127.0.0.1", port, heartbeat=False)
         r, p = comm.getRank(), comm.getSlaveNum()
-        ipc = IpcAllreduce(comm, nbytes=1 << 20)
+        ipc = IpcAllreduce(comm, nbytes=4 << 20)    # 1-4 MiB single pieces take the slots
         rng = random.Random(seed)
         jitter = random.Random(seed * 31 + r)     # rank-dependent: ranks drift apart in time
         pending = []
@@ -45,7 +45,8 @@ def _worker(port, q, seed):
                 time.sleep(jitter.choice([0.0005, 0.002, 0.005]))
             dt = rng.choice([torch.float32, torch.bfloat16, torch.float64, torch.int32])
             es = torch.empty(0, dtype=dt).element_size()
-            nbytes = rng.choice([16, 256, 4096, 65536, 300_000 // 16 * 16, (1 << 20) + 4096, 3 << 20])
+            nbytes = rng.choice([16, 256, 4096, 65536, 300_000 // 16 * 16, (1 << 20) + 4096, 3 << 20, 4 << 20,
+                                 (4 << 20) + 4096])
             n = nbytes // es
             algo = rng.choice([ONESHOT, TWOSHOT])
             opname = "SUM" if dt in (torch.int32, torch.float64) else rng.choice(["SUM", "MAX"])
