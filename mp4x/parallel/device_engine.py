@@ -896,9 +896,11 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             else:
                 oview.copy_(view)
             view, arr = oview, out
-        if algo == "ipc2" and not self._select_tuned and self._zc and self._ipc_obj is not None \
-                and self._ipc_obj.registered(view) is not None:
-            algo = "ipc2z"      # registered on this rank (registration is collective): zero-copy
+        if (algo == "ipc2" or (algo == "ipc1" and nbytes > self.ipc_oneshot_max)) and not self._select_tuned \
+                and self._zc and self._ipc_obj is not None and self._ipc_obj.registered(view) is not None:
+            # registered on this rank (registration is collective): zero-copy above the latency
+            # tier (also where two ranks would stage into the one-shot's slots)
+            algo = "ipc2z"
         self._count("allreduce." + algo)
         fused = self._run_allreduce(algo, view, op, scale=self._fused_scale(scale, view), capturing=capturing)
         self._post_scale(view, scale, fused)

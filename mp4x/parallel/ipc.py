@@ -455,6 +455,8 @@ class IpcAllreduce(IpcForms):
         incomplete — raise ``Mp4jException`` once (the word is cleared) before launching more.
         Called at the start of every IPC collective (reference fail-stop contract,
         ProcessCommSlave.java:360-373)."""
+        if self.__dict__.get("_closed"):
+            raise Mp4jException(f"rank {self.rank}: IPC instance used after close()")
         code = self.host_error()
         if code:
             ctypes.c_uint32.from_address(self._herr.value).value = 0
@@ -1355,8 +1357,9 @@ class IpcAllreduce(IpcForms):
         between the two halves, so no owner frees what a peer still maps — the process goes on
         allocating and exporting afterwards.  Without it (process teardown, failure paths that
         cannot agree) the halves run back to back."""
-        if self.lib is None:
-            return
+        if self.lib is None or self.__dict__.get("_closed"):
+            return                    # idempotent: a second (collective) close must not barrier again
+        self._closed = True
         self._fast_state = None
         self._changed()
         if sync:
