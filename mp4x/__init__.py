@@ -11,16 +11,24 @@ Quick start (host data, any machine)::
 GPU tensors (``torch.Tensor`` on an MI355X) go through RCCL over xGMI plus the
 hand-written CDNA4 HIP kernels in ``csrc/``.
 """
-from .exceptions import Mp4jException, Mp4xError
-from .operators import (Collective, Container, Operators, Operator, CustomOperator, OpCode, DType,
+import os as _os
+
+# Cross-process device memory (hipIpc handles, RCCL's peer buffers) goes through dmabuf on this
+# platform; the legacy IPC mode fails there with "hipIpcGetMemHandle: invalid argument".  Read by
+# the HSA runtime at its first use, so it only takes effect when mp4x is imported before anything
+# touches the GPU; an explicit setting is kept.
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+from .exceptions import Mp4jException, Mp4xError  # noqa: E402
+from .operators import (Collective, Container, Operators, Operator, CustomOperator, OpCode, DType,  # noqa: E402
                         IDoubleOperator, IFloatOperator, ILongOperator, IIntOperator, IShortOperator,
                         IByteOperator, IStringOperator, IObjectOperator)
-from .operands import Operand, Operands, Serializer, KryoUtils
-from .utils.commutils import CommUtils
-from .utils.scatter_allocate import ScatterAllocate
-from .control.master import CommMaster
-from .parallel.process_comm import ProcessCommSlave, ProcessComm
-from .parallel.thread_comm import ThreadCommSlave, ThreadComm
+from .operands import Operand, Operands, Serializer, KryoUtils  # noqa: E402
+from .utils.commutils import CommUtils  # noqa: E402
+from .utils.scatter_allocate import ScatterAllocate  # noqa: E402
+from .control.master import CommMaster  # noqa: E402
+from .parallel.process_comm import ProcessCommSlave, ProcessComm  # noqa: E402
+from .parallel.thread_comm import ThreadCommSlave, ThreadComm  # noqa: E402
 
 __version__ = "0.1.0"
 
