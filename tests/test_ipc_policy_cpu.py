@@ -417,3 +417,29 @@ def test_staged_calls_take_the_slots_only_when_fused_one_piece_and_small(monkeyp
         (a,) = calls
         assert not fuse or (a[8] is not None and a[8] % 16 == 0), a[8]    # the fused copy-in's source
         assert a[15:] == ((inst._slot_base, inst._slot_vecs) if want else (0, 0)), (n, algo, fuse, a[15:])
+
+
+def test_registered_tensors_keep_zero_copy_above_the_latency_tier_at_two_ranks(monkeypatch):
+    """The two-rank one-shot extension (up to the slot size) is for staged calls: a registered
+    tensor above the 256 KiB latency tier still runs the zero-copy two-shot (no staging copy)."""
+    e = _engine()
+    e.p = 2
+    e._oneshot_ar_max = ipc_mod.SLOT_BYTES
+    e.device = torch.device("cpu")
+    e.stats, e.watchdog, e._hier, e._fast_ar = {}, None, None, None
+    reg = torch.zeros((1 << 20) // 4)
+
+    class _Inst:
+        _epoch_dev = None
+
+        def registered(self, view):
+            return [1, 2] if view.data_ptr() == reg.data_ptr() else None
+    e._ipc_obj = _Inst()
+    ran = []
+    monkeypatch.setattr(e, "_run_allreduce", lambda algo, view, op, scale=1.0, capturing=None: ran.append(algo))
+    monkeypatch.setattr(e, "_post_scale", lambda *a: None)
+    monkeypatch.setattr(e, "check_failed", lambda: None, raising=False)
+    SUM, F = Operators.Float.SUM, Operands.FLOAT_OPERAND()
+    for t in (reg, torch.zeros((1 << 20) // 4), torch.zeros((64 << 10) // 4)):
+        e.allreduce(t, 0, t.numel(), SUM, F)
+    assert ran == ["ipc2z", "ipc1", "ipc1"], ran
