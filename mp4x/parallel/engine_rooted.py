@@ -135,7 +135,7 @@ class RootedMixin:
             # latency tier: the IPC allreduce kernels (non-root results are unspecified by the
             # reduce contract, ProcessCommSlave.java:1390-1421, so every rank may receive the sum)
             from .ipc import ONESHOT, TWOSHOT
-            one = nbytes <= self.ipc_oneshot_max
+            one = nbytes <= self._oneshot_limit()          # (the allreduce's crossover: two ranks, 4 MiB)
             self._count("reduce.ipc1" if one else "reduce.ipc2")
             self._ipc_obj.allreduce(view, op, algo=ONESHOT if one else TWOSHOT)
             return arr
