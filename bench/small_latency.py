@@ -46,11 +46,24 @@ def worker(port, q, sizes, iters, profile=None, ops=False):
                     fn()
                 torch.cuda.synchronize()
                 eng.barrier()
+                prof = None
+                if profile and comm.getRank() == 0:
+                    import cProfile
+                    prof = cProfile.Profile()
+                    prof.enable()
                 t0 = time.perf_counter()
                 for _ in range(iters):
                     fn()
                 torch.cuda.synchronize()
                 out.append({"op": name, "bytes": n * 8, "us_per_call": (time.perf_counter() - t0) / iters * 1e6})
+                if prof is not None:
+                    prof.disable()
+                    import io
+                    import pstats
+                    buf = io.StringIO()
+                    pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(30)
+                    with open(f"{profile}.{name}.{n * 8}.txt", "w") as f:
+                        f.write(buf.getvalue())
                 eng.barrier()
         comm.close(0)
         q.put((comm.getRank(), out))
