@@ -441,7 +441,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
 
     _FAST_MAX = 256
 
-    def _fast_remember(self, arr, frm, to, operator, operand, scale, view, op, algo: str) -> None:
+    def _fast_remember(self, arr, frm, to, operator, operand, scale, view, op, algo: str,
+                       kind: str = "allreduce") -> None:
         """Memoise the native launch of a call that just took the staged latency tier (one-/two-
         shot on the default instance, one piece, fused copy-in, in place, host epochs), keyed by
         everything that decided it, so the next call of that shape runs ``mp4x_ipc_fast_allreduce``
@@ -472,13 +473,15 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         base = arr.data_ptr()
         key = (base if getattr(fa, "by_ptr", True) else 0, arr.get_device(), arr.numel(), frm, to, arr.dtype,
                operator, getattr(operand, "codec", None), getattr(operand, "compress", False), scale)
+        if kind != "allreduce":
+            key = (kind,) + key
         if len(fa) >= self._FAST_MAX:
             fa.clear()
         # the buffer as an offset from the tensor's address: the call passes its tensor's address
         # (an unaligned one is refused natively before anything is launched: the full path runs)
         fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr - base, total,
                    inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
-                   "allreduce." + algo, inst)
+                   kind + "." + algo, inst, kind + "Array")
 
     def _probe_spin(self, inst) -> None:
         if self._probe_depth and inst is not None:

@@ -92,7 +92,10 @@ class RootedMixin:
             return False
         return self.ipc() is not None
 
-    def reduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand, root: int):
+    def reduce(self, arr: torch.Tensor, frm: int, to: int, operator, operand, root: int, memo: bool = False):
+        """``memo`` (the public API's full path): memoise the latency tier's launch (the staged IPC
+        allreduce, which a reduce may run: non-root results are unspecified) for
+        ProcessCommSlave.reduceArray's fast path."""
         flat = self._flat(arr)
         view = flat[frm:to]
         if view.numel() == 0:
@@ -138,6 +141,9 @@ class RootedMixin:
             one = nbytes <= self._oneshot_limit()          # (the allreduce's crossover: two ranks, 4 MiB)
             self._count("reduce.ipc1" if one else "reduce.ipc2")
             self._ipc_obj.allreduce(view, op, algo=ONESHOT if one else TWOSHOT)
+            if memo and self._fast_ar is not None and view.is_cuda and not capturing_now():
+                self._fast_remember(arr, frm, to, operator, operand, 1.0, view, op, "ipc1" if one else "ipc2",
+                                    kind="reduce")
             return arr
         if self.algo in ("", "auto") and self._ipc_ok(op, view.dtype, nbytes) and self._dm_large_ok(flat):
             from .ipc import TWOSHOT          # no RCCL underneath: the piecewise IPC two-shot

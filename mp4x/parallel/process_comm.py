@@ -306,13 +306,13 @@ class ProcessCommSlave:
         """Book-keeping of a fast-path call: the API and engine call counts, and the watchdog's
         device-side coverage (an event when none is outstanding, as ``CollectiveWatchdog.end``)."""
         c = self._fast_calls
-        c["allreduceArray"] = c.get("allreduceArray", 0) + 1
+        c[ent[10]] = c.get(ent[10], 0) + 1
         eng = self._device_engine
         st = eng.stats
         st[ent[8]] = st.get(ent[8], 0) + 1
         wd = eng.watchdog
         if wd is not None and not wd._npending:
-            wd.end(wd.begin("allreduce"), eng.device)
+            wd.end(wd.begin(ent[8].partition(".")[0]), eng.device)
 
     def registerBuffer(self, tensor) -> bool:
         """Collective (extension, like ``ncclCommRegister``): map a device tensor into every peer
@@ -625,13 +625,24 @@ class ProcessCommSlave:
     # ================================================================ reduce
     def reduceArray(self, arrData, operand: Operand, operator, frm: int, to: int, rootRank: int):
         """reduce-scatter + gather (reference :1390-1421)."""
+        fast = self._fast_ar
+        if fast and type(arrData) is self._fast_tensor and arrData.is_cuda and arrData.is_contiguous() and \
+                0 <= rootRank < self.slaveNum:
+            # the latency tier of a reduce is the staged IPC allreduce (every rank gets the sum;
+            # non-root results are unspecified by contract): the same native launch
+            base = arrData.data_ptr()
+            ent = fast.get(("reduce", base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
+                            arrData.dtype, operator, operand.codec, operand.compress, 1.0))
+            if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
+                self._fast_after(ent)
+                return arrData
         self._tick("reduceArray")
         if self.slaveNum == 1:
             return arrData
         CommUtils.isFromToLegal(frm, to)
         self._check_root(rootRank)
         if _is_device_tensor(arrData):
-            return self.device.reduce(arrData, frm, to, operator, operand, rootRank)
+            return self.device.reduce(arrData, frm, to, operator, operand, rootRank, memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         shm = self._shm_engine(buf, operand, operator, to - frm)
         if shm is not None and buf.flags.c_contiguous:

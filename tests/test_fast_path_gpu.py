@@ -85,6 +85,19 @@ def _fast_fn(comm):
     zc = sum(v for k, v in eng.stats.items() if k.endswith("ipc2z") or k.endswith("ipc_zc")) - zc_before
     comm.deregisterBuffer(y)
     fresh.update(reg_bad=reg_bad, keyed=keyed, zc_calls=zc, unkeyed_after=not eng._fast_ar.by_ptr)
+    # reduceArray's latency tier is the same staged allreduce: memoised, then one native call
+    launched.clear()
+    z = torch.empty(1024, device="cuda")
+    red_bad = 0
+    for k in range(6):
+        z.copy_(_pat(1024, r, k))
+        comm.reduceArray(z, F, SUM, 0, 1024, 0)
+        torch.cuda.synchronize()
+        if r == 0:
+            red_bad += int((z != _exp(1024, p, k)).sum())
+    fresh.update(reduce_bad=red_bad, reduce_launched=launched.count(0),
+                 reduce_calls=comm.stats["calls"].get("reduceArray", 0),
+                 reduce_eng=sum(v for k, v in eng.stats.items() if k.startswith("reduce.ipc")))
     comm._fast_lx = orig
     # an earlier collective that timed out fails the next call (no launch), then the job goes on
     x = torch.empty(1024, device="cuda")
@@ -125,3 +138,5 @@ def test_fast_path_is_exact_counted_invalidated_and_fail_stop():
         assert f["addrs"] == 3 and f["by_ptr"] is False, f
         assert f["launched"] >= 8 and f["refused"] == 3, f    # 9 aligned calls (1st may miss), 3 unaligned
         assert f["keyed"] and f["zc_calls"] == 4 and f["unkeyed_after"], f
+        assert f["reduce_bad"] == 0 and f["reduce_launched"] >= 5, f     # the first call memoises
+        assert f["reduce_calls"] == 6 and f["reduce_eng"] == 6, f          # counted like the full path
