@@ -27,6 +27,13 @@ using FastAllreduce = int (*)(const void* state, int algo, int dtype, int op, vo
                               float scale, void* stream);
 FastAllreduce g_fast = nullptr;
 
+// mp4x_ipc_fast_plan(state, stage, nstage, pull, npull, src_off, out_off, base, grid_len, buf_vecs,
+// blocks, stream): the same one-call path for a memoised copy plan.
+using FastPlan = int (*)(const void* state, const int64_t* stage, int nstage, const int64_t* pull, int npull,
+                         int64_t src_off, int64_t out_off, void* base, int64_t grid_len, int64_t buf_vecs, int blocks,
+                         void* stream);
+FastPlan g_fast_plan = nullptr;
+
 void* as_ptr(PyObject* o) {   // int address, or None -> NULL
   if (o == Py_None) return nullptr;
   return PyLong_AsVoidPtr(o);
@@ -115,7 +122,51 @@ PyObject* fast_allreduce(PyObject*, PyObject* const* a, Py_ssize_t na) {
   return PyLong_FromLong(rc);
 }
 
+PyObject* bind_fast_plan(PyObject*, PyObject* addr) {
+  void* f = PyLong_AsVoidPtr(addr);
+  if (!f && PyErr_Occurred()) return nullptr;
+  g_fast_plan = reinterpret_cast<FastPlan>(f);
+  Py_RETURN_NONE;
+}
+
+// fast_plan(entry, stream, base) -> rc.  `entry`: the engine's memoised copy plan (state address,
+// stage array address, nstage, pull array address, npull, src_off, out_off, grid_len, buf_vecs,
+// blocks, ...); rc != 0 = not launched (an earlier collective failed / capturing / unaligned): the
+// caller takes the full path.
+PyObject* fast_plan(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 3 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) < 10) {
+    PyErr_SetString(PyExc_TypeError, "fast_plan(entry: tuple of >= 10, stream, base)");
+    return nullptr;
+  }
+  if (!g_fast_plan) {
+    PyErr_SetString(PyExc_RuntimeError, "_mp4x_launch: bind_fast_plan() was not called");
+    return nullptr;
+  }
+  PyObject* const* t = &PyTuple_GET_ITEM(a[0], 0);
+  const void* state = PyLong_AsVoidPtr(t[0]);
+  const int64_t* stage = static_cast<const int64_t*>(PyLong_AsVoidPtr(t[1]));
+  const int nstage = (int)PyLong_AsLong(t[2]);
+  const int64_t* pull = static_cast<const int64_t*>(PyLong_AsVoidPtr(t[3]));
+  const int npull = (int)PyLong_AsLong(t[4]);
+  const int64_t src_off = PyLong_AsLongLong(t[5]);
+  const int64_t out_off = PyLong_AsLongLong(t[6]);
+  const int64_t grid_len = PyLong_AsLongLong(t[7]);
+  const int64_t buf_vecs = PyLong_AsLongLong(t[8]);
+  const int blocks = (int)PyLong_AsLong(t[9]);
+  void* stream = as_ptr(a[1]);
+  void* base = PyLong_AsVoidPtr(a[2]);
+  if (PyErr_Occurred()) return nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = g_fast_plan(state, stage, nstage, pull, npull, src_off, out_off, base, grid_len, buf_vecs, blocks, stream);
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 PyMethodDef kMethods[] = {
+    {"bind_fast_plan", bind_fast_plan, METH_O, "bind_fast_plan(address of mp4x_ipc_fast_plan in libmp4x_hip.so)"},
+    {"fast_plan", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_plan)), METH_FASTCALL,
+     "fast_plan(entry, stream, base) -> rc"},
     {"bind_fast", bind_fast, METH_O, "bind_fast(address of mp4x_ipc_fast_allreduce in the loaded libmp4x_hip.so)"},
     {"fast_allreduce", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_allreduce)), METH_FASTCALL,
      "fast_allreduce(entry, stream) -> rc"},

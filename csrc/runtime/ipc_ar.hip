@@ -190,6 +190,37 @@ extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int
                                 blocks, nullptr, scale, stream, slotted ? s->slot_base : 0, slotted ? s->slot_vecs : 0);
 }
 
+extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
+                                  const int64_t* stage, int nstage, const int64_t* pull, int npull, const void* src,
+                                  void* out, int64_t grid_len, int64_t buf_vecs, uint32_t epoch, int blocks,
+                                  const uint32_t* epoch_dev, void* stream);
+
+// The same one-call path for a memoised copy plan (the latency tier of broadcast / gather /
+// scatter / all-gather, csrc/runtime/ipc.hip k_ipc_copy_plan): error words, capture check, the
+// buffer's alignment — all refused before the epoch moves — then the epoch bump and the launch.
+// src_off / out_off: byte offsets of the plan's source / output from `base` (the caller's tensor),
+// or -1 for none.
+extern "C" int mp4x_ipc_fast_plan(const FastAr* s, const int64_t* stage, int nstage, const int64_t* pull, int npull,
+                                  int64_t src_off, int64_t out_off, void* base, int64_t grid_len, int64_t buf_vecs,
+                                  int blocks, void* stream) {
+  for (int i = 0; i < 8 && s->herr[i]; ++i)
+    if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return MP4X_E_CAPTURING;
+  }
+  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  char* b = static_cast<char*>(base);
+  const void* src = src_off >= 0 ? b + src_off : nullptr;
+  void* out = out_off >= 0 ? b + out_off : nullptr;
+  if (!b || ((uintptr_t)src & 15) || ((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  const uint32_t e = next_epoch(*s->epoch);
+  *s->epoch = e;
+  return mp4x_ipc_copy_plan(s->data_ptrs, s->signal_ptrs, s->rank, s->p, stage, nstage, pull, npull, src, out,
+                            grid_len, buf_vecs, e, blocks, nullptr, stream);
+}
+
 extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                      int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
                                      int blocks, const uint32_t* epoch_dev, float scale, void* stream) {

@@ -231,6 +231,9 @@ def launch_ext():
                         fast = getattr(lib, "mp4x_ipc_fast_allreduce", None)
                         if fast is not None and hasattr(mod, "bind_fast"):
                             mod.bind_fast(ctypes.cast(fast, ctypes.c_void_p).value)
+                        plan = getattr(lib, "mp4x_ipc_fast_plan", None)
+                        if plan is not None and hasattr(mod, "bind_fast_plan"):
+                            mod.bind_fast_plan(ctypes.cast(plan, ctypes.c_void_p).value)
                     except Exception:   # noqa: BLE001 — ctypes path stays
                         mod = False
                 _launch_ext = mod

@@ -36,6 +36,7 @@ remainder in allreduce/reduce splits, rank-order reductions) — see process_com
 from __future__ import annotations
 
 import contextlib
+import ctypes
 import datetime
 import logging
 import os
@@ -462,10 +463,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 not view.is_contiguous() or capturing_now():
             return
         from .ipc import ONESHOT, TWOSHOT
-        h = self._hier
-        words = [i._herr.value for i in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big,
-                                         h.ipc if h is not None else None) if i is not None and i._herr]
-        state = inst.fast_state(words)
+        state = inst.fast_state(self._fast_words())
         if state is None:
             return
         a = ONESHOT if algo == "ipc1" else TWOSHOT
@@ -482,6 +480,53 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr - base, total,
                    inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
                    kind + "." + algo, inst, kind + "Array")
+
+    def _fast_words(self) -> list:
+        """The pinned host error words of every IPC instance (the fast paths' fail-stop check)."""
+        h = self._hier
+        return [i._herr.value for i in (self._ipc_obj, self._ipc_large, self._ipc_fp8_big,
+                                        h.ipc if h is not None else None) if i is not None and i._herr]
+
+    def _plan_memo(self, memo: bool, kind: str, arr, key_tail: tuple, fn) -> bool:
+        """Run ``fn``, a staged copy-plan form of the default instance (the latency tier of
+        broadcast / gather / scatter / all-gather).  With ``memo`` (the public API's full path),
+        a call that ran exactly ONE host-epoch copy plan reading / writing only ``arr`` is
+        memoised for the API's fast path (``mp4x_ipc_fast_plan``), keyed like the allreduce memo
+        (shape, device, the tensor's address only while something is registered) plus
+        ``key_tail`` (ranges, root).  Anything else (a temporary for an unaligned tensor, several
+        launches, device epochs) is not memoised."""
+        inst = self._ipc_obj
+        fa = self.__dict__.get("_fast_ar")
+        if not memo or not isinstance(fa, _FastMemo) or inst is None or self._probe_depth or \
+                os.environ.get("MP4X_FAST_PATH", "1") != "1":
+            return fn()
+        sink = []
+        inst._plan_sink = sink
+        try:
+            ok = fn()
+        finally:
+            inst._plan_sink = None
+        if not ok or len(sink) != 1 or sink[0][9] is not None or capturing_now():
+            return ok
+        sa, ns, pa, npl, src, out, grid_len, buf_vecs, blocks, _ = sink[0]
+        base = arr.data_ptr()
+        end = base + arr.numel() * arr.element_size()
+        if any(x is not None and not base <= x < end for x in (src, out)):
+            return ok
+        from ..ops import native
+        lx = native.launch_ext()
+        if lx is None or not hasattr(lx, "fast_plan"):
+            return ok
+        state = inst.fast_state(self._fast_words())
+        if state is None:
+            return ok
+        key = (kind, base if fa.by_ptr else 0, arr.get_device(), arr.numel(), arr.dtype) + key_tail
+        if len(fa) >= self._FAST_MAX:
+            fa.clear()
+        fa[key] = (state, ctypes.addressof(sa), ns, ctypes.addressof(pa), npl,
+                   src - base if src is not None else -1, out - base if out is not None else -1,
+                   grid_len, buf_vecs, blocks, kind + ".ipc", kind + "Array", inst, sa, pa)
+        return ok
 
     def _probe_spin(self, inst) -> None:
         if self._probe_depth and inst is not None:
@@ -1263,13 +1308,15 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         return arr
 
     # ================================================================== allgather
-    def allgather(self, arr: torch.Tensor, froms, tos):
+    def allgather(self, arr: torch.Tensor, froms, tos, memo: bool = False):
         flat = self._flat(arr)
         whole = flat[froms[0]:tos[-1]]
         if whole.numel() and self._zc_ok(whole) and self._ipc_obj.allgather_registered(flat, froms, tos):
             self._count("allgather.ipc_zc")            # registered tensor: zero copy, any size
             return arr
-        if whole.numel() and self._ipc_direct_ok(None, whole) and self._ipc_obj.allgather(flat, froms, tos):
+        if whole.numel() and self._ipc_direct_ok(None, whole) and \
+                self._plan_memo(memo, "allgather", arr, (tuple(froms), tuple(tos)),
+                                lambda: self._ipc_obj.allgather(flat, froms, tos)):
             self._count("allgather.ipc")
             return arr
         big = self._large_choice("allgather", whole, None) if whole.numel() else None

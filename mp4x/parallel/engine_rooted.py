@@ -22,7 +22,7 @@ from ..utils.commutils import CommUtils
 class RootedMixin:
     """broadcast / reduce / gather / scatter; state lives on the engine."""
 
-    def broadcast(self, arr: torch.Tensor, frm: int, to: int, root: int):
+    def broadcast(self, arr: torch.Tensor, frm: int, to: int, root: int, memo: bool = False):
         flat = self._flat(arr)
         if to > frm:
             t = self._root_tuned("broadcast", flat[frm:to], None)
@@ -46,7 +46,8 @@ class RootedMixin:
                 self._count("broadcast.ipc_zc")
                 return arr
             if self._ipc_small_ok(flat, (to - frm) * flat.element_size()) and \
-                    self._ipc_obj.broadcast(flat, frm, to, root):
+                    self._plan_memo(memo, "broadcast", arr, (frm, to, root),
+                                    lambda: self._ipc_obj.broadcast(flat, frm, to, root)):
                 self._count("broadcast.ipc")
                 return arr
             if self._dm_large_ok(flat) and self.ipc_large().broadcast_large(flat, frm, to, root):
@@ -170,7 +171,7 @@ class RootedMixin:
         return arr
 
     # ================================================================== gather / scatter (p2p)
-    def gather(self, arr: torch.Tensor, froms, tos, root: int):
+    def gather(self, arr: torch.Tensor, froms, tos, root: int, memo: bool = False):
         flat = self._flat(arr)
         r = self.rank
         t = self._root_tuned("gather", flat[froms[0]:tos[-1]], None)
@@ -184,7 +185,8 @@ class RootedMixin:
             self._count("gather.ipc_large")
             return arr
         if t != "p2p" and self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
-                self._ipc_obj.gather(flat, froms, tos, root):
+                self._plan_memo(memo, "gather", arr, (tuple(froms), tuple(tos), root),
+                                lambda: self._ipc_obj.gather(flat, froms, tos, root)):
             self._count("gather.ipc")
             return arr
         if t != "p2p" and self._dm_large_ok(flat) and self.ipc_large().gather_large(flat, froms, tos, root):
@@ -197,7 +199,7 @@ class RootedMixin:
             self.coll.p2p([(flat[froms[r]:tos[r]], root)], [])
         return arr
 
-    def scatter(self, arr: torch.Tensor, froms, tos, root: int):
+    def scatter(self, arr: torch.Tensor, froms, tos, root: int, memo: bool = False):
         flat = self._flat(arr)
         r = self.rank
         t = self._root_tuned("scatter", flat[froms[0]:tos[-1]], None)
@@ -211,7 +213,8 @@ class RootedMixin:
             self._count("scatter.ipc_large")
             return arr
         if t != "p2p" and self._ipc_small_ok(flat, (tos[-1] - froms[0]) * flat.element_size()) and \
-                self._ipc_obj.scatter(flat, froms, tos, root):
+                self._plan_memo(memo, "scatter", arr, (tuple(froms), tuple(tos), root),
+                                lambda: self._ipc_obj.scatter(flat, froms, tos, root)):
             self._count("scatter.ipc")
             return arr
         if t != "p2p" and self._dm_large_ok(flat) and self.ipc_large().scatter_large(flat, froms, tos, root):

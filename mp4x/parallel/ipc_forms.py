@@ -426,15 +426,21 @@ class IpcForms:
     # their data into their own buffers inside the kernel, the receivers pull it over xGMI.  For
     # messages up to the buffer size; ranges must be whole 16-byte vectors from a 16-byte aligned
     # tensor (checked identically on every rank from the shared arguments).
+    _plan_sink = None        # a list while the engine records a call's plans (latency memo)
+
     def _plan(self, stage, pull, src_ptr, out_ptr, grid_len) -> None:
         self.raise_if_failed()
         st = stream_ptr()
         edev = self._next_epoch(st)
         sa = (c_int64 * (4 * max(1, len(stage))))(*[x for it in stage for x in it])
         pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
+        blocks = self._grid(grid_len)
+        sink = self._plan_sink
+        if sink is not None:
+            sink.append((sa, len(stage), pa, len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, blocks, edev))
         check(self.lib.mp4x_ipc_copy_plan(self._pp_data[0], self._pp_sig[0], self.rank, self.p, sa, len(stage), pa,
                                           len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, self.epoch,
-                                          self._grid(grid_len), edev, st), "mp4x_ipc_copy_plan")
+                                          blocks, edev, st), "mp4x_ipc_copy_plan")
 
     def _vec_ok(self, view: torch.Tensor, bounds) -> bool:
         """Rank-independent qualification (shape, ranges, capture state).  The tensor's own

@@ -114,6 +114,7 @@ class ProcessCommSlave:
         self.closed = False
         self._device_engine = None
         self._fast_ar = None       # the device engine's latency memo (allreduceArray fast path)
+        self._fast_pl = None       # its copy-plan launcher (broadcast / gather / scatter / allgather)
         self._device_index = device
         self._shm = None
         LOG.info("master host:%s, master port:%s", masterHost, masterPort)
@@ -297,22 +298,44 @@ class ProcessCommSlave:
             return
         import torch
         self._fast_lx = lx.fast_allreduce
+        self._fast_pl = getattr(lx, "fast_plan", None)
         self._fast_stream = native.stream_ptr
         self._fast_tensor = torch.Tensor
         self._fast_calls = self.stats["calls"]
         self._fast_ar = eng._fast_ar
 
-    def _fast_after(self, ent) -> None:
+    def _fast_after(self, stat: str, api: str) -> None:
         """Book-keeping of a fast-path call: the API and engine call counts, and the watchdog's
         device-side coverage (an event when none is outstanding, as ``CollectiveWatchdog.end``)."""
         c = self._fast_calls
-        c[ent[10]] = c.get(ent[10], 0) + 1
+        c[api] = c.get(api, 0) + 1
         eng = self._device_engine
         st = eng.stats
-        st[ent[8]] = st.get(ent[8], 0) + 1
+        st[stat] = st.get(stat, 0) + 1
         wd = eng.watchdog
         if wd is not None and not wd._npending:
-            wd.end(wd.begin(ent[8].partition(".")[0]), eng.device)
+            wd.end(wd.begin(stat.partition(".")[0]), eng.device)
+
+    def _fast_plan_call(self, kind: str, arrData, tail: tuple) -> bool:
+        """The latency fast path of broadcast / gather / scatter / all-gather: a call shape the
+        engine memoised (one staged copy plan, DeviceEngine._plan_memo) runs as ONE native call
+        (``mp4x_ipc_fast_plan``: error words, capture check, alignment, epoch, launch).  False:
+        not memoised or not launched — the full path decides, validates, raises or records.  A
+        hit implies the ranges and root were validated when the shape was memoised."""
+        if self._fast_pl is None or type(arrData) is not self._fast_tensor or not arrData.is_cuda or \
+                not arrData.is_contiguous():
+            return False
+        fast = self._fast_ar
+        base = arrData.data_ptr()
+        try:
+            ent = fast.get((kind, base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(),
+                            arrData.dtype) + tail)
+        except TypeError:               # unhashable ranges (e.g. arrays): the full path
+            return False
+        if ent is None or self._fast_pl(ent, self._fast_stream(), base) != 0:
+            return False
+        self._fast_after(ent[10], ent[11])
+        return True
 
     def registerBuffer(self, tensor) -> bool:
         """Collective (extension, like ``ncclCommRegister``): map a device tensor into every peer
@@ -393,6 +416,9 @@ class ProcessCommSlave:
     # ================================================================ gather
     def gatherArray(self, arrData, operand: Operand, sendfroms: Sequence[int], sendtos: Sequence[int],
                     rootRank: int):
+        if self._fast_ar and type(sendfroms) is list and type(sendtos) is list and \
+                self._fast_plan_call("gather", arrData, (tuple(sendfroms), tuple(sendtos), rootRank)):
+            return arrData
         self._tick("gatherArray")
         self._check_len(sendfroms, "sendfroms")
         self._check_len(sendtos, "sendtos")
@@ -401,7 +427,8 @@ class ProcessCommSlave:
         CommUtils.isfromsTosLegal(sendfroms, sendtos)
         self._check_root(rootRank)
         if _is_device_tensor(arrData):
-            return self.device.gather(arrData, list(sendfroms), list(sendtos), rootRank)
+            return self.device.gather(arrData, list(sendfroms), list(sendtos), rootRank,
+                                      memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         self.engine.tree_gather(buf, sendfroms, sendtos, operand, rootRank)
         return arrData
@@ -469,6 +496,9 @@ class ProcessCommSlave:
 
     # ================================================================ allgather
     def allgatherArray(self, arrData, operand: Operand, froms: Sequence[int], tos: Sequence[int]):
+        if self._fast_ar and type(froms) is list and type(tos) is list and \
+                self._fast_plan_call("allgather", arrData, (tuple(froms), tuple(tos))):
+            return arrData
         self._tick("allgatherArray")
         self._check_len(froms, "froms")
         self._check_len(tos, "tos")
@@ -476,7 +506,7 @@ class ProcessCommSlave:
             return arrData
         CommUtils.isfromsTosLegal(froms, tos)
         if _is_device_tensor(arrData):
-            return self.device.allgather(arrData, list(froms), list(tos))
+            return self.device.allgather(arrData, list(froms), list(tos), memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         shm = self._shm_engine(buf, operand, None, tos[-1] - froms[0])
         if shm is not None and buf.flags.c_contiguous:
@@ -496,13 +526,15 @@ class ProcessCommSlave:
 
     # ================================================================ broadcast
     def broadcastArray(self, arrData, operand: Operand, frm: int, to: int, rootRank: int):
+        if self._fast_ar and self._fast_plan_call("broadcast", arrData, (frm, to, rootRank)):
+            return arrData
         self._tick("broadcastArray")
         if self.slaveNum == 1:
             return arrData
         CommUtils.isFromToLegal(frm, to)
         self._check_root(rootRank)
         if _is_device_tensor(arrData):
-            return self.device.broadcast(arrData, frm, to, rootRank)
+            return self.device.broadcast(arrData, frm, to, rootRank, memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         shm = self._shm_engine(buf, operand, None, to - frm)
         if shm is not None and buf.flags.c_contiguous:
@@ -549,6 +581,9 @@ class ProcessCommSlave:
     # ================================================================ scatter
     def scatterArray(self, arrData, operand: Operand, recvfroms: Sequence[int], recvtos: Sequence[int],
                      rootRank: int):
+        if self._fast_ar and type(recvfroms) is list and type(recvtos) is list and \
+                self._fast_plan_call("scatter", arrData, (tuple(recvfroms), tuple(recvtos), rootRank)):
+            return arrData
         self._tick("scatterArray")
         self._check_len(recvfroms, "recvfroms")
         self._check_len(recvtos, "recvtos")
@@ -557,7 +592,8 @@ class ProcessCommSlave:
         CommUtils.isfromsTosLegal(recvfroms, recvtos)
         self._check_root(rootRank)
         if _is_device_tensor(arrData):
-            return self.device.scatter(arrData, list(recvfroms), list(recvtos), rootRank)
+            return self.device.scatter(arrData, list(recvfroms), list(recvtos), rootRank,
+                                       memo=self._fast_ar is not None)
         buf = _host_view(arrData, operand)
         self.engine.tree_scatter(buf, recvfroms, recvtos, operand, rootRank)
         return arrData
@@ -634,7 +670,7 @@ class ProcessCommSlave:
             ent = fast.get(("reduce", base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
                             arrData.dtype, operator, operand.codec, operand.compress, 1.0))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
-                self._fast_after(ent)
+                self._fast_after(ent[8], ent[10])
                 return arrData
         self._tick("reduceArray")
         if self.slaveNum == 1:
@@ -831,7 +867,7 @@ class ProcessCommSlave:
             ent = fast.get((base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
                             arrData.dtype, operator, operand.codec, operand.compress, scale))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
-                self._fast_after(ent)
+                self._fast_after(ent[8], ent[10])
                 return arrData
             # not memoised, or not launched (rc 1003: an earlier collective failed; 1004: the stream
             # is being captured; an unaligned buffer): the full path decides, raises or records

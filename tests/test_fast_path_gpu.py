@@ -99,6 +99,52 @@ def _fast_fn(comm):
                  reduce_calls=comm.stats["calls"].get("reduceArray", 0),
                  reduce_eng=sum(v for k, v in eng.stats.items() if k.startswith("reduce.ipc")))
     comm._fast_lx = orig
+    # broadcast / gather / scatter / all-gather: one memoised copy plan, then one native call each
+    from mp4x import CommUtils
+    plan_rc = []
+    orig_pl = comm._fast_pl
+
+    def spy_pl(*a):
+        rc = orig_pl(*a)
+        plan_rc.append(rc)
+        return rc
+    comm._fast_pl = spy_pl
+    n = 1024
+    fr, to = CommUtils.createProcessArrayFroms(n, p), CommUtils.createProcessArrayTos(n, p)
+    root = p - 1
+    plan_bad = dict.fromkeys(("broadcast", "gather", "scatter", "allgather"), 0)
+    for k in range(6):
+        w = torch.full((n,), -1.0, device="cuda")
+        if r == root:
+            w.copy_(_pat(n, 7, k))
+        comm.broadcastArray(w, F, 0, n, root)
+        torch.cuda.synchronize()
+        plan_bad["broadcast"] = plan_bad.get("broadcast", 0) + int((w != _pat(n, 7, k)).sum())
+        w = torch.full((n,), -1.0, device="cuda")
+        w[fr[r]:to[r]] = float(r + k)
+        comm.gatherArray(w, F, list(fr), list(to), root)
+        torch.cuda.synchronize()
+        if r == root:
+            plan_bad["gather"] = plan_bad.get("gather", 0) + sum(
+                int((w[fr[j]:to[j]] != float(j + k)).sum()) for j in range(p))
+        w = torch.full((n,), -1.0, device="cuda")
+        if r == root:
+            for j in range(p):
+                w[fr[j]:to[j]] = float(10 * j + k)
+        comm.scatterArray(w, F, list(fr), list(to), root)
+        torch.cuda.synchronize()
+        plan_bad["scatter"] = plan_bad.get("scatter", 0) + int((w[fr[r]:to[r]] != float(10 * r + k)).sum())
+        w = torch.full((n,), -1.0, device="cuda")
+        w[fr[r]:to[r]] = float(r - k)
+        comm.allgatherArray(w, F, list(fr), list(to))
+        torch.cuda.synchronize()
+        plan_bad["allgather"] = plan_bad.get("allgather", 0) + sum(
+            int((w[fr[j]:to[j]] != float(j - k)).sum()) for j in range(p))
+    comm._fast_pl = orig_pl
+    api_calls = comm.stats["calls"]
+    fresh.update(plan_bad=plan_bad, plan_launched=plan_rc.count(0), plan_refused=len(plan_rc) - plan_rc.count(0),
+                 plan_calls={k: api_calls.get(k + "Array", 0) for k in ("broadcast", "gather", "scatter", "allgather")},
+                 plan_eng={k: eng.stats.get(k + ".ipc", 0) for k in ("broadcast", "gather", "scatter", "allgather")})
     # an earlier collective that timed out fails the next call (no launch), then the job goes on
     x = torch.empty(1024, device="cuda")
     comm.barrier()
@@ -140,3 +186,7 @@ def test_fast_path_is_exact_counted_invalidated_and_fail_stop():
         assert f["keyed"] and f["zc_calls"] == 4 and f["unkeyed_after"], f
         assert f["reduce_bad"] == 0 and f["reduce_launched"] >= 5, f     # the first call memoises
         assert f["reduce_calls"] == 6 and f["reduce_eng"] == 6, f          # counted like the full path
+        assert all(v == 0 for v in f["plan_bad"].values()) and len(f["plan_bad"]) == 4, f
+        assert f["plan_launched"] >= 20 and f["plan_refused"] == 0, f      # 4 ops x 6 calls, first ones memoise
+        assert all(v == 6 for v in f["plan_calls"].values()), f
+        assert all(v == 6 for v in f["plan_eng"].values()), f
