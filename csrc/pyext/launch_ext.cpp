@@ -34,6 +34,12 @@ using FastPlan = int (*)(const void* state, const int64_t* stage, int nstage, co
                          void* stream);
 FastPlan g_fast_plan = nullptr;
 
+// mp4x_ipc_fast_rs(state, dtype, op, seg_lo, seg_hi, src_off, out_off, base, blocks, stream): the
+// same for a memoised fused reduce-scatter.
+using FastRs = int (*)(const void* state, int dtype, int op, const int64_t* seg_lo, const int64_t* seg_hi,
+                       int64_t src_off, int64_t out_off, void* base, int blocks, void* stream);
+FastRs g_fast_rs = nullptr;
+
 void* as_ptr(PyObject* o) {   // int address, or None -> NULL
   if (o == Py_None) return nullptr;
   return PyLong_AsVoidPtr(o);
@@ -163,7 +169,47 @@ PyObject* fast_plan(PyObject*, PyObject* const* a, Py_ssize_t na) {
   return PyLong_FromLong(rc);
 }
 
+PyObject* bind_fast_rs(PyObject*, PyObject* addr) {
+  void* f = PyLong_AsVoidPtr(addr);
+  if (!f && PyErr_Occurred()) return nullptr;
+  g_fast_rs = reinterpret_cast<FastRs>(f);
+  Py_RETURN_NONE;
+}
+
+// fast_rs(entry, stream, base) -> rc.  `entry`: the engine's memoised reduce-scatter (state
+// address, dtype, op, seg_lo array address, seg_hi array address, src_off, out_off, blocks, ...).
+PyObject* fast_rs(PyObject*, PyObject* const* a, Py_ssize_t na) {
+  if (na != 3 || !PyTuple_Check(a[0]) || PyTuple_GET_SIZE(a[0]) < 8) {
+    PyErr_SetString(PyExc_TypeError, "fast_rs(entry: tuple of >= 8, stream, base)");
+    return nullptr;
+  }
+  if (!g_fast_rs) {
+    PyErr_SetString(PyExc_RuntimeError, "_mp4x_launch: bind_fast_rs() was not called");
+    return nullptr;
+  }
+  PyObject* const* t = &PyTuple_GET_ITEM(a[0], 0);
+  const void* state = PyLong_AsVoidPtr(t[0]);
+  const int dtype = (int)PyLong_AsLong(t[1]);
+  const int op = (int)PyLong_AsLong(t[2]);
+  const int64_t* lo = static_cast<const int64_t*>(PyLong_AsVoidPtr(t[3]));
+  const int64_t* hi = static_cast<const int64_t*>(PyLong_AsVoidPtr(t[4]));
+  const int64_t src_off = PyLong_AsLongLong(t[5]);
+  const int64_t out_off = PyLong_AsLongLong(t[6]);
+  const int blocks = (int)PyLong_AsLong(t[7]);
+  void* stream = as_ptr(a[1]);
+  void* base = PyLong_AsVoidPtr(a[2]);
+  if (PyErr_Occurred()) return nullptr;
+  int rc;
+  Py_BEGIN_ALLOW_THREADS
+  rc = g_fast_rs(state, dtype, op, lo, hi, src_off, out_off, base, blocks, stream);
+  Py_END_ALLOW_THREADS
+  return PyLong_FromLong(rc);
+}
+
 PyMethodDef kMethods[] = {
+    {"bind_fast_rs", bind_fast_rs, METH_O, "bind_fast_rs(address of mp4x_ipc_fast_rs in libmp4x_hip.so)"},
+    {"fast_rs", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_rs)), METH_FASTCALL,
+     "fast_rs(entry, stream, base) -> rc"},
     {"bind_fast_plan", bind_fast_plan, METH_O, "bind_fast_plan(address of mp4x_ipc_fast_plan in libmp4x_hip.so)"},
     {"fast_plan", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)()>(fast_plan)), METH_FASTCALL,
      "fast_plan(entry, stream, base) -> rc"},

@@ -221,6 +221,33 @@ extern "C" int mp4x_ipc_fast_plan(const FastAr* s, const int64_t* stage, int nst
                             grid_len, buf_vecs, e, blocks, nullptr, stream);
 }
 
+extern "C" int mp4x_ipc_reduce_scatter_from(int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
+                                            int rank, int p, const int64_t* seg_lo, const int64_t* seg_hi,
+                                            const void* src, void* out, uint32_t epoch, int blocks,
+                                            const uint32_t* epoch_dev, void* stream);
+
+// The same one-call path for a memoised fused reduce-scatter (csrc/runtime/ipc_rs.hip: the
+// kernel stages this rank's range and writes its segment in place).  seg_lo / seg_hi: p segment
+// bounds in 16-byte vectors from the range start; src_off / out_off: byte offsets from `base`.
+extern "C" int mp4x_ipc_fast_rs(const FastAr* s, int dtype, int op, const int64_t* seg_lo, const int64_t* seg_hi,
+                                int64_t src_off, int64_t out_off, void* base, int blocks, void* stream) {
+  for (int i = 0; i < 8 && s->herr[i]; ++i)
+    if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
+    (void)hipGetLastError();
+    return MP4X_E_CAPTURING;
+  }
+  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  char* b = static_cast<char*>(base);
+  if (!b || src_off < 0 || out_off < 0 || ((uintptr_t)(b + src_off) & 15) || ((uintptr_t)(b + out_off) & 15))
+    return MP4X_E_BADARG;
+  const uint32_t e = next_epoch(*s->epoch);
+  *s->epoch = e;
+  return mp4x_ipc_reduce_scatter_from(dtype, op, s->data_ptrs, s->signal_ptrs, s->rank, s->p, seg_lo, seg_hi,
+                                      b + src_off, b + out_off, e, blocks, nullptr, stream);
+}
+
 extern "C" int mp4x_ipc_allreduce_ex(int algo, int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                      int rank, int p, int64_t nbytes, const void* src, void* out, uint32_t epoch,
                                      int blocks, const uint32_t* epoch_dev, float scale, void* stream) {

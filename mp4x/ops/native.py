@@ -234,6 +234,9 @@ def launch_ext():
                         plan = getattr(lib, "mp4x_ipc_fast_plan", None)
                         if plan is not None and hasattr(mod, "bind_fast_plan"):
                             mod.bind_fast_plan(ctypes.cast(plan, ctypes.c_void_p).value)
+                        frs = getattr(lib, "mp4x_ipc_fast_rs", None)
+                        if frs is not None and hasattr(mod, "bind_fast_rs"):
+                            mod.bind_fast_rs(ctypes.cast(frs, ctypes.c_void_p).value)
                     except Exception:   # noqa: BLE001 — ctypes path stays
                         mod = False
                 _launch_ext = mod

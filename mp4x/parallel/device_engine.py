@@ -489,9 +489,10 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
 
     def _plan_memo(self, memo: bool, kind: str, arr, key_tail: tuple, fn) -> bool:
         """Run ``fn``, a staged copy-plan form of the default instance (the latency tier of
-        broadcast / gather / scatter / all-gather).  With ``memo`` (the public API's full path),
-        a call that ran exactly ONE host-epoch copy plan reading / writing only ``arr`` is
-        memoised for the API's fast path (``mp4x_ipc_fast_plan``), keyed like the allreduce memo
+        broadcast / gather / scatter / all-gather) or its fused reduce-scatter.  With ``memo``
+        (the public API's full path), a call that ran exactly ONE host-epoch launch reading /
+        writing only ``arr`` is memoised for the API's fast path (``mp4x_ipc_fast_plan`` /
+        ``mp4x_ipc_fast_rs``), keyed like the allreduce memo
         (shape, device, the tensor's address only while something is registered) plus
         ``key_tail`` (ranges, root).  Anything else (a temporary for an unaligned tensor, several
         launches, device epochs) is not memoised."""
@@ -506,16 +507,17 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             ok = fn()
         finally:
             inst._plan_sink = None
-        if not ok or len(sink) != 1 or sink[0][9] is not None or capturing_now():
+        if not ok or len(sink) != 1 or sink[0][-1] is not None or capturing_now():
             return ok
-        sa, ns, pa, npl, src, out, grid_len, buf_vecs, blocks, _ = sink[0]
+        rec = sink[0]
+        src, out = (rec[5], rec[6])
         base = arr.data_ptr()
         end = base + arr.numel() * arr.element_size()
         if any(x is not None and not base <= x < end for x in (src, out)):
             return ok
         from ..ops import native
         lx = native.launch_ext()
-        if lx is None or not hasattr(lx, "fast_plan"):
+        if lx is None or not hasattr(lx, "fast_plan" if rec[0] == "plan" else "fast_rs"):
             return ok
         state = inst.fast_state(self._fast_words())
         if state is None:
@@ -523,9 +525,15 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         key = (kind, base if fa.by_ptr else 0, arr.get_device(), arr.numel(), arr.dtype) + key_tail
         if len(fa) >= self._FAST_MAX:
             fa.clear()
-        fa[key] = (state, ctypes.addressof(sa), ns, ctypes.addressof(pa), npl,
-                   src - base if src is not None else -1, out - base if out is not None else -1,
-                   grid_len, buf_vecs, blocks, kind + ".ipc", kind + "Array", inst, sa, pa)
+        so, oo = (src - base if src is not None else -1), (out - base if out is not None else -1)
+        if rec[0] == "plan":
+            _, sa, ns, pa, npl, _, _, grid_len, buf_vecs, blocks, _ = rec
+            fa[key] = (state, ctypes.addressof(sa), ns, ctypes.addressof(pa), npl, so, oo, grid_len, buf_vecs,
+                       blocks, kind + ".ipc", kind + "Array", inst, sa, pa)
+        else:                                       # "rs": the fused reduce-scatter
+            _, dt, code, lo_a, hi_a, _, _, blocks, _ = rec
+            fa[key] = (state, dt, code, ctypes.addressof(lo_a), ctypes.addressof(hi_a), so, oo, blocks,
+                       kind + ".ipc", "reduceScatterArray", inst, lo_a, hi_a)
         return ok
 
     def _probe_spin(self, inst) -> None:
@@ -1260,7 +1268,9 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             torch.cuda.synchronize(self.device)
 
     # ================================================================== reduce-scatter
-    def reduce_scatter(self, arr: torch.Tensor, froms, tos, operator, operand=None):
+    def reduce_scatter(self, arr: torch.Tensor, froms, tos, operator, operand=None, memo=None):
+        """``memo``: the public API's key tail for this call shape (``(frm, counts, operator,
+        codec, compress)``) — memoise the fused IPC reduce-scatter it runs for the API's fast path."""
         flat = self._flat(arr)
         r = self.rank
         base = froms[0]
@@ -1277,7 +1287,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             self._count("reduce_scatter.ipc_zc")       # registered tensor: zero copy, any size
             return arr
         if algo in ("rccl", "a2a") and self._ipc_direct_ok(op, whole):
-            if self._ipc_obj.reduce_scatter(flat, froms, tos, op):
+            if self._plan_memo(memo is not None, "reduce_scatter", arr, memo or (),
+                               lambda: self._ipc_obj.reduce_scatter(flat, froms, tos, op)):
                 self._count("reduce_scatter.ipc")
                 return arr
         if algo in ("rccl", "a2a"):

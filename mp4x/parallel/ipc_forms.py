@@ -354,10 +354,12 @@ class IpcForms:
             lo_a = (c_int64 * self.p)(*[(f - base) * es // 16 for f in froms])
             hi_a = (c_int64 * self.p)(*[(t - base) * es // 16 for t in tos])
             maxv = max(h - l_ for l_, h in zip(lo_a, hi_a))
-            check(self.lib.mp4x_ipc_reduce_scatter_from(int(dtype_of_torch(view.dtype)), int(op.code),
-                                                        self._pp_data[0], self._pp_sig[0], r, self.p, lo_a, hi_a,
-                                                        b16, b16 + mine_off, self.epoch,
-                                                        self._grid(maxv, "rs", view.dtype, op), edev, st),
+            dt, blocks = int(dtype_of_torch(view.dtype)), self._grid(maxv, "rs", view.dtype, op)
+            sink = self._plan_sink
+            if sink is not None:
+                sink.append(("rs", dt, int(op.code), lo_a, hi_a, b16, b16 + mine_off, blocks, edev))
+            check(self.lib.mp4x_ipc_reduce_scatter_from(dt, int(op.code), self._pp_data[0], self._pp_sig[0], r, self.p,
+                                                        lo_a, hi_a, b16, b16 + mine_off, self.epoch, blocks, edev, st),
                   "mp4x_ipc_reduce_scatter_from")
             if tmp is not None and tos[r] > froms[r]:
                 flat[froms[r]:tos[r]].view(torch.uint8).copy_(tmp[mine_off:(tos[r] - base) * es])
@@ -437,7 +439,8 @@ class IpcForms:
         blocks = self._grid(grid_len)
         sink = self._plan_sink
         if sink is not None:
-            sink.append((sa, len(stage), pa, len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, blocks, edev))
+            sink.append(("plan", sa, len(stage), pa, len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, blocks,
+                         edev))
         check(self.lib.mp4x_ipc_copy_plan(self._pp_data[0], self._pp_sig[0], self.rank, self.p, sa, len(stage), pa,
                                           len(pull), src_ptr, out_ptr, grid_len, self.nbytes // 16, self.epoch,
                                           blocks, edev, st), "mp4x_ipc_copy_plan")

@@ -115,6 +115,7 @@ class ProcessCommSlave:
         self._device_engine = None
         self._fast_ar = None       # the device engine's latency memo (allreduceArray fast path)
         self._fast_pl = None       # its copy-plan launcher (broadcast / gather / scatter / allgather)
+        self._fast_rs = None       # its fused reduce-scatter launcher
         self._device_index = device
         self._shm = None
         LOG.info("master host:%s, master port:%s", masterHost, masterPort)
@@ -299,6 +300,7 @@ class ProcessCommSlave:
         import torch
         self._fast_lx = lx.fast_allreduce
         self._fast_pl = getattr(lx, "fast_plan", None)
+        self._fast_rs = getattr(lx, "fast_rs", None)
         self._fast_stream = native.stream_ptr
         self._fast_tensor = torch.Tensor
         self._fast_calls = self.stats["calls"]
@@ -623,6 +625,21 @@ class ProcessCommSlave:
 
     # ================================================================ reduce-scatter
     def reduceScatterArray(self, arrData, operand: Operand, operator, frm: int, counts: Sequence[int]):
+        fast = self._fast_ar
+        tail = None
+        if fast is not None and type(counts) is list:
+            tail = (frm, tuple(counts), operator, operand.codec, operand.compress)
+            if fast and self._fast_rs is not None and type(arrData) is self._fast_tensor and arrData.is_cuda and \
+                    arrData.is_contiguous():
+                base = arrData.data_ptr()
+                try:
+                    ent = fast.get(("reduce_scatter", base if fast.by_ptr else 0, arrData.get_device(),
+                                    arrData.numel(), arrData.dtype) + tail)
+                except TypeError:
+                    ent = tail = None
+                if ent is not None and self._fast_rs(ent, self._fast_stream(), base) == 0:
+                    self._fast_after(ent[8], ent[9])
+                    return arrData
         self._tick("reduceScatterArray")
         self._check_len(counts, "counts")
         if self.slaveNum == 1:
@@ -631,7 +648,7 @@ class ProcessCommSlave:
         froms = CommUtils.getFromsFromCount(frm, counts, self.slaveNum)
         tos = CommUtils.getTosFromCount(frm, counts, self.slaveNum)
         if _is_device_tensor(arrData):
-            return self.device.reduce_scatter(arrData, froms, tos, operator, operand)
+            return self.device.reduce_scatter(arrData, froms, tos, operator, operand, memo=tail)
         buf = _host_view(arrData, operand)
         shm = self._shm_engine(buf, operand, operator, tos[-1] - froms[0])
         if shm is not None and buf.flags.c_contiguous:

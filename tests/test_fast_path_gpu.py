@@ -141,6 +141,24 @@ def _fast_fn(comm):
         plan_bad["allgather"] = plan_bad.get("allgather", 0) + sum(
             int((w[fr[j]:to[j]] != float(j - k)).sum()) for j in range(p))
     comm._fast_pl = orig_pl
+    rs_rc = []
+    orig_rs = comm._fast_rs
+
+    def spy_rs(*a):
+        rc = orig_rs(*a)
+        rs_rc.append(rc)
+        return rc
+    comm._fast_rs = spy_rs
+    counts = [t - f for f, t in zip(fr, to)]
+    rs_bad = 0
+    for k in range(6):
+        w = _pat(n, r, k)
+        comm.reduceScatterArray(w, F, SUM, 0, counts)
+        torch.cuda.synchronize()
+        rs_bad += int((w[fr[r]:to[r]] != _exp(n, p, k)[fr[r]:to[r]]).sum())
+    comm._fast_rs = orig_rs
+    fresh.update(rs_bad=rs_bad, rs_launched=rs_rc.count(0), rs_calls=comm.stats["calls"].get("reduceScatterArray", 0),
+                 rs_eng=eng.stats.get("reduce_scatter.ipc", 0))
     api_calls = comm.stats["calls"]
     fresh.update(plan_bad=plan_bad, plan_launched=plan_rc.count(0), plan_refused=len(plan_rc) - plan_rc.count(0),
                  plan_calls={k: api_calls.get(k + "Array", 0) for k in ("broadcast", "gather", "scatter", "allgather")},
@@ -190,3 +208,4 @@ def test_fast_path_is_exact_counted_invalidated_and_fail_stop():
         assert f["plan_launched"] >= 20 and f["plan_refused"] == 0, f      # 4 ops x 6 calls, first ones memoise
         assert all(v == 6 for v in f["plan_calls"].values()), f
         assert all(v == 6 for v in f["plan_eng"].values()), f
+        assert f["rs_bad"] == 0 and f["rs_launched"] >= 5 and f["rs_calls"] == 6 and f["rs_eng"] == 6, f
