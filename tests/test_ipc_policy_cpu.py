@@ -357,6 +357,9 @@ def test_fast_path_memo_only_from_the_public_api(monkeypatch):
     from mp4x.parallel import process_comm
     from mp4x.parallel.device_engine import DeviceEngine
     assert inspect.signature(DeviceEngine.allreduce.__wrapped__).parameters["memo"].default is False
+    for name in ("reduce", "broadcast", "gather", "scatter", "allgather"):
+        assert inspect.signature(getattr(DeviceEngine, name).__wrapped__).parameters["memo"].default is False, name
+    assert inspect.signature(DeviceEngine.reduce_scatter.__wrapped__).parameters["memo"].default is None
     src = inspect.getsource(process_comm.ProcessCommSlave.allreduceArray)
     assert "memo=" in src and "self._fast_lx(ent, self._fast_stream(), base)" in src
 
