@@ -170,8 +170,11 @@ struct FastAr {
   int64_t slot_base, slot_vecs;   // the double-buffered slots of the one- / two-shot (0: none)
 };
 
-extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int op, void* buf, int64_t nbytes,
-                                       int blocks, float scale, void* stream) {
+namespace {
+// The checks every fast path makes before anything moves: an earlier collective of any of the
+// engine's instances timed out (fail the call: MP4X_E_FAILED_EARLIER), or the stream is being
+// captured (the device-epoch form is needed: MP4X_E_CAPTURING).  0 = go.
+int fast_prologue(const FastAr* s, void* stream) {
   for (int i = 0; i < 8 && s->herr[i]; ++i)
     if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -179,7 +182,13 @@ extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int
     (void)hipGetLastError();
     return MP4X_E_CAPTURING;
   }
-  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  return cs != hipStreamCaptureStatusNone ? MP4X_E_CAPTURING : 0;
+}
+}  // namespace
+
+extern "C" int mp4x_ipc_fast_allreduce(const FastAr* s, int algo, int dtype, int op, void* buf, int64_t nbytes,
+                                       int blocks, float scale, void* stream) {
+  if (int e = fast_prologue(s, stream)) return e;
   // everything mp4x_ipc_allreduce_ex2 could refuse is refused HERE, before the epoch moves (a
   // refused call must leave this rank's epoch where its peers expect it): the full path runs it
   if (((uintptr_t)buf & 15) || (nbytes & 15) || nbytes <= 0) return MP4X_E_BADARG;
@@ -203,14 +212,7 @@ extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_pt
 extern "C" int mp4x_ipc_fast_plan(const FastAr* s, const int64_t* stage, int nstage, const int64_t* pull, int npull,
                                   int64_t src_off, int64_t out_off, void* base, int64_t grid_len, int64_t buf_vecs,
                                   int blocks, void* stream) {
-  for (int i = 0; i < 8 && s->herr[i]; ++i)
-    if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
-    (void)hipGetLastError();
-    return MP4X_E_CAPTURING;
-  }
-  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  if (int e = fast_prologue(s, stream)) return e;
   char* b = static_cast<char*>(base);
   const void* src = src_off >= 0 ? b + src_off : nullptr;
   void* out = out_off >= 0 ? b + out_off : nullptr;
@@ -231,14 +233,7 @@ extern "C" int mp4x_ipc_reduce_scatter_from(int dtype, int op, void* const* data
 // bounds in 16-byte vectors from the range start; src_off / out_off: byte offsets from `base`.
 extern "C" int mp4x_ipc_fast_rs(const FastAr* s, int dtype, int op, const int64_t* seg_lo, const int64_t* seg_hi,
                                 int64_t src_off, int64_t out_off, void* base, int blocks, void* stream) {
-  for (int i = 0; i < 8 && s->herr[i]; ++i)
-    if (__atomic_load_n(s->herr[i], __ATOMIC_RELAXED)) return MP4X_E_FAILED_EARLIER;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing((hipStream_t)stream, &cs) != hipSuccess) {
-    (void)hipGetLastError();
-    return MP4X_E_CAPTURING;
-  }
-  if (cs != hipStreamCaptureStatusNone) return MP4X_E_CAPTURING;
+  if (int e = fast_prologue(s, stream)) return e;
   char* b = static_cast<char*>(base);
   if (!b || src_off < 0 || out_off < 0 || ((uintptr_t)(b + src_off) & 15) || ((uintptr_t)(b + out_off) & 15))
     return MP4X_E_BADARG;
