@@ -28,7 +28,7 @@ from __future__ import annotations
 import struct
 import zlib
 from collections.abc import ItemsView, MutableMapping, ValuesView
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 

@@ -17,7 +17,6 @@ import contextlib
 import ctypes
 import logging
 import os
-import socket
 from typing import List, Optional
 
 import torch
