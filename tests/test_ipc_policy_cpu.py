@@ -446,3 +446,52 @@ def test_registered_tensors_keep_zero_copy_above_the_latency_tier_at_two_ranks(m
     for t in (reg, torch.zeros((1 << 20) // 4), torch.zeros((64 << 10) // 4)):
         e.allreduce(t, 0, t.numel(), SUM, F)
     assert ran == ["ipc2z", "ipc1", "ipc1"], ran
+
+
+def test_plan_memo_records_only_one_host_epoch_launch_on_the_callers_tensor(monkeypatch):
+    """DeviceEngine._plan_memo memoises a copy-plan / reduce-scatter call for the API fast path only
+    when it made exactly ONE host-epoch launch that reads / writes nothing but the caller's tensor
+    (a temporary for an unaligned tensor, several launches or device epochs are not replayable)."""
+    import ctypes
+    from mp4x.parallel.device_engine import _FastMemo
+    from mp4x.ops import native
+    e = _engine()
+    e._fast_ar = _FastMemo()
+    e._probe_depth = 0
+    e._ipc_large = e._ipc_fp8_big = e._hier = None
+
+    class _Inst:
+        _plan_sink = None
+        _herr = ctypes.c_void_p()
+
+        def fast_state(self, words):
+            return 4242
+    inst = e._ipc_obj = _Inst()
+    monkeypatch.setattr(native, "launch_ext", lambda: type("L", (), {"fast_plan": 1, "fast_rs": 1})())
+    monkeypatch.setattr("mp4x.parallel.device_engine.capturing_now", lambda: False)
+    arr = torch.zeros(1024)
+    base, end = arr.data_ptr(), arr.data_ptr() + 4096
+    sa = (ctypes.c_int64 * 4)()
+
+    def plan(*recs):
+        def fn():
+            for src, out, edev in recs:
+                if inst._plan_sink is not None:        # (what IpcForms._plan does)
+                    inst._plan_sink.append(("plan", sa, 1, sa, 0, src, out, 64, 1 << 16, 8, edev))
+            return True
+        return fn
+    cases = [((plan((base, None, None)),), True), ((plan((None, base + 2048, None)),), True),
+             ((plan((base - 4096, None, None)),), False), ((plan((base, end, None)),), False),
+             ((plan((base, None, None), (None, base, None)),), False), ((plan((base, None, 99)),), False)]
+    for (fn,), want in cases:
+        e._fast_ar.clear()
+        assert e._plan_memo(True, "broadcast", arr, (0, 1024, 1), fn) is True
+        assert (len(e._fast_ar) == 1) is want, (want, dict(e._fast_ar))
+        assert inst._plan_sink is None
+    e._fast_ar.clear()
+    assert e._plan_memo(False, "broadcast", arr, (0, 1024, 1), plan((base, None, None))) is True
+    assert not e._fast_ar                                     # engine-internal callers never memoise
+    e._plan_memo(True, "broadcast", arr, (0, 1024, 1), plan((base, None, None)))
+    (key, ent), = e._fast_ar.items()
+    assert key == ("broadcast", 0, arr.get_device(), 1024, torch.float32, 0, 1024, 1)
+    assert ent[0] == 4242 and ent[5] == 0 and ent[6] == -1 and ent[10:12] == ("broadcast.ipc", "broadcastArray")
