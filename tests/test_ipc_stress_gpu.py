@@ -9,6 +9,7 @@ exist for).  Every result is checked exactly (integers, small-integer floats) ag
 recomputation; the barrier error word must stay 0.
 """
 import multiprocessing as mp
+import os
 import tempfile
 import traceback
 
@@ -18,7 +19,8 @@ torch = pytest.importorskip("torch")
 
 pytestmark = pytest.mark.gpu
 
-ITERS = 120
+ITERS = int(os.environ.get("MP4X_TEST_SOAK_ITERS", 120))      # a longer soak on demand
+SEEDS = [int(x) for x in os.environ.get("MP4X_TEST_SOAK_SEEDS", "1,2").split(",")]
 
 
 def _worker(port, q, seed):
@@ -78,7 +80,7 @@ def _worker(port, q, seed):
         q.put((-1, "err", traceback.format_exc()))
 
 
-@pytest.mark.parametrize("p,seed", [(4, 1), (8, 2)])
+@pytest.mark.parametrize("p,seed", [(4, SEEDS[0]), (8, SEEDS[-1])])
 def test_ipc_protocol_random_soak(p, seed):
     from mp4x import CommMaster
     m = CommMaster(p, 0, host="127.0.0.1", exit_on_timeout=False, workdir=tempfile.mkdtemp()).start()
