@@ -35,6 +35,7 @@ remainder in allreduce/reduce splits, rank-order reductions) — see process_com
 """
 from __future__ import annotations
 
+import bisect
 import contextlib
 import ctypes
 import datetime
@@ -130,14 +131,34 @@ def local_reduce(out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: i
 
 
 class _FastMemo(dict):
-    """The allreduceArray latency fast path's memo (call shape -> native launch entry).
-    ``by_ptr``: keys carry the tensor's address (some tensor is registered) or 0 (none is: the
-    staged launch of a shape does not depend on where the tensor lives)."""
-    __slots__ = ("by_ptr",)
+    """The latency fast paths' memo (call shape -> native launch entry).  Keys carry the tensor's
+    address only when the tensor overlaps a registered tensor of the default IPC instance (a
+    call on it, or on a [from, to) range of it, may take the zero-copy kernels), 0 otherwise:
+    the staged launch of a shape does not depend on where an unregistered tensor lives.
+    ``reg_starts`` / ``reg_ends``: the registered ranges, sorted and disjoint (refreshed at every
+    invalidation — registration changes invalidate)."""
+    __slots__ = ("reg_starts", "reg_ends")
 
     def __init__(self):
         super().__init__()
-        self.by_ptr = False
+        self.reg_starts: list = []
+        self.reg_ends: list = []
+
+    @property
+    def by_ptr(self) -> bool:
+        """Is any tensor registered (then registered addresses key their own entries)?"""
+        return bool(self.reg_starts)
+
+    def addr_key(self, base: int, nbytes: int) -> int:
+        """The address part of a key: ``base`` when [base, base + nbytes) overlaps a registered
+        range, else 0 (the last range starting inside or before the tensor decides: the ranges
+        are disjoint)."""
+        s = self.reg_starts
+        if not s:
+            return 0
+        i = bisect.bisect_right(s, base + nbytes - 1) - 1
+        return base if i >= 0 and self.reg_ends[i] > base else 0
+
 
 class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
     # (class defaults: engines assembled without __init__ in unit tests see one node, no hier)
@@ -438,7 +459,9 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         fa.clear()
         if isinstance(fa, _FastMemo):
             inst = self.__dict__.get("_ipc_obj")
-            fa.by_ptr = bool(getattr(inst, "_regs", None))
+            rng = sorted((int(a), int(a) + int(n)) for a, n in (getattr(inst, "_regs", None) or {}))
+            fa.reg_starts = [a for a, _ in rng]
+            fa.reg_ends = [b for _, b in rng]
 
     _FAST_MAX = 256
 
@@ -469,7 +492,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         a = ONESHOT if algo == "ipc1" else TWOSHOT
         from ..operators import dtype_of_torch
         base = arr.data_ptr()
-        key = (base if getattr(fa, "by_ptr", True) else 0, arr.get_device(), arr.numel(), frm, to, arr.dtype,
+        key = (fa.addr_key(base, arr.numel() * arr.element_size()) if isinstance(fa, _FastMemo) else base,
+               arr.get_device(), arr.numel(), frm, to, arr.dtype,
                operator, getattr(operand, "codec", None), getattr(operand, "compress", False), scale)
         if kind != "allreduce":
             key = (kind,) + key
@@ -522,7 +546,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         state = inst.fast_state(self._fast_words())
         if state is None:
             return ok
-        key = (kind, base if fa.by_ptr else 0, arr.get_device(), arr.numel(), arr.dtype) + key_tail
+        key = (kind, fa.addr_key(base, end - base), arr.get_device(), arr.numel(), arr.dtype) + key_tail
         if len(fa) >= self._FAST_MAX:
             fa.clear()
         so, oo = (src - base if src is not None else -1), (out - base if out is not None else -1)

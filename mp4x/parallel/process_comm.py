@@ -295,7 +295,7 @@ class ProcessCommSlave:
                 or getattr(eng.device, "type", None) != "cuda":
             return
         lx = native.launch_ext()
-        if lx is None or not hasattr(lx, "fast_allreduce") or getattr(eng._fast_ar, "by_ptr", None) is None:
+        if lx is None or not hasattr(lx, "fast_allreduce") or not hasattr(eng._fast_ar, "addr_key"):
             return
         import torch
         self._fast_lx = lx.fast_allreduce
@@ -328,9 +328,9 @@ class ProcessCommSlave:
                 not arrData.is_contiguous():
             return False
         fast = self._fast_ar
-        base = arrData.data_ptr()
+        base, n = arrData.data_ptr(), arrData.numel()
         try:
-            ent = fast.get((kind, base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(),
+            ent = fast.get((kind, fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n,
                             arrData.dtype) + tail)
         except TypeError:               # unhashable ranges (e.g. arrays): the full path
             return False
@@ -631,10 +631,10 @@ class ProcessCommSlave:
             tail = (frm, tuple(counts), operator, operand.codec, operand.compress)
             if fast and self._fast_rs is not None and type(arrData) is self._fast_tensor and arrData.is_cuda and \
                     arrData.is_contiguous():
-                base = arrData.data_ptr()
+                base, n = arrData.data_ptr(), arrData.numel()
                 try:
-                    ent = fast.get(("reduce_scatter", base if fast.by_ptr else 0, arrData.get_device(),
-                                    arrData.numel(), arrData.dtype) + tail)
+                    ent = fast.get(("reduce_scatter", fast.addr_key(base, n * arrData.element_size()),
+                                    arrData.get_device(), n, arrData.dtype) + tail)
                 except TypeError:
                     ent = tail = None
                 if ent is not None and self._fast_rs(ent, self._fast_stream(), base) == 0:
@@ -683,9 +683,9 @@ class ProcessCommSlave:
                 0 <= rootRank < self.slaveNum:
             # the latency tier of a reduce is the staged IPC allreduce (every rank gets the sum;
             # non-root results are unspecified by contract): the same native launch
-            base = arrData.data_ptr()
-            ent = fast.get(("reduce", base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
-                            arrData.dtype, operator, operand.codec, operand.compress, 1.0))
+            base, n = arrData.data_ptr(), arrData.numel()
+            ent = fast.get(("reduce", fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm,
+                            to, arrData.dtype, operator, operand.codec, operand.compress, 1.0))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
                 self._fast_after(ent[8], ent[10])
                 return arrData
@@ -880,8 +880,8 @@ class ProcessCommSlave:
         """
         fast = self._fast_ar
         if fast and out is None and type(arrData) is self._fast_tensor and arrData.is_cuda and arrData.is_contiguous():
-            base = arrData.data_ptr()
-            ent = fast.get((base if fast.by_ptr else 0, arrData.get_device(), arrData.numel(), frm, to,
+            base, n = arrData.data_ptr(), arrData.numel()
+            ent = fast.get((fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm, to,
                             arrData.dtype, operator, operand.codec, operand.compress, scale))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
                 self._fast_after(ent[8], ent[10])

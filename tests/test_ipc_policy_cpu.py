@@ -337,9 +337,14 @@ def test_latency_fast_path_memo_is_invalidated_by_every_decision_input():
     inst._regs = {}
     inst._changed()
     assert e._fast_ar.by_ptr is False
-    inst._regs = {(4096, 1 << 20): object()}
+    inst._regs = {(4096, 1 << 20): object(), (1 << 30, 4096): object()}
     inst._changed()
     assert e._fast_ar.by_ptr is True
+    ak = e._fast_ar.addr_key
+    assert ak(4096, 16) == 4096 and ak(8192, 64) == 8192                # inside a registered tensor
+    assert ak(4000, 200) == 4000                                         # overlaps one (a [from, to) inside it)
+    assert ak(0, 4096) == 0 and ak(4096 + (1 << 20), 64) == 0            # adjacent, not overlapping
+    assert ak((1 << 30) - 64, 128) == (1 << 30) - 64 and ak((1 << 30) + 4096, 16) == 0
     inst._regs = {}
     inst._changed()
     assert e._fast_ar.by_ptr is False
