@@ -167,9 +167,10 @@ __host__ __device__ __forceinline__ uint32_t next_epoch(uint32_t e) {
 }
 
 // `which`: 0 start, 1 mid, 2 end.  At the START barrier a peer may already be ONE call ahead: the
-// double-buffered one-shot (k_ipc_oneshot with slots) has no end barrier, so a peer that finished
-// call e can store call e+1's start flag before this rank saw its flag of call e.  Every other
-// kernel ends with an end barrier, so a peer is never further ahead; a start flag holding the next
+// slotted one- and two-shot (k_ipc_oneshot / k_ipc_twoshot with slots) have no end barrier, so a
+// peer that finished call e can store call e+1's start flag before this rank saw its flag of call
+// e.  It can get no further (call e+1's start barrier needs this rank's arrival), and never ahead
+// at a mid barrier; every other kernel ends with an end barrier.  A start flag holding the next
 // epoch (any protocol tag) therefore means "arrived, and done with call e".
 __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int rank, int p, uint32_t epoch,
                                               Signal* self) {
