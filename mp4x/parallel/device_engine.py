@@ -42,7 +42,7 @@ import datetime
 import logging
 import os
 import time
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, NamedTuple, Optional, Sequence
 
 import torch
 import torch.distributed as dist
@@ -128,6 +128,58 @@ def local_reduce(out: torch.Tensor, inputs: Sequence[torch.Tensor], f: int, t: i
     reduce_into(o, ins, op)
     return out
 
+
+
+class _ArEntry(NamedTuple):
+    """A memoised staged allreduce (also a reduce's): the field order is what
+    ``_mp4x_launch.fast_allreduce`` reads (csrc/pyext/launch_ext.cpp)."""
+    state: int          # FastAr address (IpcAllreduce.fast_state)
+    algo: int
+    dtype: int
+    op: int
+    offset: int         # byte offset of the [from, to) range in the tensor
+    nbytes: int
+    blocks: int
+    scale: float
+    stat: str           # the engine's call count it bumps ("allreduce.ipc1", ...)
+    inst: object        # keeps the instance alive with the entry
+    api: str            # the API call count it bumps ("allreduceArray", ...)
+
+
+class _PlanEntry(NamedTuple):
+    """A memoised copy plan (``_mp4x_launch.fast_plan``)."""
+    state: int
+    stage: int          # address of the stage quadruples (sa)
+    nstage: int
+    pull: int           # address of the pull quadruples (pa)
+    npull: int
+    src_off: int        # byte offsets from the tensor's address, -1 = none
+    out_off: int
+    grid_len: int
+    buf_vecs: int
+    blocks: int
+    stat: str
+    api: str
+    inst: object
+    sa: object          # the ctypes arrays behind stage / pull, kept alive
+    pa: object
+
+
+class _RsEntry(NamedTuple):
+    """A memoised fused reduce-scatter (``_mp4x_launch.fast_rs``)."""
+    state: int
+    dtype: int
+    op: int
+    seg_lo: int         # addresses of the p segment bounds (16-byte vectors)
+    seg_hi: int
+    src_off: int
+    out_off: int
+    blocks: int
+    stat: str
+    api: str
+    inst: object
+    lo_arr: object
+    hi_arr: object
 
 
 class _FastMemo(dict):
@@ -501,9 +553,9 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             fa.clear()
         # the buffer as an offset from the tensor's address: the call passes its tensor's address
         # (an unaligned one is refused natively before anything is launched: the full path runs)
-        fa[key] = (state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr - base, total,
-                   inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
-                   kind + "." + algo, inst, kind + "Array")
+        fa[key] = _ArEntry(state, a, int(dtype_of_torch(view.dtype)), int(op.code), ptr - base, total,
+                           inst.latency_blocks(total, a, view.dtype, op), self._fused_scale(scale, view),
+                           kind + "." + algo, inst, kind + "Array")
 
     def _fast_words(self) -> list:
         """The pinned host error words of every IPC instance (the fast paths' fail-stop check)."""
@@ -552,12 +604,12 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         so, oo = (src - base if src is not None else -1), (out - base if out is not None else -1)
         if rec[0] == "plan":
             _, sa, ns, pa, npl, _, _, grid_len, buf_vecs, blocks, _ = rec
-            fa[key] = (state, ctypes.addressof(sa), ns, ctypes.addressof(pa), npl, so, oo, grid_len, buf_vecs,
-                       blocks, kind + ".ipc", kind + "Array", inst, sa, pa)
+            fa[key] = _PlanEntry(state, ctypes.addressof(sa), ns, ctypes.addressof(pa), npl, so, oo, grid_len,
+                                 buf_vecs, blocks, kind + ".ipc", kind + "Array", inst, sa, pa)
         else:                                       # "rs": the fused reduce-scatter
             _, dt, code, lo_a, hi_a, _, _, blocks, _ = rec
-            fa[key] = (state, dt, code, ctypes.addressof(lo_a), ctypes.addressof(hi_a), so, oo, blocks,
-                       kind + ".ipc", "reduceScatterArray", inst, lo_a, hi_a)
+            fa[key] = _RsEntry(state, dt, code, ctypes.addressof(lo_a), ctypes.addressof(hi_a), so, oo, blocks,
+                               kind + ".ipc", "reduceScatterArray", inst, lo_a, hi_a)
         return ok
 
     def _probe_spin(self, inst) -> None:

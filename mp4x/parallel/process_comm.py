@@ -336,7 +336,7 @@ class ProcessCommSlave:
             return False
         if ent is None or self._fast_pl(ent, self._fast_stream(), base) != 0:
             return False
-        self._fast_after(ent[10], ent[11])
+        self._fast_after(ent.stat, ent.api)
         return True
 
     def registerBuffer(self, tensor) -> bool:
@@ -638,7 +638,7 @@ class ProcessCommSlave:
                 except TypeError:
                     ent = tail = None
                 if ent is not None and self._fast_rs(ent, self._fast_stream(), base) == 0:
-                    self._fast_after(ent[8], ent[9])
+                    self._fast_after(ent.stat, ent.api)
                     return arrData
         self._tick("reduceScatterArray")
         self._check_len(counts, "counts")
@@ -687,7 +687,7 @@ class ProcessCommSlave:
             ent = fast.get(("reduce", fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm,
                             to, arrData.dtype, operator, operand.codec, operand.compress, 1.0))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
-                self._fast_after(ent[8], ent[10])
+                self._fast_after(ent.stat, ent.api)
                 return arrData
         self._tick("reduceArray")
         if self.slaveNum == 1:
@@ -884,7 +884,7 @@ class ProcessCommSlave:
             ent = fast.get((fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm, to,
                             arrData.dtype, operator, operand.codec, operand.compress, scale))
             if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
-                self._fast_after(ent[8], ent[10])
+                self._fast_after(ent.stat, ent.api)
                 return arrData
             # not memoised, or not launched (rc 1003: an earlier collective failed; 1004: the stream
             # is being captured; an unaligned buffer): the full path decides, raises or records

@@ -499,4 +499,6 @@ def test_plan_memo_records_only_one_host_epoch_launch_on_the_callers_tensor(monk
     e._plan_memo(True, "broadcast", arr, (0, 1024, 1), plan((base, None, None)))
     (key, ent), = e._fast_ar.items()
     assert key == ("broadcast", 0, arr.get_device(), 1024, torch.float32, 0, 1024, 1)
-    assert ent[0] == 4242 and ent[5] == 0 and ent[6] == -1 and ent[10:12] == ("broadcast.ipc", "broadcastArray")
+    assert ent.state == 4242 and ent.src_off == 0 and ent.out_off == -1
+    assert (ent.stat, ent.api) == ("broadcast.ipc", "broadcastArray")
+    assert isinstance(ent, tuple) and ent[0] == 4242          # (positional: what the native launcher reads)
