@@ -48,3 +48,47 @@ def _check(mod, seen):
     assert seen[1][15:] == (1 << 22, 1 << 15)
     with pytest.raises(TypeError):
         mod.allreduce_ex(1, 2, 3)
+
+
+PLAN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
+                        ctypes.c_void_p)
+RS = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                      ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p)
+
+
+def test_fast_plan_and_fast_rs_marshal_the_memo_entry():
+    """fast_plan / fast_rs read the memoised entry positionally (a named tuple is a tuple) and the
+    call's stream and tensor address; a wrong shape is a TypeError, an unbound launcher raises."""
+    try:
+        mod = native._load_ext("_mp4x_launch")
+    except native.NativeUnavailable:
+        pytest.skip("_mp4x_launch not built")
+    if not hasattr(mod, "fast_plan"):
+        pytest.skip("old _mp4x_launch build")
+    from mp4x.parallel.device_engine import _PlanEntry, _RsEntry
+    seen = []
+    cbp = PLAN(lambda *a: seen.append(("plan",) + a) or 0)
+    cbr = RS(lambda *a: seen.append(("rs",) + a) or 5)
+    mod.bind_fast_plan(ctypes.cast(cbp, ctypes.c_void_p).value)
+    mod.bind_fast_rs(ctypes.cast(cbr, ctypes.c_void_p).value)
+    try:
+        pe = _PlanEntry(0x10, 0x20, 1, 0x30, 2, 0, -1, 4096, 1 << 22, 64, "broadcast.ipc", "broadcastArray",
+                        None, None, None)
+        assert mod.fast_plan(pe, 0x40, 0x5000) == 0
+        re_ = _RsEntry(0x11, 2, 3, 0x21, 0x31, 16, 32, 8, "reduce_scatter.ipc", "reduceScatterArray", None, None,
+                       None)
+        assert mod.fast_rs(re_, 0x41, 0x6000) == 5
+        p, r = seen
+        assert p == ("plan", 0x10, 0x20, 1, 0x30, 2, 0, -1, 0x5000, 4096, 1 << 22, 64, 0x40)
+        assert r == ("rs", 0x11, 2, 3, 0x21, 0x31, 16, 32, 0x6000, 8, 0x41)
+        with pytest.raises(TypeError):
+            mod.fast_plan(pe, 0x40)
+        with pytest.raises(TypeError):
+            mod.fast_rs((1, 2), 0x40, 0x6000)
+    finally:
+        mod.bind_fast_plan(0)
+        mod.bind_fast_rs(0)
+    with pytest.raises(RuntimeError):
+        mod.fast_plan(pe, 0x40, 0x5000)
+    native._launch_ext = None
