@@ -166,7 +166,7 @@ def test_zero_copy_random_soak(p, seed):
     """The zero-copy forms of all 7 collectives on one memAlloc arena, a seeded random sequence of
     ops, roots and 16-byte-grid ranges (overlapping from call to call), every result exact."""
     from spawn_ranks import run_spawn
-    iters = 60
+    iters = int(os.environ.get("MP4X_TEST_ZC_SOAK_ITERS", 60))
     out = run_spawn(p, _zc_soak_fn, args=(seed, iters), timeout=300)
     for r, (bad, zc) in out.items():
         assert not bad, (r, bad[:5])
