@@ -568,9 +568,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         broadcast / gather / scatter / all-gather) or its fused reduce-scatter.  With ``memo``
         (the public API's full path), a call that ran exactly ONE host-epoch launch reading /
         writing only ``arr`` is memoised for the API's fast path (``mp4x_ipc_fast_plan`` /
-        ``mp4x_ipc_fast_rs``), keyed like the allreduce memo
-        (shape, device, the tensor's address only while something is registered) plus
-        ``key_tail`` (ranges, root).  Anything else (a temporary for an unaligned tensor, several
+        ``mp4x_ipc_fast_rs``), keyed like the allreduce memo (shape, device; the tensor's address
+        only when it overlaps a registered tensor) plus ``key_tail`` (ranges, root).  Anything else (a temporary for an unaligned tensor, several
         launches, device epochs) is not memoised."""
         inst = self._ipc_obj
         fa = self.__dict__.get("_fast_ar")
