@@ -118,6 +118,7 @@ class ProcessCommSlave:
         self._fast_rs = None       # its fused reduce-scatter launcher
         self._device_index = device
         self._shm = None
+        self._shm_cfg = None       # (shm allowed for this job, MP4X_SHM_MIN_BYTES), read at first use
         LOG.info("master host:%s, master port:%s", masterHost, masterPort)
         self.server = MasterClient(masterHost, masterPort)
         loop = masterHost in ("127.0.0.1", "localhost", "::1")
@@ -389,20 +390,25 @@ class ProcessCommSlave:
     mem_free = memFree
 
     def _shm_engine(self, buf, operand: Operand, operator, nelems: int):
-        """The shared-memory engine when this call qualifies (decision identical on every rank)."""
-        if os.environ.get("MP4X_SHM", "1") != "1" or self.slaveNum == 1 or not operand.is_primitive \
-                or operand.compress:
+        """The shared-memory engine when this call qualifies (decision identical on every rank).
+        The job-level inputs (``MP4X_SHM``, ``MP4X_SHM_MIN_BYTES``, all ranks on one host) are
+        read once: the per-call check is a few attribute tests on the host latency path."""
+        cfg = self._shm_cfg
+        if cfg is None:
+            from .shm import same_host
+            cfg = self._shm_cfg = (os.environ.get("MP4X_SHM", "1") == "1" and self.slaveNum > 1 and
+                                   same_host(self.addresses),
+                                   int(os.environ.get("MP4X_SHM_MIN_BYTES", SHM_MIN_BYTES)))
+        if not cfg[0] or not operand.is_primitive or operand.compress:
             return None
         if not isinstance(buf, np.ndarray) or buf.dtype != operand.np_dtype:
             return None
         if operator is not None and (getattr(operator, "is_custom", False) or operator.dtype != operand.dtype):
             return None
-        if nelems * buf.itemsize < int(os.environ.get("MP4X_SHM_MIN_BYTES", SHM_MIN_BYTES)):
-            return None
-        from .shm import ShmEngine, same_host
-        if not same_host(self.addresses):
+        if nelems * buf.itemsize < cfg[1]:
             return None
         if self._shm is None:
+            from .shm import ShmEngine
             self._shm = ShmEngine(self)
         return self._shm
 
