@@ -328,9 +328,11 @@ def _tuners_fn(comm):
 def test_autotuners_with_rccl_candidates_cross_gpu(p):
     """Every tuner on real GPUs with RCCL among the candidates: each candidate's warm-up call is an
     exact probe, run twice (the second on the first's result), so a finite time means that
-    schedule was exact on every rank; inf would mean wrong / failed / timed out somewhere."""
+    schedule was exact on every rank; inf would mean wrong / failed / timed out somewhere.  The
+    opt-in schedules join (MP4X_AUTOTUNE_EXTRA=1: RCCL with pinned channel counts, the composite
+    broadcast, ...) so every schedule the tuners know is probed here."""
     _need(p)
-    out = run_spawn(p, _tuners_fn, mode="multi", timeout=600)
+    out = run_spawn(p, _tuners_fn, mode="multi", timeout=600, env={"MP4X_AUTOTUNE_EXTRA": "1"})
     want = {k.split(":")[0]: set() for ks in COVERS.values() for k in ks}
     for ks in COVERS["test_autotuners_with_rccl_candidates_cross_gpu"]:
         kind, algo = ks.split(":")
