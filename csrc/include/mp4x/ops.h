@@ -31,7 +31,10 @@ enum mp4x_op {
 enum { MP4X_E_BADARG = 1001, MP4X_E_UNSUPPORTED = 1002,
        // latency fast path (mp4x_ipc_fast_allreduce): not launched, the caller takes the full path
        MP4X_E_FAILED_EARLIER = 1003,   // an IPC collective of this engine timed out earlier
-       MP4X_E_CAPTURING = 1004 };      // the stream is being captured into a hipGraph
+       MP4X_E_CAPTURING = 1004,        // the stream is being captured into a hipGraph
+       // a communicator's launch on a second stream inside ONE graph capture (the stream-order
+       // guard cannot join a capture's forked streams: csrc/runtime/order.hip)
+       MP4X_E_STREAM_SWITCH = 1005 };
 
 #define MP4X_MAX_NIN 8
 

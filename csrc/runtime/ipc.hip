@@ -523,14 +523,31 @@ extern "C" int mp4x_memset_async(void* dst, int value, size_t bytes, void* strea
 // Copy plan (see k_ipc_copy_plan).  stage / pull: n x {src_off, dst_off, len, peer} int64
 // quadruples in 16-byte vectors; `grid_len` (vectors) must be rank-independent — the largest
 // item of any rank — so every rank launches the same grid.
+// Every refusal of mp4x_ipc_copy_plan (the latency fast path runs it before its epoch moves).
+extern "C" int mp4x_ipc_copy_plan_check(int rank, int p, const int64_t* stage, int nstage, const int64_t* pull,
+                                        int npull, const void* src, const void* out, int64_t buf_vecs) {
+  if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p) return MP4X_E_BADARG;
+  if (nstage < 0 || nstage > kIpcMaxRanks || npull < 0 || npull > kIpcMaxRanks) return MP4X_E_BADARG;
+  if ((nstage && (!src || ((uintptr_t)src & 15))) || (npull && (!out || ((uintptr_t)out & 15)))) return MP4X_E_BADARG;
+  for (int i = 0; i < nstage; ++i) {
+    const int64_t* it = stage + 4 * i;                    // {src_off, dst_off, len, -}
+    if (it[2] < 0 || it[1] < 0 || it[1] + it[2] > buf_vecs) return MP4X_E_BADARG;   // inside the own buffer
+  }
+  for (int i = 0; i < npull; ++i) {
+    const int64_t* it = pull + 4 * i;                     // {src_off, dst_off, len, peer}
+    if (it[2] < 0 || it[3] < 0 || it[3] >= p || it[0] < 0 || it[0] + it[2] > buf_vecs)
+      return MP4X_E_BADARG;                               // pulls stay inside the peer's buffer
+  }
+  return 0;
+}
+
 extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_ptrs, int rank, int p,
                                   const int64_t* stage, int nstage, const int64_t* pull, int npull, const void* src,
                                   void* out, int64_t grid_len, int64_t buf_vecs, uint32_t epoch, int blocks,
                                   const uint32_t* epoch_dev, void* stream) {
+  if (int e = mp4x_ipc_copy_plan_check(rank, p, stage, nstage, pull, npull, src, out, buf_vecs)) return e;
   IpcPtrs P;
   if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
-  if (nstage < 0 || nstage > kIpcMaxRanks || npull < 0 || npull > kIpcMaxRanks) return MP4X_E_BADARG;
-  if ((nstage && (!src || ((uintptr_t)src & 15))) || (npull && (!out || ((uintptr_t)out & 15)))) return MP4X_E_BADARG;
   CopyPlan plan;
   plan.nstage = nstage;
   plan.npull = npull;
@@ -538,12 +555,6 @@ extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_pt
     plan.stage[i] = i < nstage ? CopyItem{stage[4 * i], stage[4 * i + 1], stage[4 * i + 2], 0} : CopyItem{0, 0, 0, 0};
     plan.pull[i] = i < npull ? CopyItem{pull[4 * i], pull[4 * i + 1], pull[4 * i + 2], pull[4 * i + 3]}
                              : CopyItem{0, 0, 0, 0};
-    if (i < nstage && (plan.stage[i].len < 0 || plan.stage[i].dst_off < 0 ||
-                       plan.stage[i].dst_off + plan.stage[i].len > buf_vecs))
-      return MP4X_E_BADARG;                               // staging stays inside the own buffer
-    if (i < npull && (plan.pull[i].len < 0 || plan.pull[i].peer < 0 || plan.pull[i].peer >= p ||
-                      plan.pull[i].src_off < 0 || plan.pull[i].src_off + plan.pull[i].len > buf_vecs))
-      return MP4X_E_BADARG;                               // pulls stay inside the peer's buffer
   }
   blocks = ipc_blocks(blocks, grid_len);
   hipLaunchKernelGGL(k_ipc_copy_plan, dim3(blocks), dim3(kIpcThreads), 0, (hipStream_t)stream, P,

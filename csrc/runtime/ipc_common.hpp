@@ -127,6 +127,23 @@ __device__ __forceinline__ uint32_t dbg_flags_of(const Signal* self) {
 
 constexpr uint64_t kDefaultSpinTicks = 600ull * 100000000ull;   // 600 s at 100 MHz
 
+// The per-communicator stream-order guard (csrc/runtime/order.hip, mp4x/parallel/order.py): the
+// device-side total order of ONE communicator's collectives across the caller's streams.  Field
+// order is the ctypes layout of mp4x.parallel.order.StreamOrder.
+struct StreamOrder {
+  void* last;            // hipStream_t of the communicator's previous launch (when have_last)
+  void* ev;              // hipEvent_t, created at the first stream switch
+  void* cap_stream;      // the stream of the current graph capture's launches (when cap_have)
+  uint64_t cap_id;       // that capture's id
+  uint64_t switches;     // stream switches joined so far (statistics, tests)
+  int32_t have_last;
+  int32_t cap_have;
+  int32_t disabled;      // MP4X_TEST_NO_STREAM_ORDER=1: tests only (shows the guard has teeth)
+  int32_t pad;
+};
+// 0, or MP4X_E_STREAM_SWITCH / a HIP error: see order.hip.
+extern "C" int mp4x_order_enter(StreamOrder* o, void* stream);
+
 struct IpcPtrs {
   const void* data[kIpcMaxRanks];   // every rank's data buffer (own one included)
   Signal* sig[kIpcMaxRanks];        // every rank's signal block
@@ -166,14 +183,19 @@ __host__ __device__ __forceinline__ uint32_t next_epoch(uint32_t e) {
   return n ? n : 2u;
 }
 
-// `which`: 0 start, 1 mid, 2 end.  At the START barrier a peer may already be ONE call ahead: the
-// slotted one- and two-shot (k_ipc_oneshot / k_ipc_twoshot with slots) have no end barrier, so a
-// peer that finished call e can store call e+1's start flag before this rank saw its flag of call
-// e.  It can get no further (call e+1's start barrier needs this rank's arrival), and never ahead
-// at a mid barrier; every other kernel ends with an end barrier.  A start flag holding the next
-// epoch (any protocol tag) therefore means "arrived, and done with call e".
+// `which`: 0 start, 1 mid, 2 end.  `accept_ahead` (start barrier of the SLOTTED one- and two-shot
+// only, k_ipc_oneshot / k_ipc_twoshot with slots): a peer may already be ONE call ahead — those
+// kernels have no end barrier, so a peer that finished call e can store call e+1's start flag
+// before this rank saw its flag of call e.  It can get no further (call e+1's start barrier needs
+// this rank's arrival), and never ahead at a mid barrier.  A start flag holding the next epoch
+// therefore means "arrived, and done with call e" — with ANY protocol tag: call e+1 may
+// legitimately be a zero-copy call (a registered tensor) after a staged slotted call e.  Only a
+// kernel without an end barrier can face a peer that is ahead, so every other kernel accepts its
+// own epoch only.  Mismatch detection is one-sided in the slotted kernels: if a peer
+// runs another protocol for call e itself (registrations differ across ranks), one side sees the
+// other tag and fails at once (code 4), the other may take that peer's flag for "ahead".
 __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int rank, int p, uint32_t epoch,
-                                              Signal* self) {
+                                              Signal* self, bool accept_ahead = false) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave drains its stores
   __syncthreads();
   __shared__ int s_fail;
@@ -195,7 +217,8 @@ __device__ __forceinline__ bool block_barrier(const IpcPtrs& P, int which, int r
     // pays one uncached round trip, not two (r4 latency: +4 us per kernel when it was read first)
     uint64_t spin = 0;
     uint32_t seen;
-    const uint32_t ahead = which == 0 ? next_epoch(epoch) : 0xFFFFFFFFu;   // (low bits never all ones)
+    // (an epoch's low bits are never all ones: 0xFFFFFFFF never matches)
+    const uint32_t ahead = accept_ahead ? next_epoch(epoch) : 0xFFFFFFFFu;
     while ((seen = __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != epoch &&
            (seen & ~kTagMask) != ahead) {
       if (spin == 0) {
@@ -350,6 +373,15 @@ template <int DT, typename F> inline int with_op(int op, F&& f) {
   }
   if (!rt_op_ok<DT>(op)) return MP4X_E_UNSUPPORTED;
   return f(IntC<kOpRt>{});
+}
+
+// 0 when the IPC kernels reduce `op` over `dtype` (a hot pair or the runtime-op kernel), else
+// MP4X_E_UNSUPPORTED — the refusal with_dtype / with_op would make at launch time.
+inline int op_supported(int dtype, int op) {
+  return with_dtype(dtype, [&](auto dtc) {
+    constexpr int DT = decltype(dtc)::value;
+    return with_op<DT>(op, [](auto) { return 0; });
+  });
 }
 
 // f(IntC<NR>{}) for a rank count 2..8.

@@ -76,11 +76,22 @@ extern "C" int mp4x_ipc_reduce_scatter(int dtype, int op, void* const* data_ptrs
 // Reduce-scatter with fused staging: `src` (16-B aligned) holds this rank's whole range laid out
 // like the buffer (vector offsets seg_lo/seg_hi per rank, relative to src and to the buffer);
 // this rank's reduced segment goes straight to `out` (16-B aligned) at out[v - lo].  One launch.
+// Every refusal of mp4x_ipc_reduce_scatter_from (the latency fast path runs it before its epoch
+// moves): alignment, rank range, segment bounds, and the (dtype, op) pair.
+extern "C" int mp4x_ipc_reduce_scatter_from_check(int dtype, int op, int rank, int p, const int64_t* seg_lo,
+                                                  const int64_t* seg_hi, const void* src, const void* out) {
+  if (!src || ((uintptr_t)src & 15) || ((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p) return MP4X_E_BADARG;
+  for (int k = 0; k < p; ++k)
+    if (seg_lo[k] < 0 || seg_hi[k] < seg_lo[k]) return MP4X_E_BADARG;
+  return op_supported(dtype, op);
+}
+
 extern "C" int mp4x_ipc_reduce_scatter_from(int dtype, int op, void* const* data_ptrs, void* const* signal_ptrs,
                                             int rank, int p, const int64_t* seg_lo, const int64_t* seg_hi,
                                             const void* src, void* out, uint32_t epoch, int blocks,
                                             const uint32_t* epoch_dev, void* stream) {
-  if (!src || ((uintptr_t)src & 15) || ((uintptr_t)out & 15)) return MP4X_E_BADARG;
+  if (int e = mp4x_ipc_reduce_scatter_from_check(dtype, op, rank, p, seg_lo, seg_hi, src, out)) return e;
   IpcPtrs P;
   if (int e = ipc_prepare(data_ptrs, signal_ptrs, rank, p, &P)) return e;
   RsOpts o;
@@ -88,7 +99,6 @@ extern "C" int mp4x_ipc_reduce_scatter_from(int dtype, int op, void* const* data
   for (int k = 0; k < kIpcMaxRanks; ++k) {
     o.segs.lo[k] = k < p ? seg_lo[k] : 0;
     o.segs.hi[k] = k < p ? seg_hi[k] : 0;
-    if (k < p && (o.segs.lo[k] < 0 || o.segs.hi[k] < o.segs.lo[k])) return MP4X_E_BADARG;
   }
   const int64_t lo = o.segs.lo[rank], hi = o.segs.hi[rank];
   return launch_rs(dtype, op, P, (Signal*)signal_ptrs[rank], rank, p, lo, hi, out, epoch, epoch_dev,

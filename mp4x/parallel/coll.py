@@ -44,32 +44,51 @@ def _scale(splits, t: torch.Tensor):
 
 
 class TorchColl:
+    """``order``: the owning engine's stream-order guard (parallel/order.py).  RCCL orders a
+    communicator's collectives on its own stream after the CURRENT stream of each call; the guard
+    first joins the current stream to the stream of the communicator's previous launch (an IPC
+    kernel, or an RCCL call issued from another stream), so IPC and RCCL calls share one order."""
+    order = None
+
     def __init__(self, pg, backend: str):
         self.pg = pg
         self.backend = backend
         self.gather_into_tensor_ok = backend != "gloo"
         self.reduce_scatter_ok = backend != "gloo"
 
+    def _enter(self, t) -> None:
+        o = self.order
+        if o is not None and getattr(t, "is_cuda", False):
+            from ..ops.native import stream_ptr
+            o.enter(stream_ptr())
+
     def all_reduce(self, t, code, avg: bool = False):
         """``avg``: SUM then divide by the group size inside the collective (ncclAvg)."""
+        self._enter(t)
         dist.all_reduce(t, op=dist.ReduceOp.AVG if avg else _RCCL_OPS[code], group=self.pg)
 
     def reduce(self, t, dst, code):
+        self._enter(t)
         dist.reduce(t, dst=dst, op=_RCCL_OPS[code], group=self.pg)
 
     def broadcast(self, t, src):
+        self._enter(t)
         dist.broadcast(_mv(t), src=src, group=self.pg)
 
     def all_to_all_single(self, out, inp, out_splits=None, in_splits=None):
+        self._enter(out)
         dist.all_to_all_single(_mv(out), _mv(inp), _scale(out_splits, out), _scale(in_splits, inp), group=self.pg)
 
     def all_gather_into_tensor(self, out, inp):
+        self._enter(out)
         dist.all_gather_into_tensor(_mv(out), _mv(inp), group=self.pg)
 
     def all_gather(self, outs, t):
+        self._enter(t)
         dist.all_gather([_mv(o) for o in outs], _mv(t), group=self.pg)
 
     def reduce_scatter_tensor(self, out, inp, code):
+        self._enter(out)
         dist.reduce_scatter_tensor(out, inp, op=_RCCL_OPS[code], group=self.pg)
 
     def p2p(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
@@ -80,6 +99,7 @@ class TorchColl:
         # RCCL orders its own stream after the current one, so the production path never waits.
         gloo_dev = self.backend == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs))
         if ops:
+            self._enter((list(sends) + list(recvs))[0][0])
             if gloo_dev:
                 torch.cuda.current_stream().synchronize()
             for w in dist.batch_isend_irecv(ops):

@@ -265,6 +265,13 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 self._init_pg()
             from .coll import TorchColl
             self.coll = TorchColl(self.pg, self.backend)
+        # the communicator's stream order (parallel/order.py): every IPC launch, fast path and
+        # RCCL call of this engine runs after the previous one, whatever stream issued it
+        self.order = None
+        if self.device.type == "cuda" and coll is None:
+            from .order import CommOrder
+            self.order = CommOrder()
+            self.coll.order = self.order
         self.algo = _env_algo()
         self.a2a_bytes = int(os.environ.get("MP4X_A2A_MIN_BYTES", 0))
         # custom xGMI IPC allreduce (csrc/runtime/ipc.hip) below these sizes
@@ -437,6 +444,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             try:
                 from .ipc import IpcAllreduce
                 inst = IpcAllreduce(self.comm)
+                self._adopt(inst)
             except Exception as e:
                 LOG.warning("IPC allreduce disabled: %s", e)
                 self.ipc_enabled = False
@@ -473,6 +481,13 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         return self._ipc_obj
 
     ipc_selftest: Optional[dict] = None
+    order = None                          # (engines assembled without __init__: no stream order)
+
+    def _adopt(self, inst) -> None:
+        """A new IPC instance of this communicator joins its stream order before its first launch
+        (the self-test and first-use probe included)."""
+        if self.order is not None:
+            inst.use_order(self.order)
 
     # ------------------------------------------------------------------ fail-stop at the call boundary
     def _ipc_all(self):
@@ -776,6 +791,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             opts.config.max_ctas = ctas
             pg = dist.new_group(ranks=list(range(self.p)), backend="nccl", pg_options=opts)
             c = self._rccl_variants[ctas] = TorchColl(pg, self.backend)
+            c.order = self.order           # the same communicator order as the default RCCL calls
         return c
 
     def ipc_large(self):
@@ -786,7 +802,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             try:
                 from .ipc import IpcAllreduce
                 inst = IpcAllreduce(self.comm, nbytes=int(os.environ.get("MP4X_IPC_LARGE_BYTES", 256 << 20)),
-                                    tag="large")
+                                    tag="large", slots=False)
+                self._adopt(inst)
             except Exception as e:
                 LOG.warning("large-message IPC allreduce disabled: %s", e)
                 self._ipc_large_failed = True
@@ -1247,7 +1264,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 self._ipc_fp8_big = None
                 inst.close(collective=True)       # re-grow mid-job: ordered, every rank here
             from .ipc import IpcAllreduce
-            inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8")
+            inst = IpcAllreduce(self.comm, nbytes=-(-need // (2 << 20)) * (2 << 20), tag="fp8", slots=False)
+            self._adopt(inst)
             bad = self._probe_instance(inst, large_forms=False, fp8=True)
             if bad:
                 self._drop_instance(inst)

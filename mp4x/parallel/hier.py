@@ -175,7 +175,8 @@ class HierAllreduce:
             from .ipc import IpcAllreduce
             try:
                 self.ipc = IpcAllreduce(_GroupComm(engine.comm, self.node, share), nbytes=self.piece_bytes,
-                                        tag="hier")
+                                        tag="hier", slots=False)
+                engine._adopt(self.ipc)
             except Exception as e:   # noqa: BLE001 — agreed inside the node's mesh setup
                 LOG.warning("rank %d: intra-node IPC mesh unavailable (%s): local process group used", r, e)
                 self.ipc = None

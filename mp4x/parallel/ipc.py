@@ -131,6 +131,12 @@ _FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
 _FP8_NARROW = os.environ.get("MP4X_FP8_NARROW") == "1"    # the r1 4-byte-lane fp8 kernel (A/B)
 
 
+def staging_needs_vmm(alloc_bytes: int) -> bool:
+    """Is a staging allocation of ``alloc_bytes`` (buffer + slots) above the IPC open limit, so it
+    must be built from VMM chunks exported as dmabuf fds instead of one hipIpc allocation?"""
+    return int(alloc_bytes) > IPC_OPEN_MAX
+
+
 def next_epoch(e: int) -> int:
     """The host epoch after ``e`` (low 30 bits, never 0, wrapping to 2 so consecutive epochs always
     alternate parity): csrc/runtime/ipc_common.hpp ``next_epoch`` — the one-shot's double-buffered
@@ -199,6 +205,15 @@ def _agree(comm, rank, obj, is_bad):
     return allv, any(is_bad(x) for x in allv)
 
 
+class FastAr(ctypes.Structure):
+    """ctypes layout of the latency fast paths' per-instance state (csrc/runtime/ipc_ar.hip
+    ``FastAr``)."""
+    _fields_ = [("herr", c_void_p * 8), ("epoch", c_void_p), ("data_ptrs", c_void_p),
+                ("signal_ptrs", c_void_p), ("rank", ctypes.c_int32), ("p", ctypes.c_int32),
+                ("slot_base", ctypes.c_int64), ("slot_vecs", ctypes.c_int64), ("order", c_void_p),
+                ("own_err", c_void_p)]
+
+
 class _Reg:
     """One registered tensor on this rank: every rank's pointer to it (``peers``, own included),
     every rank's push scratch (or None), and what this rank must release at deregistration."""
@@ -217,7 +232,7 @@ class _Reg:
 
 
 class IpcAllreduce(IpcForms):
-    def __init__(self, comm, nbytes: Optional[int] = None, tag: str = "default"):
+    def __init__(self, comm, nbytes: Optional[int] = None, tag: str = "default", slots: bool = True):
         self.comm = comm
         self.rank = comm.rank
         self.p = comm.slaveNum
@@ -256,15 +271,19 @@ class IpcAllreduce(IpcForms):
             raise Mp4jException(f"IPC allreduce needs all ranks on one node (hosts: {sorted(set(hosts))})")
         self.nbytes = int(nbytes or int(os.environ.get("MP4X_IPC_BYTES", 64 << 20)))
         self.nbytes = (self.nbytes + 4095) // 4096 * 4096
-        # the two slots live above self.nbytes (nothing else stages there)
-        slot = max(SLOT_BYTES, int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))) if SLOTS_ON else 0
+        # the two slots live above self.nbytes (nothing else stages there); only the instance that
+        # serves the latency tier has them (``slots``: the large-message, fp8 and hier instances
+        # never run a slotted call)
+        slot = max(SLOT_BYTES, int(os.environ.get("MP4X_IPC_ONESHOT_MAX", 256 << 10))) if SLOTS_ON and slots else 0
         self._slot_bytes = (slot + 4095) // 4096 * 4096
         self._slot_base = self.nbytes // 16          # in 16-byte vectors
         self._slot_vecs = self._slot_bytes // 16
         alloc_bytes = self.nbytes + 2 * self._slot_bytes
         # a staging buffer above the IPC open limit is built like a memAlloc tensor (VMM chunks,
-        # dmabuf fds to the peers): rank-independent (the size is the same on every rank)
-        self._vmm_data = self.nbytes > IPC_OPEN_MAX
+        # dmabuf fds to the peers): rank-independent (the size is the same on every rank).  The
+        # limit applies to the whole ALLOCATION, slots included (nbytes just below
+        # 2 GiB plus the slots would reach the size hipIpcOpenMemHandle never returns from)
+        self._vmm_data = staging_needs_vmm(alloc_bytes)
         self._data_regions: list = []     # VMM data buffer: own region + imported peer regions
         # a local failure here (out of memory, no IPC support) must still reach the allgather
         # below: raising before it would leave the peers waiting there for this rank
@@ -413,11 +432,7 @@ class IpcAllreduce(IpcForms):
         words = tuple(int(w) for w in herr_words if w)[:8]
         st = self._fast_state
         if st is None or st[1] != words:
-            class _FastAr(ctypes.Structure):
-                _fields_ = [("herr", c_void_p * 8), ("epoch", c_void_p), ("data_ptrs", c_void_p),
-                            ("signal_ptrs", c_void_p), ("rank", ctypes.c_int32), ("p", ctypes.c_int32),
-                            ("slot_base", ctypes.c_int64), ("slot_vecs", ctypes.c_int64)]
-            s = _FastAr()
+            s = FastAr()
             for i, w in enumerate(words):
                 s.herr[i] = w
             s.epoch = ctypes.addressof(self._epoch_box)
@@ -425,6 +440,8 @@ class IpcAllreduce(IpcForms):
             s.signal_ptrs = self._pp_sig_addr
             s.rank, s.p = self.rank, self.p
             s.slot_base, s.slot_vecs = self._slot_base, self._slot_vecs
+            s.order = self.order().addr
+            s.own_err = self._herr.value
             st = self._fast_state = (s, words)
         return ctypes.addressof(st[0])
 
@@ -459,6 +476,10 @@ class IpcAllreduce(IpcForms):
         code = self.host_error()
         if code:
             ctypes.c_uint32.from_address(self._herr.value).value = 0
+            if code == 5:
+                raise Mp4jException(f"rank {self.rank}: an earlier IPC collective failed to launch after its epoch "
+                                    f"moved (a HIP launch error); its peers' kernels of that call time out, and "
+                                    f"the result of that call is invalid")
             if code == 4:
                 raise Mp4jException(f"rank {self.rank}: IPC protocol mismatch — a peer ran the staged form of a "
                                     f"collective while this rank ran the zero-copy form (or the reverse): buffer "
@@ -576,7 +597,7 @@ class IpcAllreduce(IpcForms):
                                              blocks, out, scale)
         piece = self.nbytes - self.nbytes % 16
         off = 0
-        st = stream_ptr()
+        st = self._launch_stream()
         # once prepare_graph() ran, EVERY call (eager or captured) takes its epoch from the device
         # counter, so eager calls and graph replays can interleave without reusing an epoch
         if capturing and self._epoch_dev is None:
@@ -598,10 +619,7 @@ class IpcAllreduce(IpcForms):
             m = min(piece, total - off)
             if not fused:
                 check(self.lib.mp4x_memcpy_async(self._data.value, sp + off, m, st), "ipc input copy")
-            if edev is not None:
-                check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
-            else:
-                self.epoch = next_epoch(self.epoch)
+            self._next_epoch(st, capturing)
             sb, sv = (self._slot_base, self._slot_vecs) if slotted else (0, 0)
             if lx is not None:
                 rc = lx.allreduce_ex(algo, dt, code, self._pp_data_addr, self._pp_sig_addr, self.rank, self.p, m,
@@ -628,6 +646,7 @@ class IpcAllreduce(IpcForms):
         main = torch.cuda.current_stream()
         cs = self._copy_stream
         edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
+        self.order().enter(stream_ptr(main))    # (before the side stream joins main)
         cs.wait_stream(main)            # the input was produced on the caller's stream
         kdone = [None, None]
         ms = stream_ptr(main)
@@ -644,10 +663,7 @@ class IpcAllreduce(IpcForms):
             ev = torch.cuda.Event()
             ev.record(cs)
             main.wait_event(ev)
-            if edev is not None:
-                check(self.lib.mp4x_ipc_bump_epoch(edev, ms), "ipc_bump_epoch")
-            else:
-                self.epoch = next_epoch(self.epoch)
+            self._next_epoch(ms, False)
             pp = self._pp_hi[0] if slot else self._pp_data[0]
             check(self.lib.mp4x_ipc_allreduce_ex(algo, dt, int(op.code), pp, self._pp_sig[0], self.rank, self.p, m,
                                                  None, dst.data_ptr() + off, self.epoch, blocks, edev, scale, ms),
@@ -1190,12 +1206,8 @@ class IpcAllreduce(IpcForms):
         return view
 
     def _push_ptrs(self, total: int, op, peers, scratch, dtype, scale: float = 1.0) -> None:
-        st = stream_ptr()
-        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
-        if edev is not None:
-            check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
-        else:
-            self.epoch = next_epoch(self.epoch)
+        st = self._launch_stream()
+        edev = self._next_epoch(st)
         chunk = -(-(total // 16) // self.p)
         blocks = max(1, min(self.grid_cap("push", dtype, op), -(-chunk // 512))) if self.shared_gpu else 0
         pp = ptr_array(peers)
@@ -1222,12 +1234,8 @@ class IpcAllreduce(IpcForms):
         rank's mapped buffer).  ``grid``: block count (0 = the default, up to one per CU; the
         autotuner's ``ipc2z_b<N>`` candidates try fewer — fewer, longer-lived readers per link)."""
         self.raise_if_failed()
-        st = stream_ptr()
-        edev = self._epoch_dev.data_ptr() if self._epoch_dev is not None else None
-        if edev is not None:
-            check(self.lib.mp4x_ipc_bump_epoch(edev, st), "ipc_bump_epoch")
-        else:
-            self.epoch = next_epoch(self.epoch)
+        st = self._launch_stream()
+        edev = self._next_epoch(st)
         blocks = self._grid(total // 16, "twoshot", dtype, op)   # >= 8: every XCD passes the barriers
         if grid > 0:
             blocks = min(grid, self.grid_cap("twoshot", dtype, op))
@@ -1291,7 +1299,7 @@ class IpcAllreduce(IpcForms):
         es = view.element_size()
         dt = int(dtype_of_torch(view.dtype))
         cbmax = self._fp8_piece_blocks()
-        st = stream_ptr()
+        st = self._launch_stream()
         base = view.data_ptr()
         off = 0
         while off < n:

@@ -75,7 +75,7 @@ class IpcForms:
             from ..operators import Operators, for_dtype, DType
             op = for_dtype(Operators.Float.SUM, DType.F32)
             got = torch.empty(n, device="cuda")
-            st = stream_ptr()
+            st = self._launch_stream()
             # each form twice on new data: the second run would read any stale cache line the
             # first one left behind on this topology
             for push, salt in ((False, 0), (True, 1)):
@@ -224,7 +224,7 @@ class IpcForms:
         self.raise_if_failed()
         rng, peers, lo, hi = z
         r = self.rank
-        st = stream_ptr()
+        st = self._launch_stream()
         edev = self._next_epoch(st)
         pp = ptr_array(peers)
         maxv = max(h - l_ for l_, h in zip(lo, hi))
@@ -240,7 +240,7 @@ class IpcForms:
             return False
         self.raise_if_failed()
         rng, peers, lo, hi = z
-        st = stream_ptr()
+        st = self._launch_stream()
         edev = self._next_epoch(st)
         pp = ptr_array(peers)
         lo_a = (c_int64 * self.p)(*lo)
@@ -259,7 +259,7 @@ class IpcForms:
     # other zero-copy forms: a rank running the staged plan against these fails at once.
     def _plan_registered(self, peers, pull, out_ptr, grid_len: int, buf_vecs: int) -> None:
         self.raise_if_failed()
-        st = stream_ptr()
+        st = self._launch_stream()
         edev = self._next_epoch(st)
         pp = ptr_array(peers)
         sa = (c_int64 * 4)()
@@ -307,14 +307,41 @@ class IpcForms:
             return False
         return all(((f - base) * es) % 16 == 0 and ((t - base) * es) % 16 == 0 for f, t in zip(froms, tos))
 
-    def _next_epoch(self, st):
+    def _next_epoch(self, st, capturing=None):
+        """The epoch of a launch on stream ``st`` (every IPC launch goes through here): the
+        communicator's stream order first (parallel/order.py: a launch on another stream than the
+        previous one waits for it), then the device counter's bump (graph mode; its address is
+        returned) or the host epoch's (None)."""
         if self._epoch_dev is not None:
+            self.order().enter(st)
             check(self.lib.mp4x_ipc_bump_epoch(self._epoch_dev.data_ptr(), st), "ipc_bump_epoch")
             return self._epoch_dev.data_ptr()
-        if torch.cuda.is_current_stream_capturing():
+        if capturing if capturing is not None else torch.cuda.is_current_stream_capturing():
             raise Mp4jException("call IpcAllreduce.prepare_graph() (collectively) before capturing")
+        self.order().enter(st)
         self.epoch = ((self.epoch + 1) & 0x3FFFFFFF) or 2   # (ipc.next_epoch)
         return None
+
+    def _launch_stream(self) -> int:
+        """The current stream, joined to the communicator's stream order: every staging copy,
+        memset and kernel a form queues after this is ordered after the previous collective."""
+        st = stream_ptr()
+        self.order().enter(st)
+        return st
+
+    def order(self):
+        """The stream-order guard of this instance's launches: the owning engine's (one per
+        communicator, :meth:`use_order`), else one of its own."""
+        o = self.__dict__.get("_order")
+        if o is None:
+            from .order import CommOrder
+            o = self.__dict__["_order"] = CommOrder()
+        return o
+
+    def use_order(self, order) -> None:
+        """Share the communicator's stream-order guard (set by the engine before any launch)."""
+        self.__dict__["_order"] = order
+        self.__dict__["_fast_state"] = None
 
     def _grid(self, nvec: int, family: str = "plan", dtype=None, op=None) -> int:
         """Explicit grid for a per-block-barrier kernel.  ``nvec`` must be RANK-INDEPENDENT (the
@@ -337,7 +364,7 @@ class IpcForms:
         es = view.element_size()
         flat = view.view(-1)
         base, r = froms[0], self.rank
-        st = stream_ptr()
+        st = self._launch_stream()
         n = (tos[-1] - base) * es
         if self._fuse_copy and n:
             # one launch: the kernel stages this rank's range and writes its segment in place.
@@ -406,7 +433,7 @@ class IpcForms:
             if tmp is not None:
                 rng.view(torch.uint8).copy_(tmp)
             return True
-        st = stream_ptr()
+        st = self._launch_stream()
         seg = (tos[r] - froms[r]) * es
         if seg:
             check(self.lib.mp4x_memcpy_async(self._data.value + (froms[r] - base) * es, flat[froms[r]:].data_ptr(),
@@ -432,7 +459,7 @@ class IpcForms:
 
     def _plan(self, stage, pull, src_ptr, out_ptr, grid_len) -> None:
         self.raise_if_failed()
-        st = stream_ptr()
+        st = self._launch_stream()
         edev = self._next_epoch(st)
         sa = (c_int64 * (4 * max(1, len(stage))))(*[x for it in stage for x in it])
         pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
@@ -621,7 +648,7 @@ class IpcForms:
         sv = s * es // 16
         buf = self._data.value
         dt = int(dtype_of_torch(view.dtype))
-        st = stream_ptr()
+        st = self._launch_stream()
         for i in range(-(-max(counts) // s)):
             lens = [max(0, min(c - i * s, s)) for c in counts]
             for j in range(p):
@@ -652,7 +679,7 @@ class IpcForms:
         s = self._slab(es)
         sv = s * es // 16
         buf = self._data.value
-        st = stream_ptr()
+        st = self._launch_stream()
         for i in range(-(-max(counts) // s)):
             lens = [max(0, min(c - i * s, s)) for c in counts]
             if lens[r]:

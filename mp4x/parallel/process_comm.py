@@ -43,6 +43,26 @@ from .transport import HostTransport
 
 LOG = logging.getLogger("mp4x.comm")
 
+
+# Return codes of the native fast paths that mean "nothing was launched, the epoch did not move"
+# (csrc/include/mp4x/ops.h): the call goes on to the full path.  Any other nonzero code is a HIP
+# error AFTER the epoch moved — raised at once (falling back would bump the epoch a
+# second time and leave this rank a call ahead of its peers).
+_NOT_LAUNCHED = frozenset((1001, 1002, 1003, 1004))
+
+
+def _fast_ok(rc: int, where: str) -> bool:
+    """True: the fast path launched.  False: refused before anything moved (take the full path).
+    Raises for a launch error after the epoch moved."""
+    if rc == 0:
+        return True
+    if rc in _NOT_LAUNCHED:
+        return False
+    from ..ops import native
+    native.check(rc, where)
+    return False
+
+
 HEARTBEAT_DELAY = float(os.environ.get("MP4X_HEARTBEAT_DELAY", 5.0))
 HEARTBEAT_PERIOD = float(os.environ.get("MP4X_HEARTBEAT_PERIOD", 15.0))
 HEARTBEAT_MAX_FAIL = int(os.environ.get("MP4X_HEARTBEAT_MAX_FAIL", 4))
@@ -335,7 +355,10 @@ class ProcessCommSlave:
                             arrData.dtype) + tail)
         except TypeError:               # unhashable ranges (e.g. arrays): the full path
             return False
-        if ent is None or self._fast_pl(ent, self._fast_stream(), base) != 0:
+        if ent is None:
+            return False
+        rc = self._fast_pl(ent, self._fast_stream(), base)
+        if rc and not _fast_ok(rc, "mp4x_ipc_fast_plan"):
             return False
         self._fast_after(ent.stat, ent.api)
         return True
@@ -643,7 +666,7 @@ class ProcessCommSlave:
                                     arrData.get_device(), n, arrData.dtype) + tail)
                 except TypeError:
                     ent = tail = None
-                if ent is not None and self._fast_rs(ent, self._fast_stream(), base) == 0:
+                if ent is not None and _fast_ok(self._fast_rs(ent, self._fast_stream(), base), "mp4x_ipc_fast_rs"):
                     self._fast_after(ent.stat, ent.api)
                     return arrData
         self._tick("reduceScatterArray")
@@ -692,7 +715,7 @@ class ProcessCommSlave:
             base, n = arrData.data_ptr(), arrData.numel()
             ent = fast.get(("reduce", fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm,
                             to, arrData.dtype, operator, operand.codec, operand.compress, 1.0))
-            if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
+            if ent is not None and _fast_ok(self._fast_lx(ent, self._fast_stream(), base), "mp4x_ipc_fast_allreduce"):
                 self._fast_after(ent.stat, ent.api)
                 return arrData
         self._tick("reduceArray")
@@ -889,11 +912,13 @@ class ProcessCommSlave:
             base, n = arrData.data_ptr(), arrData.numel()
             ent = fast.get((fast.addr_key(base, n * arrData.element_size()), arrData.get_device(), n, frm, to,
                             arrData.dtype, operator, operand.codec, operand.compress, scale))
-            if ent is not None and self._fast_lx(ent, self._fast_stream(), base) == 0:
-                self._fast_after(ent.stat, ent.api)
-                return arrData
+            if ent is not None:
+                rc = self._fast_lx(ent, self._fast_stream(), base)
+                if rc == 0 or _fast_ok(rc, "mp4x_ipc_fast_allreduce"):
+                    self._fast_after(ent.stat, ent.api)
+                    return arrData
             # not memoised, or not launched (rc 1003: an earlier collective failed; 1004: the stream
-            # is being captured; an unaligned buffer): the full path decides, raises or records
+            # is being captured; 1001 / 1002: refused): the full path decides, raises or records
         self._tick("allreduceArray")
         if scale != 1.0:
             if _is_device_tensor(arrData) and self.slaveNum > 1:

@@ -400,8 +400,12 @@ def test_staged_calls_take_the_slots_only_when_fused_one_piece_and_small(monkeyp
             return 0
     monkeypatch.setattr(ipc_mod.native, "launch_ext", lambda: _Lx())
     monkeypatch.setattr(ipc_mod, "stream_ptr", lambda *a: 0)
+    from mp4x.parallel import ipc_forms as forms_mod
+    monkeypatch.setattr(forms_mod, "stream_ptr", lambda *a: 0)
     inst = object.__new__(ipc_mod.IpcAllreduce)
     inst.raise_if_failed = lambda: None
+    entered = []
+    inst._order = type("O", (), {"enter": staticmethod(entered.append)})()
     inst.nbytes, inst._slot_bytes = 1 << 20, 256 << 10
     inst._slot_base, inst._slot_vecs = (1 << 20) // 16, (256 << 10) // 16
     inst.shared_gpu, inst._epoch_dev, inst._overlap_default = False, None, False
@@ -423,6 +427,7 @@ def test_staged_calls_take_the_slots_only_when_fused_one_piece_and_small(monkeyp
         t = torch.zeros(n + 4)[shift[0]:shift[0] + n] if shift else torch.zeros(n)
         inst.allreduce(t, Operators.Float.SUM, algo=algo, out=torch.zeros(n), capturing=False)
         (a,) = calls
+        assert entered and set(entered) == {0}       # the stream order joined before the launch
         assert not fuse or (a[8] is not None and a[8] % 16 == 0), a[8]    # the fused copy-in's source
         assert a[15:] == ((inst._slot_base, inst._slot_vecs) if want else (0, 0)), (n, algo, fuse, a[15:])
 

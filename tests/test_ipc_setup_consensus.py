@@ -398,9 +398,12 @@ class _FakeInst:
     _epoch_dev = None
     made = []
 
-    def __init__(self, comm, nbytes=None, tag=""):
+    def __init__(self, comm, nbytes=None, tag="", slots=True):
         self.comm, self.tag, self.closed = comm, tag, None
         _FakeInst.made.append(self)
+
+    def use_order(self, order):
+        pass
 
     def set_spin(self, s, on_current_stream=True):
         pass

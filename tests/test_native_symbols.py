@@ -9,7 +9,7 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
-MODULES = ["mp4x.ops.device_ops", "mp4x.parallel.ipc", "mp4x.parallel.vmm", "mp4x.parallel.sparse",
+MODULES = ["mp4x.ops.device_ops", "mp4x.parallel.ipc", "mp4x.parallel.order", "mp4x.parallel.vmm", "mp4x.parallel.sparse",
            "mp4x.parallel.zs", "mp4x.utils.topology"]
 
 
