@@ -48,6 +48,9 @@ import sys
 import time
 
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (mp4x/__init__.py), before any HIP call
+# the tier sweep's pins persist under this job's topology key, and the next job on the same
+# topology loads them at creation (mp4x/parallel/tiers.py)
+os.environ.setdefault("MP4X_TUNE_AUTO", "1")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -414,7 +417,9 @@ def main():
                        "in_place": p > 1, "scale": scale if p > 1 else None, "autotune_ms": tuned,
                        "autotune_iters": args.autotune_iters, "ipc_selftest": selftest, "ipc": ipc_info,
                        "probe_failures": probes, "calls": stats, "tier_sweep_ms": tiers,
-                       "baseline_configs": configs, "extras": extras, "topology": topo},
+                       "baseline_configs": configs, "extras": extras, "topology": topo,
+                       "tune_store": None if (p == 1 or args.cpu) else
+                       {"path": comm.device.tune_path(), "loaded_at_start": comm.device.tune_loaded}},
             "verified": verified,
             "max_abs_err": max_err,
             "busbw_gbps_per_rank": round(busbw, 3),

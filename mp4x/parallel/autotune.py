@@ -498,11 +498,21 @@ class AutotuneMixin:
                     "reduce": {"rccl", "ipc", "a2a"}, "broadcast": {"rccl", "ipc", "composite"},
                     "gather": {"p2p", "ipc"}, "scatter": {"p2p", "ipc"}}
 
+    _topo_agreed = None
+
     def _topology(self) -> dict:
+        """The topology a tuning table applies to: rank count, device name, backend, node count and
+        the xGMI pair map of the ranks' devices (parallel/tiers.py).  Agreed at engine creation
+        (rank 0's record, ``_load_shared_tuning``) so every rank keys and checks tables alike."""
+        if self._topo_agreed is not None:
+            return self._topo_agreed
         dev = torch.cuda.get_device_name(self.device) if self.device.type == "cuda" else "cpu"
         top = {"p": self.p, "device": dev, "backend": self.backend}
         if self.layout.multi_node:
             top["nodes"] = len(self.layout.nodes)
+        if self.device.type == "cuda":
+            from .tiers import xgmi_map
+            top["xgmi"] = xgmi_map(self.p, self.device.index)
         return top
 
     def tuning_table(self) -> dict:
@@ -520,6 +530,8 @@ class AutotuneMixin:
         if self.rank != 0:
             return
         import json
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
         tmp = f"{path}.tmp{os.getpid()}"
         with open(tmp, "w") as f:
             json.dump(self.tuning_table(), f, indent=1)
@@ -547,8 +559,18 @@ class AutotuneMixin:
             n += 1
         return n
 
-    def _autosave(self) -> None:
+    def tune_path(self):
+        """Where this job's pinned table is saved: ``MP4X_TUNE_FILE``, else with
+        ``MP4X_TUNE_AUTO=1`` the topology-keyed file in ``MP4X_TUNE_DIR`` (parallel/tiers.py)."""
         path = os.environ.get("MP4X_TUNE_FILE")
+        if not path:
+            from . import tiers
+            if tiers.auto_enabled():
+                path = tiers.tune_path(self._topology())
+        return path
+
+    def _autosave(self) -> None:
+        path = self.tune_path()
         if path:
             try:
                 self.save_tuning(path)

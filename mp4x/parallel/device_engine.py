@@ -282,8 +282,12 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         # two ranks: the one-shot moves the same bytes over the one link as the two-shot with one
         # barrier fewer, so the staged allreduce takes it for every size a slot holds (measured on
         # one GPU: 1.7-2.2x faster than the two-shot at 256 KiB - 4 MiB, profiles/r5/tiers/)
+        # the staged allreduce's one-shot / two-shot crossover follows the per-link byte model at
+        # this rank count (parallel/tiers.py): the slot size (4 MiB) at two ranks, 512 KiB at
+        # three, 256 KiB from four on; autotune re-pins the size classes it measures
         from .ipc import SLOTS_ON, SLOT_BYTES
-        self._oneshot_ar_max = max(self.ipc_oneshot_max, SLOT_BYTES) if self.p == 2 and SLOTS_ON and \
+        from .tiers import oneshot_max
+        self._oneshot_ar_max = oneshot_max(self.p, SLOT_BYTES) if self.p >= 2 and SLOTS_ON and \
             "MP4X_IPC_ONESHOT_MAX" not in os.environ else 0
         self._ipc_obj = None
         self._ipc_large = None
@@ -300,7 +304,6 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         self._dm_large = os.environ.get("MP4X_DM_LARGE", "auto")
         self._zc = os.environ.get("MP4X_IPC_ZC", "1") == "1"   # zero-copy two-shot on registered tensors
         self._select_tuned = False
-        self._load_shared_tuning(shared=coll is None)
         # which ranks share a node (parallel/hier.py): a job spanning nodes has no global IPC mesh;
         # its allreduce can run node-aware (xGMI inside a node, RCCL across nodes)
         from .hier import node_id
@@ -308,6 +311,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                                  else ["local"] * self.p)
         if self.layout.multi_node:
             self.ipc_enabled = False
+        self._load_shared_tuning(shared=coll is None)      # (keys on the layout's node count)
         self.hier_min_bytes = int(os.environ.get("MP4X_HIER_MIN_BYTES", 1 << 20))
         self._hier = None
         self._hier_failed = False
@@ -316,31 +320,43 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         self.watchdog = watchdog.CollectiveWatchdog(self) if coll is None and watchdog.enabled() else None
 
     def _load_shared_tuning(self, shared: bool = True) -> None:
-        """``MP4X_TUNE_FILE``: rank 0 reads the table and every rank pins RANK 0's copy (shared
-        through the control plane).  A file present on one host only, or unreadable on one rank,
-        can then never make ranks pin different schedules for the same call (which would pair
-        mismatched collectives and hang).  Collective when more than one rank."""
+        """``MP4X_TUNE_FILE``, else (``MP4X_TUNE_AUTO=1``) the topology-keyed table of this job's
+        topology in ``MP4X_TUNE_DIR`` (parallel/tiers.py): rank 0 reads the table and every rank
+        pins RANK 0's copy (shared through the control plane), checked against rank 0's topology
+        record (agreed here, used by every later ``_topology`` call).  A file present on one host
+        only, or unreadable on one rank, can then never make ranks pin different schedules for the
+        same call (which would pair mismatched collectives and hang).  Collective when more than
+        one rank."""
+        from . import tiers
         table, err = None, None
         path = os.environ.get("MP4X_TUNE_FILE")
-        if (self.rank == 0 or not shared) and path and os.path.exists(path):
-            try:
-                import json
-                with open(path) as f:
-                    table = json.load(f)
-            except Exception as e:   # noqa: BLE001 — a broken table is ignored, not fatal
-                err = str(e)
+        topo = None
+        if self.rank == 0 or not shared:
+            topo = self._topology()
+            if not path and tiers.auto_enabled():
+                path = tiers.tune_path(topo)
+            if path and os.path.exists(path):
+                try:
+                    import json
+                    with open(path) as f:
+                        table = json.load(f)
+                except Exception as e:   # noqa: BLE001 — a broken table is ignored, not fatal
+                    err = str(e)
         if self.p > 1 and shared:      # (injected loopback ranks share one process and file)
             try:
-                table = self.all_gather_object(table)[0]
+                table, topo = self.all_gather_object((table, topo))[0]
             except Exception as e:   # noqa: BLE001
                 LOG.warning("tuning table not shared (%s): none pinned", e)
                 return
+        if topo is not None:
+            self._topo_agreed = topo
         if err:
             LOG.warning("ignoring tuning table %s: %s", path, err)
         if table is None:
             return
         try:
             n = self.load_tuning(table)
+            self.tune_loaded = n
             LOG.info("rank %d: %d pinned schedules from rank 0's %s", self.rank, n, path)
         except Exception as e:   # noqa: BLE001 — a foreign table is refused identically on every rank
             self._tuned.clear()
@@ -481,6 +497,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         return self._ipc_obj
 
     ipc_selftest: Optional[dict] = None
+    tune_loaded = 0                       # schedules pinned from a saved table at creation
     order = None                          # (engines assembled without __init__: no stream order)
 
     def _adopt(self, inst) -> None:

@@ -30,3 +30,14 @@ def test_multi_plan_needs_enough_gpus():
         device_plan(4, 2, "multi")
     with pytest.raises(ValueError):
         device_plan(2, 2, "bogus")
+
+
+def test_multi_dryrun_plans_shared(monkeypatch):
+    """MP4X_TEST_MULTI_DRYRUN=1 (VERDICT r5 Next #2): the cross-GPU tests run on one GPU with gloo
+    instead of skipping; without the knob the multi plan still needs a GPU per rank."""
+    monkeypatch.setenv("MP4X_TEST_MULTI_DRYRUN", "1")
+    plan, env = device_plan(8, 1, "multi")
+    assert plan == "shared" and env["MP4X_DEVICE_BACKEND"] == "gloo" and env["GPU_MAX_HW_QUEUES"] == "2"
+    monkeypatch.setenv("MP4X_TEST_MULTI_DRYRUN", "0")
+    with pytest.raises(ValueError):
+        device_plan(8, 1, "multi")

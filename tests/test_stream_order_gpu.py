@@ -127,9 +127,21 @@ def _order_fn(comm, batches, jitter, stop_on_failure):
             "eng": {k: v for k, v in eng.stats.items() if "ipc" in k}}
 
 
+def _record(name, out):
+    """Per-rank outcomes as JSON lines into ``MP4X_TEST_RECORD`` (evidence for profiles/)."""
+    import json
+    import os
+    path = os.environ.get("MP4X_TEST_RECORD")
+    if path:
+        with open(path, "a") as f:
+            for r, o in sorted(out.items()):
+                f.write(json.dumps({"test": name, "rank": r, **o}, default=str) + "\n")
+
+
 @pytest.mark.parametrize("p,batches", [(2, 90), (4, 90), (8, 90)])
 def test_two_stream_soak_is_exact(p, batches):
     out = run_spawn(p, _order_fn, args=(batches, True, False), timeout=600)
+    _record(f"soak_p{p}", out)
     for r, o in out.items():
         assert o["oracle_ok"], (r, o)
         assert o["calls"] >= 1000, o
@@ -148,5 +160,6 @@ def test_without_the_guard_the_soak_fails():
     in 2 s instead of the fail-stop budget."""
     out = run_spawn(2, _order_fn, args=(40, True, True), timeout=400,
                     env={"MP4X_TEST_NO_STREAM_ORDER": "1", "MP4X_IPC_SPIN_S": "2"})
+    _record("no_guard_p2", out)
     assert any(o["bad"] or o["raised"] or any(o["words"]) for o in out.values()), out
     assert all(o["switches"] == 0 for o in out.values()), out       # the guard really was off
