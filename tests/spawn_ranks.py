@@ -102,9 +102,19 @@ def run_spawn(p, fn, args=(), env=None, timeout=240, threads=0, mode="shared"):
     out = {}
     import queue as _queue
     import time as _time
-    deadline = _time.monotonic() + timeout
+    t_start = _time.monotonic()
+    deadline = t_start + timeout
+    beat = t_start
+    progress = os.environ.get("MP4X_TEST_PROGRESS")
     try:
         while len(out) < p:
+            if progress and _time.monotonic() - beat > 30:
+                # a heartbeat for long multi-rank tests: a GPU call with nothing new on its outputs
+                # for minutes is taken to be hung
+                beat = _time.monotonic()
+                with open(progress, "a") as f:
+                    f.write(f"{_time.strftime('%H:%M:%S')} run_spawn {getattr(fn, '__name__', fn)} p={p}: "
+                            f"{len(out)}/{p} ranks done after {beat - t_start:.0f} s\n")
             try:
                 r, st, val = q.get(timeout=1.0)
             except _queue.Empty:
