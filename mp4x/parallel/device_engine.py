@@ -462,8 +462,13 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
                 inst = IpcAllreduce(self.comm)
                 self._adopt(inst)
             except Exception as e:
-                LOG.warning("IPC allreduce disabled: %s", e)
+                # never a silent fall-back: the verdict says why (e.g. the legacy IPC mode) and how
+                # to fix it, once, on every rank (setup failures are agreed inside IpcAllreduce)
+                from .ipc import ipc_mode_report
+                rep = ipc_mode_report(str(e))
+                LOG.warning("IPC allreduce disabled: %s%s", e, f" — {rep['reason']}" if rep.get("reason") else "")
                 self.ipc_enabled = False
+                self.ipc_selftest = {"ok": False, "failures": [f"setup: {str(e)[:300]}"], "ipc_mode": rep}
                 return None
             bad = self._ipc_self_test(inst)
             if bad and all(": zero_copy_memalloc" in b for b in bad):
@@ -788,7 +793,9 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             fails.append("injected failure (MP4X_IPC_SELFTEST_INJECT)")
         allf = self.comm.server.call("allgather_obj", self.rank, fails)
         bad = [f"rank {i}: {x}" for i, fl in enumerate(allf) for x in (fl or [])]
-        self.ipc_selftest = {"ok": not bad, "failures": bad, "seconds": round(time.perf_counter() - t0, 3)}
+        from .ipc import ipc_mode_report
+        self.ipc_selftest = {"ok": not bad, "failures": bad, "seconds": round(time.perf_counter() - t0, 3),
+                             "ipc_mode": ipc_mode_report()}
         if not bad:
             LOG.info("rank %d: IPC self-test passed in %.3f s", self.rank, self.ipc_selftest["seconds"])
         return bad or None

@@ -131,6 +131,32 @@ _FLOAT_DTYPES = (torch.float32, torch.float64, torch.bfloat16, torch.float16)
 _FP8_NARROW = os.environ.get("MP4X_FP8_NARROW") == "1"    # the r1 4-byte-lane fp8 kernel (A/B)
 
 
+def ipc_mode_report(err: Optional[str] = None) -> dict:
+    """Which IPC mode the HIP runtime of this process most likely uses, and — for a failed handle
+    export or open (``err``) — the reason and the fix.  The dmabuf mode needs
+    ``HSA_ENABLE_IPC_MODE_LEGACY=0`` in the environment when the HSA runtime starts; ``import mp4x``
+    sets it (unless set), which is too late when HIP was initialised before (mp4x/__init__.py)."""
+    import mp4x
+    at = dict(getattr(mp4x, "IPC_MODE_AT_IMPORT", {}) or {})
+    env = at.get("env_before_import")
+    legacy = env not in (None, "0") or (env is None and at.get("hip_initialized_before_import"))
+    rep = {"legacy_env_before_import": env, "hip_initialized_before_import": at.get("hip_initialized_before_import"),
+           "dmabuf_expected": not legacy}
+    if err is not None:
+        handle = any(k in err for k in ("ipc_get_handle", "ipc_open_handle", "hipIpc", "invalid argument"))
+        if legacy:
+            cause = (f"HSA_ENABLE_IPC_MODE_LEGACY={env}" if env not in (None, "0") else
+                     "HIP was initialised before `import mp4x` with HSA_ENABLE_IPC_MODE_LEGACY unset")
+            rep["reason"] = (f"IPC handle export/import failed in the legacy IPC mode ({cause}); this platform "
+                             f"needs dmabuf IPC: start the process with HSA_ENABLE_IPC_MODE_LEGACY=0 (or import mp4x "
+                             f"before anything touches the GPU)")
+        elif handle:
+            rep["reason"] = "IPC handle export/import failed although the dmabuf mode was requested: " + err[:200]
+        else:
+            rep["reason"] = err[:200]
+    return rep
+
+
 def staging_needs_vmm(alloc_bytes: int) -> bool:
     """Is a staging allocation of ``alloc_bytes`` (buffer + slots) above the IPC open limit, so it
     must be built from VMM chunks exported as dmabuf fds instead of one hipIpc allocation?"""
