@@ -329,6 +329,45 @@ def run_starts(sorted_keys: torch.Tensor, stream=None):
     return starts, nruns
 
 
+def hash_rbk_supported(dtype: torch.dtype, op: int) -> bool:
+    """Does the hash reduce-by-key (K5h, csrc/kernels/sparse_hash.hip) serve (dtype, op)?"""
+    try:
+        dt = dtype_of_torch(dtype)
+    except Exception:   # noqa: BLE001
+        return False
+    return bool(native.hip().mp4x_hash_rbk_supported(int(dt), int(op)))
+
+
+def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=None):
+    """K5h: (unique_keys, reduced_rows, counts) in hash-table order — open addressing + atomic
+    combine (SUM / MAX / MIN of f32 / f64 / i32 / i64 rows).  Float sums combine in arrival order
+    (exact for integer-valued data).  Returns None when a key equals -1 (the table's EMPTY marker):
+    the caller takes the sort path (:func:`reduce_by_key`)."""
+    _dev_check(keys, vals)
+    n = keys.numel()
+    if keys.dtype != torch.int64 or vals.dim() not in (1, 2) or vals.shape[0] != n:
+        raise ValueError("hash_reduce_by_key: int64 keys[n] and vals[n] / vals[n, dim]")
+    if not hash_rbk_supported(vals.dtype, op):
+        raise ValueError(f"hash_reduce_by_key: {vals.dtype} op {op} not supported")
+    dev = keys.device
+    dim = 1 if vals.dim() == 1 else int(vals.shape[1])
+    lib = native.hip()
+    sb = lib.mp4x_hash_rbk_scratch_bytes(n)
+    scratch = torch.empty(sb, dtype=torch.uint8, device=dev)
+    m_flag = torch.empty(2, dtype=torch.int64, device=dev)
+    out_keys = torch.empty(n, dtype=torch.int64, device=dev)
+    out_vals = torch.empty_like(vals)
+    out_count = torch.empty(n, dtype=torch.int32, device=dev)
+    check(lib.mp4x_hash_reduce_by_key(int(dtype_of_torch(vals.dtype)), int(op), keys.data_ptr(), n, vals.data_ptr(),
+                                      dim, scratch.data_ptr(), sb, out_keys.data_ptr(), out_vals.data_ptr(),
+                                      out_count.data_ptr(), m_flag.data_ptr(), stream_ptr(stream)),
+          "mp4x_hash_reduce_by_key")
+    m, flag = m_flag.tolist()
+    if flag & 0xFFFFFFFF:
+        return None
+    return out_keys[:m], out_vals[:m], out_count[:m]
+
+
 def reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op: int, key_bits: Optional[int] = None,
                   stream=None):
     """Deterministic reduce-by-key: returns (unique_keys, reduced_vals, counts), keys ascending.

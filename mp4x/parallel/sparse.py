@@ -153,11 +153,22 @@ def _sync_new_keys(engine, new: List) -> None:
 
 
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins
+# Reduce-by-key of the device map collectives (K5): "sort" (default: rocPRIM radix sort + run
+# starts + the segmented reduce — deterministic, keys ascending per owner) or "hash" (K5h,
+# csrc/kernels/sparse_hash.hip: open addressing + atomic combine for SUM / MAX / MIN of f32 / f64 /
+# i32 / i64 rows; keys in table order, float sums in arrival order).  A/B: profiles/r6/sparse/.
+RBK_MODE = os.environ.get("MP4X_SPARSE_RBK", "sort").lower()
 def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bits: Optional[int] = None):
     """``key_bits``: every key is in [0, 2**key_bits) (dense dictionary ids) — the radix sort
     covers those bits only."""
     if keys.is_cuda:
         from ..ops.device_ops import reduce_by_key
+        if vals is not None and RBK_MODE == "hash" and not getattr(op, "is_custom", False):
+            from ..ops.device_ops import hash_rbk_supported, hash_reduce_by_key
+            if hash_rbk_supported(vals.dtype, int(op.code)):
+                got = hash_reduce_by_key(keys, vals, int(op.code))
+                if got is not None:
+                    return got
         return reduce_by_key(keys, vals, int(op.code) if vals is not None else 0, key_bits=key_bits)
     # CPU twin for the gloo test configuration only
     uk, inv, cnt = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)

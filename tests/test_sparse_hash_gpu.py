@@ -1,0 +1,69 @@
+"""K5h, the hash reduce-by-key (csrc/kernels/sparse_hash.hip, VERDICT r5 Next #6): exact against
+the deterministic sort path (K5) on integer-valued rows, for SUM / MAX / MIN of f32 / f64 / i32 /
+i64, on the BASELINE config-4 shape (the rows one owner receives at 8 ranks: 200k keys x float[64]
+per rank, half of them shared) and on small / odd shapes; a key equal to the table's EMPTY
+marker (-1) makes it decline (the caller takes the sort path)."""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+
+def _config4_owner_rows(p=8, nkeys=200_000, dim=64, owner=3, dtype=torch.float32):
+    """The (keys, rows) owner ``owner`` receives in config 4: every rank's keys with id % p ==
+    owner, rank after rank; integer-valued rows."""
+    shared = nkeys // 2
+    ks, vs = [], []
+    for r in range(p):
+        ids = torch.cat([torch.arange(shared), 10_000_000 + r * nkeys + torch.arange(nkeys - shared)])
+        ids = ids[ids % p == owner]
+        ks.append(ids)
+        vs.append(((ids.view(-1, 1) * 7 + torch.arange(dim) + r) % 23 - 11).to(dtype))
+    return torch.cat(ks).cuda(), torch.cat(vs).cuda()
+
+
+def _sorted(k, v, c):
+    o = torch.argsort(k)
+    return k[o], v[o], c[o]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int32, torch.int64])
+@pytest.mark.parametrize("op", [0, 1, 2])           # SUM, MAX, MIN
+def test_hash_matches_sort_path(dtype, op):
+    from mp4x.ops.device_ops import hash_reduce_by_key, reduce_by_key
+    cases = [_config4_owner_rows(dtype=dtype)]
+    g = torch.Generator().manual_seed(7)
+    for n, dim, nk in ((1, 1, 1), (1000, 3, 50), (4096, 16, 4096), (70000, 5, 900)):
+        keys = torch.randint(0, nk, (n,), generator=g) * 7919 - 123456
+        rows = torch.randint(-50, 50, (n, dim), generator=g).to(dtype)
+        cases.append((keys.cuda(), rows.cuda()))
+    for keys, rows in cases:
+        hk, hv, hc = _sorted(*hash_reduce_by_key(keys, rows, op))
+        sk, sv, sc = reduce_by_key(keys, rows, op)
+        assert torch.equal(hk, sk)
+        assert torch.equal(hc, sc)
+        assert torch.equal(hv, sv), (dtype, op, keys.numel(), (hv != sv).sum().item())
+
+
+def test_empty_marker_key_declines():
+    from mp4x.ops.device_ops import hash_reduce_by_key
+    keys = torch.tensor([5, -1, 5, 9], device="cuda")
+    rows = torch.ones(4, 8, device="cuda")
+    assert hash_reduce_by_key(keys, rows, 0) is None
+    k, v, c = _sorted(*hash_reduce_by_key(keys.abs() + 1, rows, 0))
+    assert k.tolist() == [2, 6, 10] and c.tolist() == [1, 2, 1] and v[1].tolist() == [2.0] * 8
+
+
+def test_sparse_allreduce_in_hash_mode(monkeypatch):
+    """The map path with MP4X_SPARSE_RBK=hash: the same set of (key, row) pairs as the sort path."""
+    from mp4x.parallel import sparse
+    keys, rows = _config4_owner_rows(p=4, nkeys=20000, dim=16)
+    from mp4x.operators import Operators, for_dtype, DType
+    op = for_dtype(Operators.Float.SUM, DType.F32)
+    monkeypatch.setattr(sparse, "RBK_MODE", "sort")
+    sk, sv, _ = sparse._reduce_by_key(keys, rows, op)
+    monkeypatch.setattr(sparse, "RBK_MODE", "hash")
+    hk, hv, _ = sparse._reduce_by_key(keys, rows, op)
+    o = torch.argsort(hk)
+    assert torch.equal(hk[o], sk) and torch.equal(hv[o], sv)
