@@ -139,8 +139,8 @@ class AutotuneMixin:
 
     def allreduce_candidates(self, nbytes: int, op, dtype) -> List[str]:
         """The default decision tree's allreduce candidates (DESIGN.md "Default schedules"): at
-        most six — ``rccl``, ``ipc1`` (<= 4 MiB), ``ipc2``, ``ipc2z``, ``ipc2w``, ``a2a`` (``hier``
-        replaces the IPC forms on a multi-node job).  The rest only with :meth:`_extra_schedules`."""
+        most six — ``rccl``, ``ipc1`` (<= 4 MiB), ``ipc2``, ``ipc2z``, ``ipc2w``, ``a2a``.  The rest only
+        with :meth:`_extra_schedules`; ``hier`` (a multi-node job) also with ``MP4X_HIER=1``."""
         c = []
         extra = self._extra_schedules()
         if self._stand_in() and self._ipc_ok(op, dtype, nbytes):
@@ -162,8 +162,8 @@ class AutotuneMixin:
                 c.append("ipc2w")     # ... its push form: every xGMI transfer a posted write
                 if extra and nbytes >= (64 << 20) and not getattr(self._ipc_obj, "shared_gpu", True):
                     c += [f"ipc2z_b{g}" for g in ZC_GRIDS]     # ... with fewer, longer-lived blocks
-        if self._hier_ok(op, dtype, nbytes):
-            c.append("hier")
+        if (extra or self._hier_auto) and self._hier_ok(op, dtype, nbytes):
+            c.append("hier")          # opt-in: multi-node only (one node is the whole target machine)
         c.append("a2a")
         if extra and nbytes <= (64 << 20):
             c.append("rhd")

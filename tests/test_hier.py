@@ -68,7 +68,7 @@ def hier_body(comm, n):
 def test_hier_allreduce_simulated_nodes(p, size, piece):
     n = 10_000
     res, _, _ = run_ranks(p, hier_body, args=(n,), timeout=180,
-                          env={"MP4X_SIM_NODE_SIZE": str(size), "MP4X_HIER_MIN_BYTES": "0",
+                          env={"MP4X_SIM_NODE_SIZE": str(size), "MP4X_HIER_MIN_BYTES": "0", "MP4X_HIER": "1",
                                "MP4X_HIER_PIECE_BYTES": str(piece), "MP4X_DEVICE_BACKEND": "gloo"})
     for calls, pieces, odd_algo in res.values():
         assert calls == 4
@@ -87,7 +87,8 @@ def unequal_body(comm):
 
 def test_unequal_nodes_use_the_flat_schedule():
     res, _, _ = run_ranks(3, unequal_body, timeout=120,
-                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_HIER_MIN_BYTES": "0", "MP4X_DEVICE_BACKEND": "gloo"})
+                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_HIER_MIN_BYTES": "0", "MP4X_HIER": "1",
+                               "MP4X_DEVICE_BACKEND": "gloo"})
     for multi, ok, stats in res.values():
         assert multi and not ok and "allreduce.hier" not in stats
 
@@ -100,7 +101,16 @@ def autotune_body(comm):
 
 def test_hier_is_an_autotune_candidate():
     res, _, _ = run_ranks(4, autotune_body, timeout=180,
-                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_DEVICE_BACKEND": "gloo"})
+                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_DEVICE_BACKEND": "gloo", "MP4X_HIER": "1"})
     names = {tuple(v[0]) for v in res.values()}
     assert len(names) == 1 and "hier" in next(iter(names))
     assert len({v[1] for v in res.values()}) == 1      # every rank pinned the same schedule
+
+
+def test_hier_is_opt_in():
+    """VERDICT r5 Next #7: one MI355X node is the whole target machine, so the node-aware schedule
+    is neither picked nor autotuned on a multi-node layout unless MP4X_HIER=1 asks for it."""
+    res, _, _ = run_ranks(4, autotune_body, timeout=180,
+                          env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_DEVICE_BACKEND": "gloo", "MP4X_HIER": "0"})
+    for names, sel in res.values():
+        assert "hier" not in names and sel != "hier"

@@ -35,7 +35,7 @@ def hier_gpu_body(comm, n):
 @pytest.mark.parametrize("n,piece", [(1 << 20, 1 << 20), (3 * (1 << 20) + 4096, 4 << 20)])
 def test_hier_allreduce_two_simulated_nodes(n, piece):
     res = run_spawn(4, hier_gpu_body, args=(n,), timeout=200,
-                    env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_HIER_MIN_BYTES": "0",
+                    env={"MP4X_SIM_NODE_SIZE": "2", "MP4X_HIER_MIN_BYTES": "0", "MP4X_HIER": "1",
                          "MP4X_HIER_PIECE_BYTES": str(piece)})
     for r, (ok_sum, ok_max, ok_avg, has_ipc, ipc_pieces, st, calls) in res.items():
         assert ok_sum and ok_max and ok_avg, (r, ok_sum, ok_max, ok_avg)

@@ -68,7 +68,7 @@ def test_universe_is_not_trivially_small():
 
 # Opt-in schedules (MP4X_AUTOTUNE_EXTRA=1, MP4X_DEVICE_ALGO, MP4X_AUTOTUNE_CANDIDATES or a tune
 # file): never autotune candidates by default, still covered by the cross-GPU module above.
-OPT_IN = {"rccl_c64", "rccl_c112", "ipc2p", "ipc2z_b64", "ipc2z_b128", "rhd"}
+OPT_IN = {"rccl_c64", "rccl_c112", "ipc2p", "ipc2z_b64", "ipc2z_b128", "rhd"}     # (+ hier: MP4X_HIER=1)
 
 
 def _engine(hier=False):
@@ -95,6 +95,12 @@ def test_default_decision_tree_has_at_most_six_schedules_per_size(monkeypatch):
         seen |= set(c)
     assert not seen & OPT_IN, seen & OPT_IN
     assert seen == {"rccl", "ipc1", "ipc2", "ipc2z", "ipc2w", "a2a"}, seen
+    # a multi-node layout does not add the node-aware schedule by default (opt-in: MP4X_HIER=1)
+    h = _engine(hier=True)
+    assert all("hier" not in h.allreduce_candidates(nb, Operators.Float.SUM, torch.float32)
+               for nb in (1 << 20, 1 << 30))
+    h._hier_auto = True
+    assert "hier" in h.allreduce_candidates(1 << 20, Operators.Float.SUM, torch.float32)
     monkeypatch.setenv("MP4X_AUTOTUNE_EXTRA", "1")
     extra = set()
     for nb in (4096, 1 << 20, 64 << 20, 1 << 30):

@@ -196,7 +196,7 @@ def test_hier_allreduce_cross_gpu(p, node):
     each "node", RCCL sub-communicators across them, 8 MiB pipelined pieces."""
     _need(p)
     res = run_spawn(p, _hier_fn, timeout=240, mode="multi",
-                    env={"MP4X_SIM_NODE_SIZE": str(node), "MP4X_HIER_PIECE_BYTES": str(8 << 20)})
+                    env={"MP4X_SIM_NODE_SIZE": str(node), "MP4X_HIER_PIECE_BYTES": str(8 << 20), "MP4X_HIER": "1"})
     for r, (ok, has_ipc, st, calls) in res.items():
         assert ok and has_ipc and st["ok"] and calls == 1, (r, ok, has_ipc, st, calls)
 
@@ -344,7 +344,9 @@ def test_autotuners_with_rccl_candidates_cross_gpu(p):
     opt-in schedules join (MP4X_AUTOTUNE_EXTRA=1: RCCL with pinned channel counts, the composite
     broadcast, ...) so every schedule the tuners know is probed here."""
     _need(p)
-    out = run_spawn(p, _tuners_fn, mode="multi", timeout=600, env={"MP4X_AUTOTUNE_EXTRA": "1"})
+    # (dry run: gloo stands in for RCCL, and the tuners keep its candidates only when asked)
+    env = {"MP4X_AUTOTUNE_EXTRA": "1", **({"MP4X_AUTOTUNE_GLOO": "1"} if DRY else {})}
+    out = run_spawn(p, _tuners_fn, mode="multi", timeout=600, env=env)
     want = {k.split(":")[0]: set() for ks in COVERS.values() for k in ks}
     for ks in COVERS["test_autotuners_with_rccl_candidates_cross_gpu"]:
         kind, algo = ks.split(":")
@@ -440,7 +442,7 @@ def _thread_fn(comm):
 
     def body(t):
         try:
-            torch.cuda.set_device(r)
+            torch.cuda.set_device(0 if DRY else r)       # (the dry run puts every rank on cuda:0)
             comm.setThreadId(t)
             x = _pattern(n, r * T + t)
             comm.allreduceArray(x, Operands.FLOAT_OPERAND(), Operators.Float.SUM, 0, n)
