@@ -339,10 +339,12 @@ def hash_rbk_supported(dtype: torch.dtype, op: int) -> bool:
 
 
 def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=None):
-    """K5h: (unique_keys, reduced_rows, counts) in hash-table order — open addressing + atomic
-    combine (SUM / MAX / MIN of f32 / f64 / i32 / i64 rows).  Float sums combine in arrival order
-    (exact for integer-valued data).  Returns None when a key equals -1 (the table's EMPTY marker):
-    the caller takes the sort path (:func:`reduce_by_key`)."""
+    """K5h (csrc/kernels/sparse_hash.hip): (unique_keys, reduced_rows, counts) with the keys in
+    hash-table order — one hashing pass finds the runs (instead of the sort path's radix sort of
+    the 64-bit keys), a counting sort groups the rows, and the sort path's segmented reduce
+    combines them in input order (runs up to 64 rows: the same values, bit for bit).  Every
+    reduction except the FIRST rule.  Returns None when a key equals -1 (the table's EMPTY
+    marker): the caller takes the sort path (:func:`reduce_by_key`)."""
     _dev_check(keys, vals)
     n = keys.numel()
     if keys.dtype != torch.int64 or vals.dim() not in (1, 2) or vals.shape[0] != n:
@@ -353,13 +355,15 @@ def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=N
     dim = 1 if vals.dim() == 1 else int(vals.shape[1])
     lib = native.hip()
     sb = lib.mp4x_hash_rbk_scratch_bytes(n)
-    scratch = torch.empty(sb, dtype=torch.uint8, device=dev)
+    scratch = torch.empty(sb + 256, dtype=torch.uint8, device=dev)
+    sp = scratch.data_ptr()
+    sp += (-sp) % 256                                       # the native layout is 256-byte aligned
     m_flag = torch.empty(2, dtype=torch.int64, device=dev)
     out_keys = torch.empty(n, dtype=torch.int64, device=dev)
     out_vals = torch.empty_like(vals)
     out_count = torch.empty(n, dtype=torch.int32, device=dev)
     check(lib.mp4x_hash_reduce_by_key(int(dtype_of_torch(vals.dtype)), int(op), keys.data_ptr(), n, vals.data_ptr(),
-                                      dim, scratch.data_ptr(), sb, out_keys.data_ptr(), out_vals.data_ptr(),
+                                      dim, sp, sb, out_keys.data_ptr(), out_vals.data_ptr(),
                                       out_count.data_ptr(), m_flag.data_ptr(), stream_ptr(stream)),
           "mp4x_hash_reduce_by_key")
     m, flag = m_flag.tolist()

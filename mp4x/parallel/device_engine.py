@@ -335,9 +335,9 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
         table, err = None, None
         path = os.environ.get("MP4X_TUNE_FILE")
         topo = None
-        if self.rank == 0 or not shared:
-            topo = self._topology()
-            if not path and tiers.auto_enabled():
+        if (self.rank == 0 or not shared) and (path or tiers.auto_enabled()):
+            topo = self._topology()            # (the xGMI probe runs only when a table is in play)
+            if not path:
                 path = tiers.tune_path(topo)
             if path and os.path.exists(path):
                 try:

@@ -1,6 +1,6 @@
 """K5h, the hash reduce-by-key (csrc/kernels/sparse_hash.hip, VERDICT r5 Next #6): exact against
 the deterministic sort path (K5) on integer-valued rows, for SUM / MAX / MIN of f32 / f64 / i32 /
-i64, on the BASELINE config-4 shape (the rows one owner receives at 8 ranks: 200k keys x float[64]
+i64, bit-identical on random floats (both combine in input order), on the BASELINE config-4 shape (the rows one owner receives at 8 ranks: 200k keys x float[64]
 per rank, half of them shared) and on small / odd shapes; a key equal to the table's EMPTY
 marker (-1) makes it decline (the caller takes the sort path)."""
 import pytest
@@ -44,6 +44,22 @@ def test_hash_matches_sort_path(dtype, op):
         assert torch.equal(hk, sk)
         assert torch.equal(hc, sc)
         assert torch.equal(hv, sv), (dtype, op, keys.numel(), (hv != sv).sum().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float64])
+def test_hash_is_bit_identical_to_sort_on_random_floats(dtype):
+    """Rows combine in input order in both paths (runs up to 64 rows), through the same segmented
+    reduce: random (non-integer) floats give the same bits, for SUM and PROD."""
+    from mp4x.ops.device_ops import hash_reduce_by_key, reduce_by_key
+    g = torch.Generator(device="cuda").manual_seed(3)
+    for n, dim, nk in ((200_000, 64, 60_000), (50_000, 7, 3000), (4096, 16, 64)):
+        keys = torch.randint(0, nk, (n,), device="cuda", generator=g) * 1_000_003
+        rows = torch.randn(n, dim, device="cuda", generator=g).to(dtype)
+        for op in (0, 3):
+            hk, hv, hc = _sorted(*hash_reduce_by_key(keys, rows, op))
+            sk, sv, sc = reduce_by_key(keys, rows, op)
+            assert torch.equal(hk, sk) and torch.equal(hc, sc)
+            assert torch.equal(hv.view(torch.uint8), sv.view(torch.uint8)), (dtype, n, op)
 
 
 def test_empty_marker_key_declines():
