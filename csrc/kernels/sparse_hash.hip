@@ -26,8 +26,8 @@
 // Differences from the sort path (why it stays opt-in): the output keys come in table order, not
 // ascending, and a run longer than 64 rows combines in scatter order (float SUM / PROD of such a
 // key is then not bit-reproducible; integer-valued data and MAX / MIN are exact either way).
-// MP4X_FIRST (K8, the first row in rank order) is not served.  A key equal to -1 (the EMPTY
-// marker) makes the call report it (flag) and the caller takes the sort path.
+// MP4X_FIRST (K8, the first row in rank order) is not served.  Rows whose key equals -1 (the
+// table's EMPTY marker) never enter the table: they are counted aside and form one extra run.
 #include <rocprim/device/device_scan.hpp>
 
 #include "common.hpp"
@@ -53,15 +53,21 @@ __device__ __forceinline__ uint64_t hash_mix(uint64_t k) {   // splitmix64 final
   return k;
 }
 
+// The side run of rows keyed -1 (the EMPTY marker): its row count and, once compacted, its run.
+struct SideRun {
+  int32_t rows;
+  int32_t u;
+};
+
 __global__ __launch_bounds__(kBlock) void k_hash_insert(const int64_t* __restrict__ keys, int64_t n,
                                                         unsigned long long* __restrict__ tkeys,
                                                         int32_t* __restrict__ tcount, uint64_t mask,
-                                                        int32_t* __restrict__ row_slot, int32_t* __restrict__ flag) {
+                                                        int32_t* __restrict__ row_slot, SideRun* __restrict__ side) {
   const int64_t nthr = (int64_t)gridDim.x * kBlock;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
     const unsigned long long k = (unsigned long long)keys[i];
     if (k == kHashEmpty) {
-      atomicOr(flag, 1);
+      atomicAdd(&side->rows, 1);
       row_slot[i] = -1;
       continue;
     }
@@ -85,9 +91,15 @@ __global__ __launch_bounds__(kBlock) void k_hash_insert(const int64_t* __restric
 __global__ __launch_bounds__(kBlock) void k_hash_compact(const unsigned long long* __restrict__ tkeys,
                                                          const int32_t* __restrict__ tcount, int64_t nslots,
                                                          int32_t* __restrict__ tidx, int32_t* __restrict__ run_len,
-                                                         unsigned long long* __restrict__ counter) {
+                                                         unsigned long long* __restrict__ counter,
+                                                         SideRun* __restrict__ side) {
   __shared__ int s_pre[kBlock];
   __shared__ unsigned long long s_base;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && side->rows > 0) {     // the side run, if any
+    const int32_t u = (int32_t)atomicAdd(counter, 1ull);
+    side->u = u;
+    run_len[u] = side->rows;
+  }
   const int64_t tile = (int64_t)blockIdx.x * kBlock * kCompactPer;
   int mine = 0;
 #pragma unroll
@@ -122,12 +134,11 @@ __global__ __launch_bounds__(kBlock) void k_hash_scatter(const int64_t* __restri
                                                          const int32_t* __restrict__ tidx,
                                                          const int64_t* __restrict__ starts,
                                                          int32_t* __restrict__ cursor, int64_t* __restrict__ perm,
-                                                         int64_t* __restrict__ sk) {
+                                                         int64_t* __restrict__ sk, const SideRun* __restrict__ side) {
   const int64_t nthr = (int64_t)gridDim.x * kBlock;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
     const int32_t s = row_slot[i];
-    if (s < 0) continue;
-    const int32_t u = tidx[s];
+    const int32_t u = s < 0 ? side->u : tidx[s];        // every row lands in a run: n positions in all
     const int64_t pos = starts[u] + atomicAdd(&cursor[u], 1);
     perm[pos] = i;
     sk[pos] = keys[i];
@@ -173,9 +184,9 @@ size_t scan_temp_bytes(int64_t n) {
 }
 
 // The scratch layout (every part 256-byte aligned): table keys, slot counts, slot -> run, the
-// row -> slot map, run lengths, run cursors, run starts, perm, sorted keys, scan temp.
+// row -> slot map, run lengths, run cursors, the side run, run starts, perm, sorted keys, scan temp.
 struct Layout {
-  size_t tkeys, tcount, tidx, row_slot, run_len, cursor, starts, perm, sk, temp, total, temp_bytes;
+  size_t tkeys, tcount, tidx, row_slot, run_len, cursor, side, starts, perm, sk, temp, total, temp_bytes;
   int64_t t;
 };
 
@@ -189,6 +200,7 @@ Layout layout(int64_t n) {
   L.row_slot = o; o += align256((size_t)n * 4);
   L.run_len = o;  o += align256((size_t)n * 4);
   L.cursor = o;   o += align256((size_t)n * 4);
+  L.side = o;     o += 256;
   L.starts = o;   o += align256((size_t)n * 8);
   L.perm = o;     o += align256((size_t)n * 8);
   L.sk = o;       o += align256((size_t)n * 8);
@@ -218,8 +230,8 @@ extern "C" int mp4x_hash_rbk_supported(int dtype, int op) {
 }
 
 // keys[n], vals[n][dim] -> out_keys[m] (table order), out_vals[m][dim], out_count[m] (optional);
-// m_flag[0] = m and m_flag[1] = 1 when a key equal to -1 was seen (result invalid: use the sort
-// path), both written on the device (stream-ordered).  out_* must hold n rows.
+// m_flag[0] = m, written on the device (stream-ordered; m_flag[1] is zeroed).  out_* must hold
+// n rows.
 extern "C" int mp4x_hash_reduce_by_key(int dtype, int op, const int64_t* keys, int64_t n, const void* vals, int64_t dim,
                                        void* scratch, size_t scratch_bytes, int64_t* out_keys, void* out_vals,
                                        int32_t* out_count, int64_t* m_flag, void* stream) {
@@ -238,23 +250,23 @@ extern "C" int mp4x_hash_reduce_by_key(int dtype, int op, const int64_t* keys, i
   auto* perm = (int64_t*)(p + L.perm);
   auto* sk = (int64_t*)(p + L.sk);
   auto* counter = (unsigned long long*)m_flag;            // m_flag[0]: the run counter IS m
-  auto* flag = (int32_t*)(m_flag + 1);
+  auto* side = (SideRun*)(p + L.side);
   if (hipError_t e = hipMemsetAsync(tkeys, 0xFF, (size_t)L.t * 8, st)) return (int)e;
   if (hipError_t e = hipMemsetAsync(tcount, 0, (size_t)L.t * 4, st)) return (int)e;
-  if (hipError_t e = hipMemsetAsync(p + L.run_len, 0, L.starts - L.run_len, st)) return (int)e;  // run_len, cursor
+  if (hipError_t e = hipMemsetAsync(p + L.run_len, 0, L.starts - L.run_len, st)) return (int)e;  // run_len, cursor, side
   if (hipError_t e = hipMemsetAsync(m_flag, 0, 16, st)) return (int)e;
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, tkeys, tcount,
-                     (uint64_t)(L.t - 1), row_slot, flag);
+                     (uint64_t)(L.t - 1), row_slot, side);
   const int64_t tile = (int64_t)kBlock * kCompactPer;
   hipLaunchKernelGGL(k_hash_compact, dim3((unsigned)((L.t + tile - 1) / tile)), dim3(kBlock), 0, st,
-                     (const unsigned long long*)tkeys, (const int32_t*)tcount, L.t, tidx, run_len, counter);
+                     (const unsigned long long*)tkeys, (const int32_t*)tcount, L.t, tidx, run_len, counter, side);
   size_t tb = L.temp_bytes;
   if (hipError_t e = rocprim::exclusive_scan(p + L.temp, tb, (const int32_t*)run_len, starts, (int64_t)0, (size_t)n,
                                              rocprim::plus<int64_t>(), st))
     return (int)e;
   hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, (const int32_t*)row_slot,
-                     (const int32_t*)tidx, (const int64_t*)starts, cursor, perm, sk);
+                     (const int32_t*)tidx, (const int64_t*)starts, cursor, perm, sk, (const SideRun*)side);
   hipLaunchKernelGGL(k_hash_order, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, (const int64_t*)starts,
                      (const int32_t*)run_len, (const unsigned long long*)counter, perm);
   if (int e = (int)hipGetLastError()) return e;

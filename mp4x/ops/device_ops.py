@@ -343,8 +343,7 @@ def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=N
     hash-table order — one hashing pass finds the runs (instead of the sort path's radix sort of
     the 64-bit keys), a counting sort groups the rows, and the sort path's segmented reduce
     combines them in input order (runs up to 64 rows: the same values, bit for bit).  Every
-    reduction except the FIRST rule.  Returns None when a key equals -1 (the table's EMPTY
-    marker): the caller takes the sort path (:func:`reduce_by_key`)."""
+    reduction except the FIRST rule (then use :func:`reduce_by_key`)."""
     _dev_check(keys, vals)
     n = keys.numel()
     if keys.dtype != torch.int64 or vals.dim() not in (1, 2) or vals.shape[0] != n:
@@ -366,9 +365,7 @@ def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=N
                                       dim, sp, sb, out_keys.data_ptr(), out_vals.data_ptr(),
                                       out_count.data_ptr(), m_flag.data_ptr(), stream_ptr(stream)),
           "mp4x_hash_reduce_by_key")
-    m, flag = m_flag.tolist()
-    if flag & 0xFFFFFFFF:
-        return None
+    m = int(m_flag[0].item())
     return out_keys[:m], out_vals[:m], out_count[:m]
 
 

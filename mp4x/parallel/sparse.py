@@ -166,9 +166,7 @@ def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bit
         if vals is not None and RBK_MODE == "hash" and not getattr(op, "is_custom", False):
             from ..ops.device_ops import hash_rbk_supported, hash_reduce_by_key
             if hash_rbk_supported(vals.dtype, int(op.code)):
-                got = hash_reduce_by_key(keys, vals, int(op.code))
-                if got is not None:
-                    return got
+                return hash_reduce_by_key(keys, vals, int(op.code))
         return reduce_by_key(keys, vals, int(op.code) if vals is not None else 0, key_bits=key_bits)
     # CPU twin for the gloo test configuration only
     uk, inv, cnt = torch.unique(keys, sorted=True, return_inverse=True, return_counts=True)
