@@ -14,7 +14,7 @@
 //   insert   one lane per row: splitmix64 hash, linear probing, 64-bit CAS on an EMPTY slot
 //            (table >= 2n slots, power of two: an empty slot always exists); the slot's row count
 //            += 1 (an int atomic spread over the table) and the row's slot are kept
-//   compact  16 slots per lane, one atomic per BLOCK (LDS prefix over the block's lanes): every
+//   compact  4 slots per lane, one atomic per BLOCK (LDS prefix over the block's lanes): every
 //            occupied slot gets a dense run index u and its run length
 //   scan     exclusive sum of the run lengths (rocPRIM) -> run starts
 //   scatter  one lane per row: position = start[u] + (atomic cursor of u); perm / sorted keys
@@ -41,7 +41,7 @@ namespace mp4x {
 
 namespace {
 constexpr unsigned long long kHashEmpty = ~0ull;
-constexpr int kCompactPer = 16;            // slots per lane in k_hash_compact
+constexpr int kCompactPer = 4;             // slots per lane in k_hash_compact (>= 2 blocks per CU at 2n = 400k)
 constexpr int kOrderMax = 64;              // longest run whose rows are put in input order
 
 __device__ __forceinline__ uint64_t hash_mix(uint64_t k) {   // splitmix64 finalizer
@@ -183,10 +183,11 @@ size_t scan_temp_bytes(int64_t n) {
   return b;
 }
 
-// The scratch layout (every part 256-byte aligned): table keys, slot counts, slot -> run, the
-// row -> slot map, run lengths, run cursors, the side run, run starts, perm, sorted keys, scan temp.
+// The scratch layout (every part 256-byte aligned): table keys; then the zero-initialised block
+// (slot counts, run lengths, run cursors, the side run: ONE memset); slot -> run, the row -> slot
+// map, run starts, perm, sorted keys, scan temp.
 struct Layout {
-  size_t tkeys, tcount, tidx, row_slot, run_len, cursor, side, starts, perm, sk, temp, total, temp_bytes;
+  size_t tkeys, tcount, run_len, cursor, side, zero_end, tidx, row_slot, starts, perm, sk, temp, total, temp_bytes;
   int64_t t;
 };
 
@@ -196,11 +197,12 @@ Layout layout(int64_t n) {
   size_t o = 0;
   L.tkeys = o;    o += align256((size_t)L.t * 8);
   L.tcount = o;   o += align256((size_t)L.t * 4);
-  L.tidx = o;     o += align256((size_t)L.t * 4);
-  L.row_slot = o; o += align256((size_t)n * 4);
   L.run_len = o;  o += align256((size_t)n * 4);
   L.cursor = o;   o += align256((size_t)n * 4);
   L.side = o;     o += 256;
+  L.zero_end = o;
+  L.tidx = o;     o += align256((size_t)L.t * 4);
+  L.row_slot = o; o += align256((size_t)n * 4);
   L.starts = o;   o += align256((size_t)n * 8);
   L.perm = o;     o += align256((size_t)n * 8);
   L.sk = o;       o += align256((size_t)n * 8);
@@ -252,8 +254,7 @@ extern "C" int mp4x_hash_reduce_by_key(int dtype, int op, const int64_t* keys, i
   auto* counter = (unsigned long long*)m_flag;            // m_flag[0]: the run counter IS m
   auto* side = (SideRun*)(p + L.side);
   if (hipError_t e = hipMemsetAsync(tkeys, 0xFF, (size_t)L.t * 8, st)) return (int)e;
-  if (hipError_t e = hipMemsetAsync(tcount, 0, (size_t)L.t * 4, st)) return (int)e;
-  if (hipError_t e = hipMemsetAsync(p + L.run_len, 0, L.starts - L.run_len, st)) return (int)e;  // run_len, cursor, side
+  if (hipError_t e = hipMemsetAsync(p + L.tcount, 0, L.zero_end - L.tcount, st)) return (int)e;  // counts .. side
   if (hipError_t e = hipMemsetAsync(m_flag, 0, 16, st)) return (int)e;
   if (n == 0) return 0;
   hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, tkeys, tcount,
