@@ -141,7 +141,8 @@ struct StreamOrder {
   int32_t disabled;      // MP4X_TEST_NO_STREAM_ORDER=1: tests only (shows the guard has teeth)
   int32_t pad;
 };
-// 0, or MP4X_E_STREAM_SWITCH / a HIP error: see order.hip.
+// 0, or MP4X_E_STREAM_SWITCH / a HIP error: see order.hip (mp4x_order_enter: the caller knows the
+// stream is not being captured).
 extern "C" int mp4x_order_enter(StreamOrder* o, void* stream);
 
 struct IpcPtrs {

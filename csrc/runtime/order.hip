@@ -20,15 +20,19 @@
 // Contract (DESIGN.md §"Stream order"): a stream handed to a collective stays alive until the
 // communicator's next collective was issued (torch's pooled streams always do).  Graph capture:
 // the captured launches of one capture must all be on one stream (a switch inside a capture is
-// refused: MP4X_E_STREAM_SWITCH); a capture does not move the eager order, and replays are
-// ordered by the stream they are launched on, like any graph.
+// refused: MP4X_E_STREAM_SWITCH; callers that cannot rule a capture out pass capturing = -1 and
+// the status is queried); a capture does not move the eager order, and replays are ordered by the
+// stream they are launched on, like any graph.
 #include "ipc_common.hpp"
 
 using namespace mp4x;
 
-extern "C" int mp4x_order_enter(StreamOrder* o, void* stream) {
+// `capturing`: 0 = the caller knows the stream is not being captured (the fast paths checked it),
+// 1 = it is, -1 = unknown (queried here).  The steady state (same stream as the previous launch,
+// not capturing) is one compare.
+extern "C" int mp4x_order_enter_ex(StreamOrder* o, void* stream, int capturing) {
   if (!o) return 0;
-  if (o->have_last && o->last == stream) return 0;        // the steady state
+  if (capturing == 0 && o->have_last && o->last == stream) return 0;      // the steady state
   hipStream_t s = (hipStream_t)stream;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   unsigned long long id = 0;
@@ -36,6 +40,7 @@ extern "C" int mp4x_order_enter(StreamOrder* o, void* stream) {
     (void)hipGetLastError();
     return (int)e;
   }
+  if (cs != hipStreamCaptureStatusActive && o->have_last && o->last == stream) return 0;
   if (cs == hipStreamCaptureStatusActive) {
     if (o->cap_have && o->cap_id == id && o->cap_stream != stream) return MP4X_E_STREAM_SWITCH;
     o->cap_have = 1;
@@ -66,6 +71,8 @@ extern "C" int mp4x_order_enter(StreamOrder* o, void* stream) {
   o->have_last = 1;
   return 0;
 }
+
+extern "C" int mp4x_order_enter(StreamOrder* o, void* stream) { return mp4x_order_enter_ex(o, stream, 0); }
 
 // Release the guard's event (the communicator is closing; its streams were drained).
 extern "C" int mp4x_order_release(StreamOrder* o) {

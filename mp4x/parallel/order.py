@@ -29,6 +29,7 @@ from ..ops import native
 
 native.register_signatures({
     "mp4x_order_enter": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "mp4x_order_enter_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "mp4x_order_release": (ctypes.c_int, [ctypes.c_void_p]),
 })
 
@@ -60,12 +61,13 @@ class CommOrder:
         """Order ``stream`` (a raw hipStream_t; 0 = the null stream) after the communicator's
         previous launch.  Raises on a stream switch inside one graph capture."""
         s = self.s
-        if s.have_last and (s.last or 0) == stream:
+        cap = native.capturing_now()
+        if not cap and s.have_last and (s.last or 0) == stream:
             return
         f = self._enter
         if f is None:
-            f = self._enter = native.hip().mp4x_order_enter
-        rc = f(self.addr, stream)
+            f = self._enter = native.hip().mp4x_order_enter_ex
+        rc = f(self.addr, stream, 1 if cap else 0)
         if rc:
             if rc == STREAM_SWITCH:
                 from ..exceptions import Mp4jException

@@ -163,3 +163,46 @@ def test_without_the_guard_the_soak_fails():
     _record("no_guard_p2", out)
     assert any(o["bad"] or o["raised"] or any(o["words"]) for o in out.values()), out
     assert all(o["switches"] == 0 for o in out.values()), out       # the guard really was off
+
+
+def _capture_switch_fn(comm):
+    from mp4x import Operands, Operators
+    from mp4x.exceptions import Mp4jException
+    r, p = comm.getRank(), comm.getSlaveNum()
+    eng = comm.device
+    eng.ipc()
+    a = torch.ones(4096, device="cuda")
+    b = torch.ones(4096, device="cuda")
+    side = torch.cuda.Stream()
+    F, SUM = Operands.FLOAT_OPERAND(), Operators.Float.SUM
+
+    def step():
+        comm.allreduceArray(a, F, SUM, 0, a.numel())
+        side.wait_stream(torch.cuda.current_stream())        # fork a second stream ...
+        with torch.cuda.stream(side):
+            comm.allreduceArray(b, F, SUM, 0, b.numel())     # ... and issue the next collective on it
+        torch.cuda.current_stream().wait_stream(side)
+    raised = None
+    try:
+        eng.capture(step)
+    except Mp4jException as e:
+        raised = str(e)
+    except RuntimeError as e:        # (torch reporting the capture the exception invalidated)
+        raised = "runtime: " + str(e)
+    torch.cuda.synchronize()
+    comm.barrier()
+    x = torch.full((4096,), float(r + 1), device="cuda")      # the job goes on, exact
+    comm.allreduceArray(x, F, SUM, 0, x.numel())
+    torch.cuda.synchronize()
+    return raised, bool((x == p * (p + 1) / 2).all())
+
+
+def test_a_stream_switch_inside_one_capture_is_refused():
+    """Inside one graph capture the guard cannot join a forked stream to the previous launch (an
+    eager event is not part of the graph): the second collective on another stream of the same
+    capture raises, on every rank, and eager calls after it are exact (warm-up calls of the same
+    step, eager, switch streams legally)."""
+    out = run_spawn(2, _capture_switch_fn, timeout=240)
+    for r, (raised, ok) in out.items():
+        assert raised and "ONE stream" in raised, (r, raised)
+        assert ok, r
