@@ -179,9 +179,11 @@ def _capture_switch_fn(comm):
     def step():
         comm.allreduceArray(a, F, SUM, 0, a.numel())
         side.wait_stream(torch.cuda.current_stream())        # fork a second stream ...
-        with torch.cuda.stream(side):
-            comm.allreduceArray(b, F, SUM, 0, b.numel())     # ... and issue the next collective on it
-        torch.cuda.current_stream().wait_stream(side)
+        try:
+            with torch.cuda.stream(side):
+                comm.allreduceArray(b, F, SUM, 0, b.numel())  # ... and issue the next collective on it
+        finally:
+            torch.cuda.current_stream().wait_stream(side)     # (joined back: the capture ends cleanly)
     raised = None
     try:
         eng.capture(step)
