@@ -2,7 +2,9 @@
 """Where the host time of a small device allreduce goes: p processes on GPU 0, the same 4 KiB
 f32 SUM issued through each layer in turn (public API with its native latency fast path ->
 the public API's full Python path -> DeviceEngine -> IpcAllreduce -> the bare ctypes launch),
-wall time per call (MAX over ranks).  Rehearsal numbers: protocol
+wall time per call (MAX over ranks).  Also the public call inside a stream context, on one
+stream or alternating between two: the difference is the cost of the communicator's
+stream-order join (an event on the previous stream, a wait on the new one).  Rehearsal numbers: protocol
 and host overhead, not xGMI latency.
 
     python bench/latency_layers.py --procs 2 --iters 3000 [--bytes 4096]
@@ -50,7 +52,20 @@ def worker(port, q, nbytes, iters):
             comm.allreduceArray(x, opnd, op, 0, n)
         finally:
             comm._fast_ar = fast_memo
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    flip = [0]
+
+    def api_stream(alternate):
+        # the public call inside a stream context: the same stream every call, or alternating
+        # between two (every call then joins the other stream: the stream-order guard's switch)
+        def fn():
+            i = flip[0] = flip[0] + 1 if alternate else 0
+            with torch.cuda.stream(streams[i & 1]):
+                comm.allreduceArray(x, opnd, op, 0, n)
+        return fn
     layers = {"api": lambda: comm.allreduceArray(x, opnd, op, 0, n),
+              "api_stream_ctx_same": api_stream(False),
+              "api_stream_ctx_alternating": api_stream(True),
               "api_full_path": api_full,
               "engine": lambda: eng.allreduce(x, 0, n, op, opnd),
               "ipc": lambda: inst.allreduce(x, fop, algo=ipcm.ONESHOT),
@@ -89,7 +104,8 @@ def main():
     m.stop(timeout=5)
     us = {k: round(max(res[r][k] for r in res), 2) for k in res[0]}
     print(json.dumps({"procs_on_one_gpu": a.procs, "bytes": a.bytes, "watchdog": os.environ.get("MP4X_WATCHDOG", "1"),
-                      "us_per_call_max_rank": us, "api_minus_raw_launch_us": round(us["api"] - us["raw_launch"], 2)}))
+                      "us_per_call_max_rank": us, "api_minus_raw_launch_us": round(us["api"] - us["raw_launch"], 2),
+                      "stream_switch_us": round(us["api_stream_ctx_alternating"] - us["api_stream_ctx_same"], 2)}))
 
 
 if __name__ == "__main__":
