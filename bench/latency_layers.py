@@ -64,12 +64,15 @@ def worker(port, q, nbytes, iters):
                 comm.allreduceArray(x, opnd, op, 0, n)
         return fn
     layers = {"api": lambda: comm.allreduceArray(x, opnd, op, 0, n),
-              "api_stream_ctx_same": api_stream(False),
-              "api_stream_ctx_alternating": api_stream(True),
               "api_full_path": api_full,
               "engine": lambda: eng.allreduce(x, 0, n, op, opnd),
               "ipc": lambda: inst.allreduce(x, fop, algo=ipcm.ONESHOT),
-              "raw_launch": raw}
+              "raw_launch": raw,
+              # last: work on two more streams changes how this process's launches are scheduled
+              # from then on (bench/stream_switch.py)
+              "api_stream_ctx_same": api_stream(False),
+              "api_stream_ctx_alternating": api_stream(True),
+              "api_after_streams": lambda: comm.allreduceArray(x, opnd, op, 0, n)}
     out = {}
     for name, fn in layers.items():
         for _ in range(50):
