@@ -17,8 +17,10 @@
 // previous collective included.  No cycle can form: the old stream's tail only waits for work
 // that was queued before this call.
 //
-// Contract (DESIGN.md §"Stream order"): a stream handed to a collective stays alive until the
-// communicator's next collective was issued (torch's pooled streams always do).  Graph capture:
+// Contract (DESIGN.md §"Stream order"): a stream handed to a collective should stay alive until
+// the communicator's next collective was issued (torch's pooled streams always do); if it was
+// destroyed, the event cannot be recorded there and the join falls back to a device-wide
+// synchronisation (ROCclr validates stream handles and returns an error).  Graph capture:
 // the captured launches of one capture must all be on one stream (a switch inside a capture is
 // refused: MP4X_E_STREAM_SWITCH; callers that cannot rule a capture out pass capturing = -1 and
 // the status is queried); a capture does not move the eager order, and replays are ordered by the
@@ -57,11 +59,15 @@ extern "C" int mp4x_order_enter_ex(StreamOrder* o, void* stream, int capturing) 
       }
       o->ev = ev;
     }
-    if (hipError_t e = hipEventRecord((hipEvent_t)o->ev, (hipStream_t)o->last)) {
+    if (hipEventRecord((hipEvent_t)o->ev, (hipStream_t)o->last) != hipSuccess) {
+      // the previous stream is gone (destroyed by its owner since the last collective): order the
+      // new launch after everything queued on the device instead — slow, but never unordered
       (void)hipGetLastError();
-      return (int)e;
-    }
-    if (hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)o->ev, 0)) {
+      if (hipError_t e = hipDeviceSynchronize()) {
+        (void)hipGetLastError();
+        return (int)e;
+      }
+    } else if (hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)o->ev, 0)) {
       (void)hipGetLastError();
       return (int)e;
     }
