@@ -79,6 +79,26 @@ class _TunedTable(dict):
         self._bump()
         super().update(*a, **k)
 
+    def pinned(self, key: tuple):
+        """The schedule for ``key`` = (..., size class): the pin of that class, else — between two
+        measured classes of the same (kind, dtype, op) that pinned the SAME schedule — that
+        schedule (it won on both sides; the tier sweep visits 4 KiB, 64 KiB, 256 KiB, ... so the
+        classes in between follow the measurements instead of the model defaults), else None."""
+        hit = self.get(key)
+        if hit is not None or not self:
+            return hit
+        pre, cls = key[:-1], key[-1]
+        lo = hi = None
+        for k, v in self.items():
+            if len(k) != len(key) or k[:-1] != pre:
+                continue
+            c = k[-1]
+            if c < cls and (lo is None or c > lo[0]):
+                lo = (c, v)
+            elif c > cls and (hi is None or c < hi[0]):
+                hi = (c, v)
+        return lo[1] if lo is not None and hi is not None and lo[1] == hi[1] else None
+
     def setdefault(self, k, d=None):
         self._bump()
         return super().setdefault(k, d)
@@ -310,7 +330,7 @@ class AutotuneMixin:
         None.  Only for unforced, uncaptured calls (a capture keeps the tier logic)."""
         if not self._tuned or self.algo not in ("", "auto") or (view.is_cuda and capturing_now()):
             return None
-        return self._tuned.get(self._rsag_key(kind, view, op))
+        return self._tuned.pinned(self._rsag_key(kind, view, op))
 
     def autotune_reduce(self, like: torch.Tensor, operator, root: int = 0, iters: int = 3) -> Dict[str, float]:
         """``reduce`` schedules timed side by side (RCCL ``ncclReduce``; ``ipc`` = the IPC two-shot

@@ -947,7 +947,8 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             return forced
         self._select_tuned = False
         if kind == "allreduce" and op is not None and forced in ("", "auto") and self._tuned:
-            t = self._tuned.get(_tune_key(dtype, op, nbytes))
+            tt = self._tuned
+            t = tt.pinned(_tune_key(dtype, op, nbytes)) if hasattr(tt, "pinned") else tt.get(_tune_key(dtype, op, nbytes))
             if t is not None and self._algo_valid(t, op, dtype, nbytes):
                 self._select_tuned = True
                 return t
@@ -1473,7 +1474,7 @@ class DeviceEngine(AutotuneMixin, ScheduleMixin, RootedMixin):
             return "ipc" if self.ipc_enabled and (op is None or self._ipc_ok(op, whole.dtype, 16)) else None
         if self.algo not in ("", "auto"):
             return None
-        t = self._tuned.get(self._rsag_key(kind, whole, op)) if self._tuned else None
+        t = self._tuned.pinned(self._rsag_key(kind, whole, op)) if self._tuned else None
         if t is None and self._dm_large_ok(whole) and (op is None or self._ipc_ok(op, whole.dtype, 16)):
             return "ipc"     # no RCCL underneath (see _dm_large_ok): the piecewise IPC kernels
         if t is None and op is not None and not self.rccl_ok(op, whole.dtype) and whole.is_cuda and \

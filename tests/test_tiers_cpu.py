@@ -102,3 +102,25 @@ def test_tune_store_is_loaded_by_the_next_job_with_the_same_key(tmp_path):
     env_off = dict(env, MP4X_TUNE_AUTO="0")
     res5, code, _ = run_ranks(2, _tune_job, args=("read",), timeout=120, env=env_off)
     assert code == 0 and all(not r["loaded"] and r["path"] is None for r in res5.values())
+
+
+def test_pins_between_measured_classes_follow_the_measurement():
+    """A size class the tier sweep did not visit takes the schedule its two measured neighbours
+    (same kind, dtype, op) both pinned; neighbours that disagree leave it to the tier defaults."""
+    from mp4x.parallel.autotune import _TunedTable
+    t = _TunedTable()
+    f32, f64 = torch.float32, torch.float64
+    t[(f32, 0, 12)] = "ipc1"           # 4 KiB
+    t[(f32, 0, 16)] = "ipc1"           # 64 KiB
+    t[(f32, 0, 18)] = "ipc2"           # 256 KiB
+    t[("reduce", f32, 0, 20)] = "rccl"
+    t[("reduce", f32, 0, 24)] = "rccl"
+    assert t.pinned((f32, 0, 14)) == "ipc1"          # between two ipc1 pins
+    assert t.pinned((f32, 0, 17)) is None            # ipc1 below, ipc2 above: the defaults decide
+    assert t.pinned((f32, 0, 18)) == "ipc2"          # an exact pin
+    assert t.pinned((f32, 0, 10)) is None            # below every measurement
+    assert t.pinned((f32, 0, 30)) is None            # above every measurement
+    assert t.pinned((f64, 0, 14)) is None            # another dtype
+    assert t.pinned((f32, 1, 14)) is None            # another op
+    assert t.pinned(("reduce", f32, 0, 22)) == "rccl"
+    assert t.pinned(("broadcast", f32, 0, 22)) is None
