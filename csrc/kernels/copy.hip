@@ -70,9 +70,61 @@ __global__ __launch_bounds__(kBlock) void k_gather_rows(char* __restrict__ out, 
   }
 }
 
+// Sparse exchanges (mp4x/parallel/sparse.py): the ragged all-to-all-v / all-gather-v of the map
+// collectives stage a rank's rows and keys in its IPC buffer as two regions, rows (V 16-byte
+// vectors each) and keys as 16-byte {key, 0} vectors, so one copy-plan kernel moves both with
+// 16-byte pulls whatever the row counts, and the received rows land contiguous (no unpack pass).
+// Stage: one grid-stride over the n * V row vectors then the n key vectors (no index division).
+__global__ __launch_bounds__(kBlock) void k_stage_split(const int64_t* __restrict__ keys, const u32x4* __restrict__ vals,
+                                                        int64_t n, int64_t V, u32x4* __restrict__ dv,
+                                                        u32x4* __restrict__ dk) {
+  const int64_t nv = n * V, total = nv + n;
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total; i += nthr) {
+    if (i < nv) {
+      dv[i] = vals[i];
+    } else {
+      const uint64_t k = (uint64_t)keys[i - nv];
+      dk[i - nv] = u32x4{(uint32_t)k, (uint32_t)(k >> 32), 0u, 0u};
+    }
+  }
+}
+
+// The received {key, 0} vectors -> int64 keys.
+__global__ __launch_bounds__(kBlock) void k_keys_from16(const u32x4* __restrict__ k16, int64_t n,
+                                                        int64_t* __restrict__ keys) {
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
+    const u32x4 x = k16[i];
+    keys[i] = (int64_t)(((uint64_t)x[1] << 32) | x[0]);
+  }
+}
+
 }  // namespace mp4x
 
 using namespace mp4x;
+
+// keys[n] (int64) + vals[n][row_bytes] (row_bytes a multiple of 16, 16-byte aligned; NULL when
+// row_bytes == 0) -> dst_vals[n][row_bytes] + dst_keys16[n][16].
+extern "C" int mp4x_stage_split(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, void* dst_vals,
+                                void* dst_keys16, void* stream) {
+  if (n <= 0) return 0;
+  if ((row_bytes & 15) || row_bytes < 0 || ((uintptr_t)keys & 7) || !keys || !dst_keys16 ||
+      ((uintptr_t)dst_keys16 & 15) || (row_bytes && (!vals || !dst_vals || (((uintptr_t)vals | (uintptr_t)dst_vals) & 15))))
+    return MP4X_E_BADARG;
+  const int64_t V = row_bytes / 16;
+  hipLaunchKernelGGL(k_stage_split, dim3(grid_for(n * (V + 1), 2)), dim3(kBlock), 0, (hipStream_t)stream, keys,
+                     (const u32x4*)vals, n, V, (u32x4*)dst_vals, (u32x4*)dst_keys16);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp4x_keys_from16(const void* keys16, int64_t n, int64_t* keys, void* stream) {
+  if (n <= 0) return 0;
+  if (!keys16 || !keys || ((uintptr_t)keys16 & 15) || ((uintptr_t)keys & 7)) return MP4X_E_BADARG;
+  hipLaunchKernelGGL(k_keys_from16, dim3(grid_for(n, 2)), dim3(kBlock), 0, (hipStream_t)stream,
+                     (const u32x4*)keys16, n, keys);
+  return (int)hipGetLastError();
+}
 
 extern "C" int mp4x_segment_copy(void* dst, const void* src, const int64_t* dev_table, int nseg, int64_t max_len,
                                  void* stream) {

@@ -329,6 +329,34 @@ def run_starts(sorted_keys: torch.Tensor, stream=None):
     return starts, nruns
 
 
+def stage_split(keys: torch.Tensor, vals: Optional[torch.Tensor], vals_ptr: int, keys16_ptr: int,
+                stream=None) -> None:
+    """Sparse exchange staging (see mp4x/parallel/sparse.py): rows of ``vals`` [n, ...] copied to
+    device address ``vals_ptr`` and ``keys`` [n] written as 16-byte {key, 0} vectors at
+    ``keys16_ptr``, one launch (csrc/kernels/copy.hip k_stage_split)."""
+    n = keys.shape[0]
+    if n == 0:
+        return
+    _dev_check(keys, vals)
+    rb = 0 if vals is None else vals[0].numel() * vals.element_size()
+    if keys.dtype != torch.int64 or not keys.is_contiguous() or rb % 16 or \
+            (vals is not None and (vals.shape[0] != n or not vals.is_contiguous())):
+        raise ValueError("stage_split: contiguous int64 keys[n], rows of whole 16-byte vectors")
+    check(native.hip().mp4x_stage_split(keys.data_ptr(), vals.data_ptr() if vals is not None else None, n, rb,
+                                        vals_ptr if rb else None, keys16_ptr, stream_ptr(stream)), "mp4x_stage_split")
+
+
+def keys_from16(k16: torch.Tensor, stream=None) -> torch.Tensor:
+    """int64 keys of a uint8 [m * 16] region of {key, 0} vectors (the inverse of the key half of
+    :func:`stage_split`)."""
+    _dev_check(k16)
+    m = k16.numel() // 16
+    keys = torch.empty(m, dtype=torch.int64, device=k16.device)
+    if m:
+        check(native.hip().mp4x_keys_from16(k16.data_ptr(), m, keys.data_ptr(), stream_ptr(stream)), "mp4x_keys_from16")
+    return keys
+
+
 def hash_rbk_supported(dtype: torch.dtype, op: int) -> bool:
     """Does the hash reduce-by-key (K5h, csrc/kernels/sparse_hash.hip) serve (dtype, op)?"""
     try:

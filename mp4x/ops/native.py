@@ -63,6 +63,8 @@ _HIP_SIGS = {
     "mp4x_run_starts": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_segment_reduce_rows": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,
                                          c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mp4x_stage_split": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_void_p, c_void_p]),
+    "mp4x_keys_from16": (c_int, [c_void_p, c_int64, c_void_p, c_void_p]),
     "mp4x_hash_rbk_scratch_bytes": (c_size_t, [c_int64]),
     "mp4x_hash_rbk_supported": (c_int, [c_int, c_int]),
     "mp4x_hash_reduce_by_key": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_size_t,

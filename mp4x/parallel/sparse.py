@@ -238,19 +238,23 @@ def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
 
 # ------------------------------------------------------------------ IPC data plane for the sparse path
 # The ragged exchanges of the map collectives as ONE copy-plan kernel each over the IPC mesh
-# (csrc/runtime/ipc.hip k_ipc_copy_plan): keys and rows travel together as fixed-width records
-# (row bytes | int64 key | 8 pad bytes, a 16-byte multiple).  All-to-all-v: every rank stages
-# its owner-sorted records into its own IPC buffer, one stage item per destination, and pulls
-# its block from every peer at once (every xGMI link busy; no RCCL all_to_all).  All-gather-v:
-# every rank stages its owned result and pulls every peer's.  The grid is sized from the full
-# count matrix, which every rank knows, so every rank launches the same grid.
+# (csrc/runtime/ipc.hip k_ipc_copy_plan).  Every rank stages its rows and keys in its own IPC
+# buffer as two regions — the rows (16-byte multiples), then the keys as 16-byte {key, 0} vectors
+# from a rank-independent offset — so every block is whole 16-byte vectors whatever the row
+# counts; the receiver pulls rows straight into a contiguous row block and keys into a key block
+# (one small pass turns those into int64 keys).  All-to-all-v: each rank pulls its block from
+# every peer at once (every xGMI link busy; no RCCL all_to_all).  All-gather-v: every rank pulls
+# every peer's owned result.  The staging copy runs right before the plan, on the stream joined to
+# the communicator's order: the previous collective of the instance has finished on this rank, and
+# its end barrier means every peer has finished reading this buffer too.  The grid is sized from
+# the full count matrix, which every rank knows, so every rank launches the same grid.
 _SPARSE_IPC = os.environ.get("MP4X_SPARSE_IPC", "1") == "1"
 
 
-def _rec_width(vals: Optional[torch.Tensor]) -> int:
-    """Record bytes (row bytes + 16), or 0 when rows are not a whole number of 16-byte vectors."""
+def _row_bytes(vals: Optional[torch.Tensor]) -> int:
+    """Row bytes (0 without rows), or -1 when rows are not a whole number of 16-byte vectors."""
     rb = 0 if vals is None else int(np.prod(vals.shape[1:], dtype=np.int64)) * vals.element_size()
-    return rb + 16 if rb % 16 == 0 else 0
+    return rb if rb % 16 == 0 else -1
 
 
 def _ipc_inst(engine, need_bytes: int):
@@ -268,57 +272,53 @@ def _sparse_ipc_ok(engine, keys: torch.Tensor) -> bool:
         engine.coll.__class__.__name__ == "TorchColl" and not capturing_now() and engine.ipc() is not None
 
 
-def _pack_records(keys: torch.Tensor, vals: Optional[torch.Tensor], wb: int) -> torch.Tensor:
-    n = keys.shape[0]
-    rec = torch.empty((n, wb), dtype=torch.uint8, device=keys.device)
-    rb = wb - 16
-    if n == 0:
-        return rec
-    if rb:
-        rec[:, :rb] = vals.contiguous().view(n, -1).view(torch.uint8).view(n, rb)
-    rec[:, rb:rb + 8] = keys.contiguous().view(torch.uint8).view(n, 8)
-    return rec
-
-
-def _unpack_records(rec: torch.Tensor, like_vals: Optional[torch.Tensor], wb: int):
-    m = rec.shape[0]
-    rb = wb - 16
-    keys = rec[:, rb:rb + 8].contiguous().view(torch.int64).view(-1)
-    vals = None
-    if like_vals is not None:
-        vals = rec[:, :rb].contiguous().view(like_vals.dtype).view((m,) + tuple(like_vals.shape[1:]))
-    return keys, vals
+def _split_exchange(engine, keys, vals, rb: int, nmax: int, blocks, grid_rows: int):
+    """Stage (keys, rows) in this rank's buffer (rows at vector 0, keys at ``nmax * V``) and run
+    one copy plan; ``blocks`` = [(peer, src_row, rows)] pulled in order; ``grid_rows`` = the
+    largest block of ANY rank (the plan's grid must be rank-independent).  Returns the received
+    (keys, rows), or None when the largest rank's payload does not fit (rank-independent)."""
+    from ..ops.device_ops import keys_from16, stage_split
+    inst = _ipc_inst(engine, nmax * (rb + 16))
+    if inst is None:
+        return None
+    V = rb // 16
+    koff = nmax * V                               # first key vector: the same on every rank
+    inst._launch_stream()                         # the communicator's stream order, then stage
+    base = inst._data.value
+    stage_split(keys.contiguous(), vals.contiguous() if vals is not None else None, base, base + koff * 16)
+    total = sum(c for _, _, c in blocks)
+    out = torch.empty(total * (rb + 16), dtype=torch.uint8, device=keys.device)
+    pulls, off = [], 0
+    for j, s0, c in blocks:
+        if c:
+            if V:
+                pulls.append((s0 * V, off * V, c * V, j))
+            pulls.append((koff + s0, total * V + off, c, j))
+        off += c
+    grid = grid_rows * max(V, 1)
+    if grid:
+        inst._plan([], pulls, None, out.data_ptr() if pulls else None, grid)
+    rk = keys_from16(out[total * rb:])
+    rv = None
+    if vals is not None:
+        rv = out[:total * rb].view(vals.dtype).view((total,) + tuple(vals.shape[1:]))
+    return rk, rv
 
 
 def _ipc_alltoallv(engine, skeys, svals, mat: List[List[int]]):
     """Owner exchange over the IPC mesh; ``mat[i][j]`` = rows rank i sends to rank j.  Returns
-    (keys, rows) received in source-rank order, or None when records are not 16-byte vectors
-    or the largest rank's payload exceeds the staging buffers (both rank-independent)."""
-    wb = _rec_width(svals)
+    (keys, rows) received in source-rank order, or None when rows are not 16-byte vectors or the
+    largest rank's payload exceeds the staging buffers (both rank-independent)."""
+    rb = _row_bytes(svals)
+    if rb < 0:
+        return None
     p, r = engine.p, engine.rank
-    if not wb:
-        return None
-    inst = _ipc_inst(engine, max(sum(row) for row in mat) * wb)
-    if inst is None:
-        return None
-    v = wb // 16
-    rec = _pack_records(skeys, svals, wb)
-    sp = [0] * p                                   # this rank's block offsets (rows)
-    for j in range(1, p):
-        sp[j] = sp[j - 1] + mat[r][j - 1]
-    stage = [(sp[j] * v, sp[j] * v, mat[r][j] * v, 0) for j in range(p) if mat[r][j]]
-    pulls, off = [], 0
-    for j in range(p):
-        src = sum(mat[j][:r])                      # rank j's block for this rank
-        if mat[j][r]:
-            pulls.append((src * v, off * v, mat[j][r] * v, j))
-        off += mat[j][r]
-    out = torch.empty((off, wb), dtype=torch.uint8, device=skeys.device)
-    grid = max(max(row) for row in mat) * v
-    if grid:
-        inst._plan(stage, pulls, rec.data_ptr() if stage else None, out.data_ptr() if pulls else None, grid)
-    engine._count("sparse.a2a.ipc")
-    return _unpack_records(out, svals, wb)
+    blocks = [(j, sum(mat[j][:r]), mat[j][r]) for j in range(p)]     # rank j's block for this rank
+    got = _split_exchange(engine, skeys, svals, rb, max(sum(row) for row in mat), blocks,
+                          max(max(row) for row in mat))
+    if got is not None:
+        engine._count("sparse.a2a.ipc")
+    return got
 
 
 def _ipc_rows_alltoallv(engine, rows: torch.Tensor, mat: List[List[int]]):
@@ -353,27 +353,13 @@ def _ipc_rows_alltoallv(engine, rows: torch.Tensor, mat: List[List[int]]):
 
 def _ipc_allgatherv(engine, keys, vals, sizes: List[int]):
     """Every rank's (keys, rows), rank order, over the IPC mesh (see above), or None."""
-    wb = _rec_width(vals)
-    if not wb:
+    rb = _row_bytes(vals)
+    if rb < 0:
         return None
-    inst = _ipc_inst(engine, max(sizes) * wb)
-    if inst is None:
-        return None
-    v = wb // 16
-    n = sizes[engine.rank]
-    rec = _pack_records(keys, vals, wb)
-    stage = [(0, 0, n * v, 0)] if n else []
-    pulls, off = [], 0
-    for j, sz in enumerate(sizes):
-        if sz:
-            pulls.append((0, off * v, sz * v, j))
-        off += sz
-    out = torch.empty((off, wb), dtype=torch.uint8, device=keys.device)
-    grid = max(sizes) * v
-    if grid:
-        inst._plan(stage, pulls, rec.data_ptr() if stage else None, out.data_ptr() if pulls else None, grid)
-    engine._count("sparse.allgatherv.ipc")
-    return _unpack_records(out, vals, wb)
+    got = _split_exchange(engine, keys, vals, rb, max(sizes), [(j, 0, sz) for j, sz in enumerate(sizes)], max(sizes))
+    if got is not None:
+        engine._count("sparse.allgatherv.ipc")
+    return got
 
 
 def _host_counts(engine) -> bool:
