@@ -42,21 +42,25 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_gather(IpcPtrs P, Signal* s
 
 // ---------------------------------------------------------------- copy plans (bcast / scatter / gather)
 // The data-movement collectives as ONE kernel per call: a plan of up to kIpcMaxRanks "stage"
-// items (this rank's input -> its own buffer, fused copy-in) and up to kIpcMaxRanks "pull" items
+// items (this rank's input -> its own buffer, fused copy-in) and up to kPlanMaxPulls "pull" items
 // (a peer's buffer -> this rank's output, over xGMI, all pulls interleaved so every link
-// streams).  Every item is walked with the same grid-stride relative index on every rank, so
+// streams; two per peer: the sparse exchanges pull a row block and a key block from each).  Every item is walked with the same grid-stride relative index on every rank, so
 // the vectors block b stages are exactly the vectors block b of the peers pull: per-block
 // barriers suffice, as in the two-shot.  Units: 16-byte vectors.
 struct CopyItem {
   int64_t src_off, dst_off, len;
   int64_t peer;          // pull: source rank; stage: unused
 };
+constexpr int kPlanMaxPulls = 2 * kIpcMaxRanks;
 struct CopyPlan {
   CopyItem stage[kIpcMaxRanks];
-  CopyItem pull[kIpcMaxRanks];
+  CopyItem pull[kPlanMaxPulls];
   int nstage, npull;
 };
 
+// NP: the pulls the kernel keeps in flight per vector step (kIpcMaxRanks, or kPlanMaxPulls for
+// plans with more pulls than that: the wider form takes ~30 more VGPRs, so it only runs when needed).
+template <int NP>
 __global__ __launch_bounds__(kIpcThreads) void k_ipc_copy_plan(IpcPtrs P, Signal* self, int rank, int p,
                                                                 CopyPlan plan, const u32x4* __restrict__ src,
                                                                 u32x4* __restrict__ out, uint32_t epoch,
@@ -74,13 +78,13 @@ __global__ __launch_bounds__(kIpcThreads) void k_ipc_copy_plan(IpcPtrs P, Signal
   int64_t maxlen = 0;
   for (int i = 0; i < plan.npull; ++i) maxlen = plan.pull[i].len > maxlen ? plan.pull[i].len : maxlen;
   for (int64_t v = off0; v < maxlen; v += stride) {
-    u32x4 x[kIpcMaxRanks];
+    u32x4 x[NP];
 #pragma unroll
-    for (int i = 0; i < kIpcMaxRanks; ++i)           // every pull's vector in flight at once
+    for (int i = 0; i < NP; ++i)                     // every pull's vector in flight at once
       if (i < plan.npull && v < plan.pull[i].len)
         x[i] = reinterpret_cast<const u32x4*>(P.data[plan.pull[i].peer])[plan.pull[i].src_off + v];
 #pragma unroll
-    for (int i = 0; i < kIpcMaxRanks; ++i)
+    for (int i = 0; i < NP; ++i)
       if (i < plan.npull && v < plan.pull[i].len) out[plan.pull[i].dst_off + v] = x[i];
   }
   block_barrier(P, 2, rank, p, epoch, self);
@@ -527,7 +531,7 @@ extern "C" int mp4x_memset_async(void* dst, int value, size_t bytes, void* strea
 extern "C" int mp4x_ipc_copy_plan_check(int rank, int p, const int64_t* stage, int nstage, const int64_t* pull,
                                         int npull, const void* src, const void* out, int64_t buf_vecs) {
   if (p < 2 || p > kIpcMaxRanks || rank < 0 || rank >= p) return MP4X_E_BADARG;
-  if (nstage < 0 || nstage > kIpcMaxRanks || npull < 0 || npull > kIpcMaxRanks) return MP4X_E_BADARG;
+  if (nstage < 0 || nstage > kIpcMaxRanks || npull < 0 || npull > kPlanMaxPulls) return MP4X_E_BADARG;
   if ((nstage && (!src || ((uintptr_t)src & 15))) || (npull && (!out || ((uintptr_t)out & 15)))) return MP4X_E_BADARG;
   for (int i = 0; i < nstage; ++i) {
     const int64_t* it = stage + 4 * i;                    // {src_off, dst_off, len, -}
@@ -551,14 +555,18 @@ extern "C" int mp4x_ipc_copy_plan(void* const* data_ptrs, void* const* signal_pt
   CopyPlan plan;
   plan.nstage = nstage;
   plan.npull = npull;
-  for (int i = 0; i < kIpcMaxRanks; ++i) {
+  for (int i = 0; i < kIpcMaxRanks; ++i)
     plan.stage[i] = i < nstage ? CopyItem{stage[4 * i], stage[4 * i + 1], stage[4 * i + 2], 0} : CopyItem{0, 0, 0, 0};
+  for (int i = 0; i < kPlanMaxPulls; ++i)
     plan.pull[i] = i < npull ? CopyItem{pull[4 * i], pull[4 * i + 1], pull[4 * i + 2], pull[4 * i + 3]}
                              : CopyItem{0, 0, 0, 0};
-  }
   blocks = ipc_blocks(blocks, grid_len);
-  hipLaunchKernelGGL(k_ipc_copy_plan, dim3(blocks), dim3(kIpcThreads), 0, (hipStream_t)stream, P,
-                     (Signal*)signal_ptrs[rank], rank, p, plan, (const u32x4*)src, (u32x4*)out, epoch, epoch_dev);
+  if (npull <= kIpcMaxRanks)
+    hipLaunchKernelGGL(k_ipc_copy_plan<kIpcMaxRanks>, dim3(blocks), dim3(kIpcThreads), 0, (hipStream_t)stream, P,
+                       (Signal*)signal_ptrs[rank], rank, p, plan, (const u32x4*)src, (u32x4*)out, epoch, epoch_dev);
+  else
+    hipLaunchKernelGGL(k_ipc_copy_plan<kPlanMaxPulls>, dim3(blocks), dim3(kIpcThreads), 0, (hipStream_t)stream, P,
+                       (Signal*)signal_ptrs[rank], rank, p, plan, (const u32x4*)src, (u32x4*)out, epoch, epoch_dev);
   return (int)hipGetLastError();
 }
 
@@ -570,7 +578,8 @@ extern "C" int mp4x_ipc_occupancy_misc(int family, int dtype, int p, int* blocks
   int m = 1 << 30;
   int e = 0;
   if (family == 1) {
-    occ_min(k_ipc_copy_plan, &m);
+    occ_min(k_ipc_copy_plan<kIpcMaxRanks>, &m);       // the shared-GPU cap must hold for both forms
+    occ_min(k_ipc_copy_plan<kPlanMaxPulls>, &m);
   } else {
     e = with_nr(p, [&](auto nrc) {
       constexpr int NR = decltype(nrc)::value;

@@ -65,6 +65,8 @@ native.register_signatures({
                                              ctypes.POINTER(c_int64), c_void_p, c_void_p, ctypes.c_uint32, c_int,
                                              c_void_p, c_void_p]),
     "mp4x_ipc_bump_epoch": (c_int, [c_void_p, c_void_p]),
+    "mp4x_ipc_copy_plan_check": (c_int, [c_int, c_int, ctypes.POINTER(c_int64), c_int, ctypes.POINTER(c_int64), c_int,
+                                         c_void_p, c_void_p, c_int64]),
     "mp4x_ipc_copy_plan": (c_int, [PP, PP, c_int, c_int, ctypes.POINTER(c_int64), c_int, ctypes.POINTER(c_int64), c_int,
                                    c_void_p, c_void_p, c_int64, c_int64, ctypes.c_uint32, c_int, c_void_p, c_void_p]),
     "mp4x_device_pci_id": (c_int, [ctypes.c_char_p, c_int]),

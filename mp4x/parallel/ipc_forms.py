@@ -459,10 +459,13 @@ class IpcForms:
 
     def _plan(self, stage, pull, src_ptr, out_ptr, grid_len) -> None:
         self.raise_if_failed()
-        st = self._launch_stream()
-        edev = self._next_epoch(st)
         sa = (c_int64 * (4 * max(1, len(stage))))(*[x for it in stage for x in it])
         pa = (c_int64 * (4 * max(1, len(pull))))(*[x for it in pull for x in it])
+        # every refusal BEFORE the epoch moves: a refused plan leaves this rank's epoch in step
+        check(self.lib.mp4x_ipc_copy_plan_check(self.rank, self.p, sa, len(stage), pa, len(pull), src_ptr, out_ptr,
+                                                self.nbytes // 16), "mp4x_ipc_copy_plan")
+        st = self._launch_stream()
+        edev = self._next_epoch(st)
         blocks = self._grid(grid_len)
         sink = self._plan_sink
         if sink is not None:

@@ -119,7 +119,9 @@ def table_bpc(family: str, dtype_code: int, dtype_name: str, op_code: int, p: in
     elif family == "gather":
         args = (p,)
     elif family == "plan":
-        args = ()
+        # both pull widths (csrc/runtime/ipc.hip k_ipc_copy_plan<NP>): the cap must hold for either
+        got = [load_table().get((k, (w,))) for w in (8, 16)]
+        return None if None in got else min(blocks_per_cu(r) for r in got)
     else:
         args = (dtype_code, p)
     res = load_table().get((k, args))

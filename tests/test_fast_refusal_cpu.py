@@ -122,3 +122,45 @@ def test_fast_ok_falls_back_only_when_nothing_was_launched(monkeypatch):
         _fast_ok(1, "mp4x_ipc_fast_allreduce")          # a HIP launch error after the epoch moved
     with pytest.raises(native.NativeError):
         _fast_ok(1005, "mp4x_ipc_fast_allreduce")
+
+
+def test_copy_plan_takes_two_pulls_per_peer_at_eight_ranks():
+    """The sparse exchanges pull a row block and a key block from every peer: 2p pulls at p = 8
+    must pass the plan check on every rank (a refusal on the ranks with more non-empty blocks
+    than the others would leave the rest waiting in the kernel's barrier)."""
+    import mp4x.parallel.ipc  # noqa: F401  (registers the ipc signatures)
+    lib = _lib()
+    c64 = ctypes.c_int64
+
+    def check(npull, p=8):
+        pa = (c64 * (4 * npull))(*[x for j in range(npull) for x in (j, j, 1, j % p)])
+        sa = (c64 * 4)()
+        return lib.mp4x_ipc_copy_plan_check(0, p, sa, 0, pa, npull, None, 0x1000, 1 << 20)
+    assert check(16) == 0
+    assert check(17) == 1001                              # MP4X_E_BADARG
+
+
+def test_refused_plan_leaves_the_epoch_in_step(monkeypatch):
+    """IpcForms._plan runs the plan check before the epoch moves: a refused plan raises with the
+    epoch (and the stream order) untouched."""
+    from mp4x.exceptions import NativeError
+    from mp4x.parallel import ipc_forms
+    import mp4x.parallel.ipc  # noqa: F401
+    lib = _lib()
+
+    class _Inst(ipc_forms.IpcForms):
+        def __init__(self):
+            self.lib, self.rank, self.p, self.nbytes, self.epoch = lib, 0, 8, 1 << 20, 5
+            self._plan_sink = None
+
+        def raise_if_failed(self):
+            pass
+
+        def _launch_stream(self):
+            raise AssertionError("stream joined before the check")
+
+    inst = _Inst()
+    pulls = [(j, j, 1, j % 8) for j in range(17)]
+    with pytest.raises(NativeError):
+        inst._plan([], pulls, None, 0x1000, 1)
+    assert inst.epoch == 5

@@ -1,7 +1,8 @@
-"""The sparse map collectives' ragged exchanges over the IPC mesh (copy-plan kernel, keys + rows
-as 16-byte-vector records) with real processes on one GPU, against a reference built from every
-rank's seed: exact for integer-valued rows, f32 and bf16, p = 2 / 3 / 4, plus the fallback for
-rows that are not whole 16-byte vectors and empty ranks."""
+"""The sparse map collectives' ragged exchanges over the IPC mesh (copy-plan kernel pulling a row
+block and a 16-byte key block from every peer) with real processes on one GPU, against a
+reference built from every rank's seed: exact for integer-valued rows, f32 and bf16,
+p = 2 / 3 / 4 / 8 (8: 2p = 16 pulls per plan), plus the fallback for rows that are not whole
+16-byte vectors and empty ranks."""
 import pytest
 
 torch = pytest.importorskip("torch")
@@ -36,7 +37,7 @@ def _sparse_fn(comm, dim, dtype_name, n, empty_rank):
 
 
 @pytest.mark.parametrize("p,dim,dtype,empty", [(2, 64, "float32", -1), (3, 8, "bfloat16", -1), (4, 64, "float32", 2),
-                                               (3, 3, "float32", -1)])
+                                               (3, 3, "float32", -1), (8, 16, "float32", 5)])
 def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty):
     n = 20000
     out = run_spawn(p, _sparse_fn, args=(dim, dtype, n, empty))
