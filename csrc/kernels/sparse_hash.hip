@@ -7,35 +7,23 @@
 // Here the keys are 64-bit ids and a map is (keys[n], rows[n][dim]).
 //
 // The sort path radix-sorts the full 64-bit keys (8 onesweep passes over keys + indices) to find
-// the runs.  The hash path finds them with ONE pass over the keys instead, then groups the rows
-// by a counting sort over the dense key index:
+// the runs, then a run-start select and the segmented reduce.  The hash path needs four launches
+// and no sort, no scan and no permutation arrays:
 //
-//   memset   table keys <- EMPTY (-1: all 0xFF bytes), slot counts / run counters <- 0
+//   init     table keys <- EMPTY, slot list heads <- -1, the run counter <- 0 (one kernel)
 //   insert   one lane per row: splitmix64 hash, linear probing, 64-bit CAS on an EMPTY slot
-//            (table >= 2n slots, power of two: an empty slot always exists); the slot's row count
-//            += 1 (an int atomic spread over the table) and the row's slot are kept
+//            (table >= 2n slots, power of two: an empty slot always exists); the row is pushed on
+//            its slot's list (one atomic exchange of the head; next[row] = the old head)
 //   compact  4 slots per lane, one atomic per BLOCK (LDS prefix over the block's lanes): every
-//            occupied slot gets a dense run index u and its run length
-//   scan     exclusive sum of the run lengths (rocPRIM) -> run starts
-//   scatter  one lane per row: position = start[u] + (atomic cursor of u); perm / sorted keys
-//   order    one lane per run: the run's row indices sorted ascending (runs up to 64 rows), so
-//            rows combine in input (= rank) order — the same values, bit for bit, as the sort path
-//   reduce   the sort path's segmented reduce (k_segment_reduce_vec: G lanes per run, 16-byte
-//            vectors, two rows in flight), unchanged
+//            occupied slot gets a dense run index u; out_keys[u] and the run's list head
+//   reduce   G lanes per run (a 16-byte vector each): one lane walks the run's list into LDS and
+//            puts the row indices in ascending order (runs up to 64 rows), then the group combines
+//            the rows in that order (= input = rank order): the same values, bit for bit, as the
+//            sort path, which also combines in input order
 //
-// Differences from the sort path (why it stays opt-in): the output keys come in table order, not
-// ascending, and a run longer than 64 rows combines in scatter order (float SUM / PROD of such a
-// key is then not bit-reproducible; integer-valued data and MAX / MIN are exact either way).
-// MP4X_FIRST (K8, the first row in rank order) is not served.  Rows whose key equals -1 (the
-// table's EMPTY marker) never enter the table: they are counted aside and form one extra run.
-#include <rocprim/device/device_scan.hpp>
+#include <type_traits>
 
 #include "common.hpp"
-
-extern "C" int mp4x_segment_reduce_rows(int dtype, int op, const int64_t* sk, const int64_t* perm,
-                                        const int64_t* starts, const int64_t* nruns_dev, int64_t n, int64_t max_runs,
-                                        const void* vals, int64_t dim, int64_t* out_keys, void* out_vals,
-                                        int32_t* out_count, void* stream);
 
 namespace mp4x {
 
@@ -53,52 +41,67 @@ __device__ __forceinline__ uint64_t hash_mix(uint64_t k) {   // splitmix64 final
   return k;
 }
 
-// The side run of rows keyed -1 (the EMPTY marker): its row count and, once compacted, its run.
+// The side run of rows keyed -1 (the EMPTY marker): its list head and, once compacted, its run.
 struct SideRun {
-  int32_t rows;
+  int32_t head;
   int32_t u;
 };
 
+__global__ __launch_bounds__(kBlock) void k_hash_init(unsigned long long* __restrict__ tkeys,
+                                                      int32_t* __restrict__ thead, int64_t nslots,
+                                                      SideRun* __restrict__ side, unsigned long long* __restrict__ m_flag) {
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t0 == 0) {
+    side->head = -1;
+    side->u = -1;
+    m_flag[0] = 0;
+    m_flag[1] = 0;
+  }
+  for (int64_t h = t0; h < nslots; h += nthr) {
+    tkeys[h] = kHashEmpty;
+    thead[h] = -1;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_hash_insert(const int64_t* __restrict__ keys, int64_t n,
                                                         unsigned long long* __restrict__ tkeys,
-                                                        int32_t* __restrict__ tcount, uint64_t mask,
-                                                        int32_t* __restrict__ row_slot, SideRun* __restrict__ side) {
+                                                        int32_t* __restrict__ thead, uint64_t mask,
+                                                        int32_t* __restrict__ next, SideRun* __restrict__ side) {
   const int64_t nthr = (int64_t)gridDim.x * kBlock;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
     const unsigned long long k = (unsigned long long)keys[i];
-    if (k == kHashEmpty) {
-      atomicAdd(&side->rows, 1);
-      row_slot[i] = -1;
-      continue;
-    }
-    uint64_t h = hash_mix(k) & mask;
-    for (;;) {
-      unsigned long long cur = __hip_atomic_load(&tkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur == kHashEmpty) {
-        cur = atomicCAS(&tkeys[h], kHashEmpty, k);
-        if (cur == kHashEmpty) cur = k;                  // inserted here
+    int32_t* head = &side->head;
+    if (k != kHashEmpty) {
+      uint64_t h = hash_mix(k) & mask;
+      for (;;) {
+        unsigned long long cur = __hip_atomic_load(&tkeys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == kHashEmpty) {
+          cur = atomicCAS(&tkeys[h], kHashEmpty, k);
+          if (cur == kHashEmpty) cur = k;                // inserted here
+        }
+        if (cur == k) break;
+        h = (h + 1) & mask;
       }
-      if (cur == k) break;
-      h = (h + 1) & mask;
+      head = &thead[h];
     }
-    atomicAdd(&tcount[h], 1);
-    row_slot[i] = (int32_t)h;
+    next[i] = atomicExch(head, (int32_t)i);              // push row i on its run's list
   }
 }
 
 // A tile of kBlock * kCompactPer slots per block (slot = tile + j * kBlock + lane, coalesced);
 // the block's occupied slots take consecutive run indices from ONE atomic on the run counter.
 __global__ __launch_bounds__(kBlock) void k_hash_compact(const unsigned long long* __restrict__ tkeys,
-                                                         const int32_t* __restrict__ tcount, int64_t nslots,
-                                                         int32_t* __restrict__ tidx, int32_t* __restrict__ run_len,
+                                                         const int32_t* __restrict__ thead, int64_t nslots,
+                                                         int64_t* __restrict__ out_keys, int32_t* __restrict__ rhead,
                                                          unsigned long long* __restrict__ counter,
-                                                         SideRun* __restrict__ side) {
+                                                         const SideRun* __restrict__ side) {
   __shared__ int s_pre[kBlock];
   __shared__ unsigned long long s_base;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && side->rows > 0) {     // the side run, if any
-    const int32_t u = (int32_t)atomicAdd(counter, 1ull);
-    side->u = u;
-    run_len[u] = side->rows;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && side->head >= 0) {     // the side run, if any
+    const int64_t u = (int64_t)atomicAdd(counter, 1ull);
+    out_keys[u] = -1;
+    rhead[u] = side->head;
   }
   const int64_t tile = (int64_t)blockIdx.x * kBlock * kCompactPer;
   int mine = 0;
@@ -121,49 +124,117 @@ __global__ __launch_bounds__(kBlock) void k_hash_compact(const unsigned long lon
 #pragma unroll
   for (int j = 0; j < kCompactPer; ++j) {
     const int64_t h = tile + (int64_t)j * kBlock + threadIdx.x;
-    if (h < nslots && tkeys[h] != kHashEmpty) {
-      tidx[h] = (int32_t)u;
-      run_len[u] = tcount[h];
-      ++u;
+    if (h < nslots) {
+      const unsigned long long k = tkeys[h];
+      if (k != kHashEmpty) {
+        out_keys[u] = (int64_t)k;
+        rhead[u] = thead[h];
+        ++u;
+      }
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_hash_scatter(const int64_t* __restrict__ keys, int64_t n,
-                                                         const int32_t* __restrict__ row_slot,
-                                                         const int32_t* __restrict__ tidx,
-                                                         const int64_t* __restrict__ starts,
-                                                         int32_t* __restrict__ cursor, int64_t* __restrict__ perm,
-                                                         int64_t* __restrict__ sk, const SideRun* __restrict__ side) {
-  const int64_t nthr = (int64_t)gridDim.x * kBlock;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
-    const int32_t s = row_slot[i];
-    const int32_t u = s < 0 ? side->u : tidx[s];        // every row lands in a run: n positions in all
-    const int64_t pos = starts[u] + atomicAdd(&cursor[u], 1);
-    perm[pos] = i;
-    sk[pos] = keys[i];
-  }
+// LDS written by one lane, read by the others of its wave: complete the writes, keep the compiler
+// from moving LDS accesses across (no s_barrier: the groups of a block diverge).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// One lane per run: insertion sort of the run's row indices (runs of 2..kOrderMax rows).
-__global__ __launch_bounds__(kBlock) void k_hash_order(const int64_t* __restrict__ starts,
-                                                       const int32_t* __restrict__ run_len,
-                                                       const unsigned long long* __restrict__ m_dev,
-                                                       int64_t* __restrict__ perm) {
+constexpr int kMinG = 4;                   // lanes per run at least (bounds the LDS index lists)
+
+// G lanes per run, 64 / G runs per wave.  Unit = a 16-byte vector of W elements (VEC) or one
+// element; `units` per row.  Lane 0 of a group walks the run's list into its LDS list (ascending
+// insertion: runs up to kOrderMax rows), the group combines the rows in that order, two in flight.
+// A longer run combines in list order (walking the list again).
+template <int DT, int OP, bool VEC>
+__global__ __launch_bounds__(kBlock) void k_hash_reduce(const int32_t* __restrict__ rhead,
+                                                        const int32_t* __restrict__ next,
+                                                        const unsigned long long* __restrict__ m_dev,
+                                                        const void* __restrict__ vals_, int64_t units, int G,
+                                                        void* __restrict__ out_, int32_t* __restrict__ out_count) {
+  using E = Elem<DT>;
+  using S = typename E::S;
+  using A = typename E::A;
+  using U = typename std::conditional<VEC, u32x4, S>::type;
+  constexpr int W = VEC ? 16 / (int)sizeof(S) : 1;
+  __shared__ int32_t s_idx[kBlock / kMinG][kOrderMax];
+  const U* vals = reinterpret_cast<const U*>(vals_);
+  U* out = reinterpret_cast<U*>(out_);
+  const int lane = threadIdx.x & 63;
+  const int grp = lane / G, sub = lane % G, R = 64 / G;
+  int32_t* buf = s_idx[(threadIdx.x >> 6) * R + grp];
   const int64_t m = (int64_t)*m_dev;
-  const int64_t nthr = (int64_t)gridDim.x * kBlock;
-  for (int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x; u < m; u += nthr) {
-    const int L = run_len[u];
-    if (L < 2 || L > kOrderMax) continue;
-    int64_t* p = perm + starts[u];
-    for (int a = 1; a < L; ++a) {
-      const int64_t x = p[a];
-      int b = a - 1;
-      while (b >= 0 && p[b] > x) {
-        p[b + 1] = p[b];
-        --b;
+  const int64_t wave = wave_id();
+  const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
+  for (int64_t u0 = wave * R; u0 < m; u0 += nwaves * R) {
+    const int64_t u = u0 + grp;
+    const bool live = u < m;
+    int L = 0;
+    if (live) {
+      const int32_t h0 = rhead[u];
+      if (sub == 0) {                                    // the walk, sorted insertion
+        for (int32_t i = h0; i >= 0; i = next[i]) {
+          if (L < kOrderMax) {
+            int b = L - 1;
+            while (b >= 0 && buf[b] > i) {
+              buf[b + 1] = buf[b];
+              --b;
+            }
+            buf[b + 1] = i;
+          }
+          ++L;
+        }
       }
-      p[b + 1] = x;
+    }
+    wave_lds_sync();
+    L = __shfl(L, lane - sub, 64);                      // the group's walker has the length
+    if (!live) continue;
+    if (sub == 0 && out_count) out_count[u] = L;
+    const bool listed = L <= kOrderMax;
+    for (int64_t v = sub; v < units; v += G) {
+      A acc[W];
+      auto load = [&](int32_t row, A* dst) {
+        U t = vals[(int64_t)row * units + v];
+        S x[W];
+        __builtin_memcpy(x, &t, sizeof(U));
+#pragma unroll
+        for (int q = 0; q < W; ++q) dst[q] = E::load(x[q]);
+      };
+      if (listed) {
+        load(buf[0], acc);
+        int j = 1;
+        for (; j + 1 < L; j += 2) {                      // two rows in flight
+          A y0[W], y1[W];
+          load(buf[j], y0);
+          load(buf[j + 1], y1);
+#pragma unroll
+          for (int q = 0; q < W; ++q) acc[q] = combine<DT, OP>(combine<DT, OP>(acc[q], y0[q]), y1[q]);
+        }
+        if (j < L) {
+          A y0[W];
+          load(buf[j], y0);
+#pragma unroll
+          for (int q = 0; q < W; ++q) acc[q] = combine<DT, OP>(acc[q], y0[q]);
+        }
+      } else {
+        int32_t i = rhead[u];
+        load(i, acc);
+        for (i = next[i]; i >= 0; i = next[i]) {
+          A y0[W];
+          load(i, y0);
+#pragma unroll
+          for (int q = 0; q < W; ++q) acc[q] = combine<DT, OP>(acc[q], y0[q]);
+        }
+      }
+      S x[W];
+#pragma unroll
+      for (int q = 0; q < W; ++q) x[q] = E::store(acc[q]);
+      U o;
+      __builtin_memcpy(&o, x, sizeof(U));
+      out[u * units + v] = o;
     }
   }
 }
@@ -176,18 +247,10 @@ int64_t table_slots(int64_t n) {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-size_t scan_temp_bytes(int64_t n) {
-  size_t b = 0;
-  (void)rocprim::exclusive_scan(nullptr, b, (const int32_t*)nullptr, (int64_t*)nullptr, (int64_t)0,
-                                (size_t)(n < 1 ? 1 : n), rocprim::plus<int64_t>(), (hipStream_t)0);
-  return b;
-}
-
-// The scratch layout (every part 256-byte aligned): table keys; then the zero-initialised block
-// (slot counts, run lengths, run cursors, the side run: ONE memset); slot -> run, the row -> slot
-// map, run starts, perm, sorted keys, scan temp.
+// The scratch layout (every part 256-byte aligned): table keys, slot list heads, next[row],
+// run list heads, the side run.
 struct Layout {
-  size_t tkeys, tcount, run_len, cursor, side, zero_end, tidx, row_slot, starts, perm, sk, temp, total, temp_bytes;
+  size_t tkeys, thead, next, rhead, side, total;
   int64_t t;
 };
 
@@ -195,21 +258,51 @@ Layout layout(int64_t n) {
   Layout L;
   L.t = table_slots(n);
   size_t o = 0;
-  L.tkeys = o;    o += align256((size_t)L.t * 8);
-  L.tcount = o;   o += align256((size_t)L.t * 4);
-  L.run_len = o;  o += align256((size_t)n * 4);
-  L.cursor = o;   o += align256((size_t)n * 4);
-  L.side = o;     o += 256;
-  L.zero_end = o;
-  L.tidx = o;     o += align256((size_t)L.t * 4);
-  L.row_slot = o; o += align256((size_t)n * 4);
-  L.starts = o;   o += align256((size_t)n * 8);
-  L.perm = o;     o += align256((size_t)n * 8);
-  L.sk = o;       o += align256((size_t)n * 8);
-  L.temp_bytes = scan_temp_bytes(n);
-  L.temp = o;     o += align256(L.temp_bytes);
+  L.tkeys = o;  o += align256((size_t)L.t * 8);
+  L.thead = o;  o += align256((size_t)L.t * 4);
+  L.next = o;   o += align256((size_t)n * 4);
+  L.rhead = o;  o += align256((size_t)n * 4);
+  L.side = o;   o += 256;
   L.total = o;
   return L;
+}
+
+template <int DT, int OP>
+int launch_reduce(const int32_t* rhead, const int32_t* next, const unsigned long long* m_dev, int64_t n,
+                  const void* vals, int64_t dim, void* out, int32_t* out_count, hipStream_t st) {
+  if constexpr (!op_valid<DT, OP>()) {
+    return MP4X_E_UNSUPPORTED;
+  } else {
+    using S = typename Elem<DT>::S;
+    const int64_t row_bytes = dim * (int64_t)sizeof(S);
+    const bool vec = (row_bytes & 15) == 0 && ((((uintptr_t)vals | (uintptr_t)out) & 15) == 0);
+    const int64_t units = vec ? row_bytes / 16 : dim;
+    int G = kMinG;
+    while (G < units && G < 64) G <<= 1;
+    const int g = grid_for((n * G + 63) / 64 * 64, 1);
+    if (vec)
+      hipLaunchKernelGGL((k_hash_reduce<DT, OP, true>), dim3(g), dim3(kBlock), 0, st, rhead, next, m_dev, vals, units,
+                         G, out, out_count);
+    else
+      hipLaunchKernelGGL((k_hash_reduce<DT, OP, false>), dim3(g), dim3(kBlock), 0, st, rhead, next, m_dev, vals, units,
+                         G, out, out_count);
+    return (int)hipGetLastError();
+  }
+}
+
+template <int DT>
+int reduce_dt(int op, const int32_t* rhead, const int32_t* next, const unsigned long long* m_dev, int64_t n,
+              const void* vals, int64_t dim, void* out, int32_t* oc, hipStream_t st) {
+  switch (op) {
+    case MP4X_SUM: return launch_reduce<DT, MP4X_SUM>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_MAX: return launch_reduce<DT, MP4X_MAX>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_MIN: return launch_reduce<DT, MP4X_MIN>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_PROD: return launch_reduce<DT, MP4X_PROD>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_BAND: return launch_reduce<DT, MP4X_BAND>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_BOR: return launch_reduce<DT, MP4X_BOR>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    case MP4X_BXOR: return launch_reduce<DT, MP4X_BXOR>(rhead, next, m_dev, n, vals, dim, out, oc, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
 }
 }  // namespace
 
@@ -243,34 +336,31 @@ extern "C" int mp4x_hash_reduce_by_key(int dtype, int op, const int64_t* keys, i
   hipStream_t st = (hipStream_t)stream;
   char* p = (char*)scratch;
   auto* tkeys = (unsigned long long*)(p + L.tkeys);
-  auto* tcount = (int32_t*)(p + L.tcount);
-  auto* tidx = (int32_t*)(p + L.tidx);
-  auto* row_slot = (int32_t*)(p + L.row_slot);
-  auto* run_len = (int32_t*)(p + L.run_len);
-  auto* cursor = (int32_t*)(p + L.cursor);
-  auto* starts = (int64_t*)(p + L.starts);
-  auto* perm = (int64_t*)(p + L.perm);
-  auto* sk = (int64_t*)(p + L.sk);
-  auto* counter = (unsigned long long*)m_flag;            // m_flag[0]: the run counter IS m
+  auto* thead = (int32_t*)(p + L.thead);
+  auto* next = (int32_t*)(p + L.next);
+  auto* rhead = (int32_t*)(p + L.rhead);
   auto* side = (SideRun*)(p + L.side);
-  if (hipError_t e = hipMemsetAsync(tkeys, 0xFF, (size_t)L.t * 8, st)) return (int)e;
-  if (hipError_t e = hipMemsetAsync(p + L.tcount, 0, L.zero_end - L.tcount, st)) return (int)e;  // counts .. side
-  if (hipError_t e = hipMemsetAsync(m_flag, 0, 16, st)) return (int)e;
-  if (n == 0) return 0;
-  hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, tkeys, tcount,
-                     (uint64_t)(L.t - 1), row_slot, side);
+  auto* counter = (unsigned long long*)m_flag;            // m_flag[0]: the run counter IS m
+  hipLaunchKernelGGL(k_hash_init, dim3(grid_for(L.t, 2)), dim3(kBlock), 0, st, tkeys, thead, L.t, side, counter);
+  if (n == 0) return (int)hipGetLastError();
+  hipLaunchKernelGGL(k_hash_insert, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, tkeys, thead,
+                     (uint64_t)(L.t - 1), next, side);
   const int64_t tile = (int64_t)kBlock * kCompactPer;
   hipLaunchKernelGGL(k_hash_compact, dim3((unsigned)((L.t + tile - 1) / tile)), dim3(kBlock), 0, st,
-                     (const unsigned long long*)tkeys, (const int32_t*)tcount, L.t, tidx, run_len, counter, side);
-  size_t tb = L.temp_bytes;
-  if (hipError_t e = rocprim::exclusive_scan(p + L.temp, tb, (const int32_t*)run_len, starts, (int64_t)0, (size_t)n,
-                                             rocprim::plus<int64_t>(), st))
-    return (int)e;
-  hipLaunchKernelGGL(k_hash_scatter, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, (const int32_t*)row_slot,
-                     (const int32_t*)tidx, (const int64_t*)starts, cursor, perm, sk, (const SideRun*)side);
-  hipLaunchKernelGGL(k_hash_order, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, (const int64_t*)starts,
-                     (const int32_t*)run_len, (const unsigned long long*)counter, perm);
+                     (const unsigned long long*)tkeys, (const int32_t*)thead, L.t, out_keys, rhead, counter,
+                     (const SideRun*)side);
   if (int e = (int)hipGetLastError()) return e;
-  return mp4x_segment_reduce_rows(dtype, op, sk, perm, starts, m_flag, n, n, vals, dim, out_keys, out_vals, out_count,
-                                  stream);
+  const unsigned long long* m_dev = counter;
+  switch (dtype) {
+    case MP4X_F64: return reduce_dt<MP4X_F64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_F32: return reduce_dt<MP4X_F32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I64: return reduce_dt<MP4X_I64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I32: return reduce_dt<MP4X_I32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_BF16: return reduce_dt<MP4X_BF16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_F16: return reduce_dt<MP4X_F16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I16: return reduce_dt<MP4X_I16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I8: return reduce_dt<MP4X_I8>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_U8: return reduce_dt<MP4X_U8>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
 }

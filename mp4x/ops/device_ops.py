@@ -368,9 +368,9 @@ def hash_rbk_supported(dtype: torch.dtype, op: int) -> bool:
 
 def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=None):
     """K5h (csrc/kernels/sparse_hash.hip): (unique_keys, reduced_rows, counts) with the keys in
-    hash-table order — one hashing pass finds the runs (instead of the sort path's radix sort of
-    the 64-bit keys), a counting sort groups the rows, and the sort path's segmented reduce
-    combines them in input order (runs up to 64 rows: the same values, bit for bit).  Every
+    hash-table order — one hashing pass finds the runs and links each key's rows (instead of the
+    sort path's radix sort of the 64-bit keys), and lane groups combine every key's rows in input
+    order (runs up to 64 rows: the same values, bit for bit, as :func:`reduce_by_key`).  Every
     reduction except the FIRST rule (then use :func:`reduce_by_key`)."""
     _dev_check(keys, vals)
     n = keys.numel()

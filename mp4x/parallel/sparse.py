@@ -155,8 +155,9 @@ def _sync_new_keys(engine, new: List) -> None:
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins
 # Reduce-by-key of the device map collectives (K5): "sort" (default: rocPRIM radix sort + run
 # starts + the segmented reduce — deterministic, keys ascending per owner) or "hash" (K5h,
-# csrc/kernels/sparse_hash.hip: open addressing + atomic combine for SUM / MAX / MIN of f32 / f64 /
-# i32 / i64 rows; keys in table order, float sums in arrival order).  A/B: profiles/r6/sparse/.
+# csrc/kernels/sparse_hash.hip: open addressing, a row list per key, rows combined in input order —
+# the same values bit for bit, 1.4-1.6x faster on config 4's owner rows; keys in table order,
+# which depends on the CAS races of colliding keys).  A/B: profiles/r6/sparse/v3_*.
 RBK_MODE = os.environ.get("MP4X_SPARSE_RBK", "sort").lower()
 def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bits: Optional[int] = None):
     """``key_bits``: every key is in [0, 2**key_bits) (dense dictionary ids) — the radix sort
