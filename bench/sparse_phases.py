@@ -48,13 +48,13 @@ def worker(port, q, nkeys, dim, iters):
         eng.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        skeys, svals, hist = sp._pack_by_owner(ids, vals, eng.p)
+        skeys, svals, info = sp._pack_by_owner(ids, vals, eng.p, want_range=True)
         t = tick("pack_by_owner", t)
-        mat = sp._count_matrix(eng, hist)
+        mat, bits = sp._split_info(sp._count_matrix(eng, info), eng.p)
         t = tick("count_matrix", t)
         rk, rv = sp._ipc_alltoallv(eng, skeys, svals, mat)
         t = tick("ipc_alltoallv", t)
-        uk, uv, _ = sp._reduce_by_key(rk, rv, op, None)
+        uk, uv, _ = sp._reduce_by_key(rk, rv, op, bits)
         t = tick("reduce_by_key", t)
         sizes = sp._row_counts(eng, uk.shape[0], uk.device)
         t = tick("row_counts", t)

@@ -96,11 +96,12 @@ int mp4x_sort_pairs_i32key(const int32_t* keys_in, int32_t* keys_out, const int6
                            int64_t n, int begin_bit, int end_bit, void* temp, size_t temp_bytes, void* stream);
 // Fused stable partition by owner ((uint64)key % p, p <= 2048): out_keys / out_vals (rows of
 // row_bytes, 16-B aligned; vals may be NULL) in owner-major, input-stable order; out_perm
-// (optional) = source row of every slot; counts[p] = rows per owner.  Deterministic.
+// (optional) = source row of every slot; counts[p] = rows per owner; range[2] (optional) = the
+// smallest and largest key (0, 0 when n == 0).  Deterministic.
 size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p);
 int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
-                        int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts, void* scratch,
-                        size_t scratch_bytes, void* stream);
+                        int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts, int64_t* range,
+                        void* scratch, size_t scratch_bytes, void* stream);
 // Run-length encode a SORTED key array: starts[u] = first index of run u, *nruns (device int64).
 size_t mp4x_rle_temp_bytes(int64_t n);
 int mp4x_run_starts(const int64_t* sorted_keys, int64_t n, int64_t* starts, int64_t* nruns_dev,

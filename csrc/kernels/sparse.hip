@@ -201,15 +201,41 @@ constexpr int kPackMaxP = 2048;
 
 __device__ __forceinline__ int owner_of(int64_t k, int p) { return (int)((uint64_t)k % (uint64_t)p); }
 
+// bmin / bmax (optional): the tile's smallest / largest key, for the key range the count
+// exchange carries (k_pack_scatter block 0 reduces them).
 __global__ __launch_bounds__(kBlock) void k_pack_hist(const int64_t* __restrict__ keys, int64_t n, int p, int64_t nblk,
-                                                      int64_t* __restrict__ hist) {
+                                                      int64_t* __restrict__ hist, int64_t* __restrict__ bmin,
+                                                      int64_t* __restrict__ bmax) {
   extern __shared__ __attribute__((aligned(16))) int32_t lh[];
+  __shared__ int64_t wmin[kBlock / 64], wmax[kBlock / 64];
   for (int i = threadIdx.x; i < p; i += kBlock) lh[i] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) atomicAdd(&lh[owner_of(keys[i], p)], 1);
+  const int64_t k = i < n ? keys[i] : 0;
+  if (i < n) atomicAdd(&lh[owner_of(k, p)], 1);
+  if (bmin) {
+    int64_t lo = i < n ? k : INT64_MAX, hi = i < n ? k : INT64_MIN;
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      wmin[threadIdx.x >> 6] = lo;
+      wmax[threadIdx.x >> 6] = hi;
+    }
+  }
   __syncthreads();
   for (int d = threadIdx.x; d < p; d += kBlock) hist[(int64_t)d * nblk + blockIdx.x] = lh[d];
+  if (bmin && threadIdx.x == 0) {
+    int64_t lo = wmin[0], hi = wmax[0];
+    for (int q = 1; q < kBlock / 64; ++q) {
+      lo = wmin[q] < lo ? wmin[q] : lo;
+      hi = wmax[q] > hi ? wmax[q] : hi;
+    }
+    bmin[blockIdx.x] = lo;
+    bmax[blockIdx.x] = hi;
+  }
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restrict__ keys,
@@ -220,7 +246,10 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restri
                                                          int64_t* __restrict__ out_keys,
                                                          u32x4* __restrict__ out_vals,
                                                          int64_t* __restrict__ out_perm,
-                                                         int64_t* __restrict__ counts) {
+                                                         int64_t* __restrict__ counts,
+                                                         const int64_t* __restrict__ bmin,
+                                                         const int64_t* __restrict__ bmax,
+                                                         int64_t* __restrict__ range) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int32_t* wcnt = reinterpret_cast<int32_t*>(smem);                         // [4][p]
   int64_t* pos = reinterpret_cast<int64_t*>(smem + ((4 * p * 4 + 15) & ~15));  // [kBlock]
@@ -257,6 +286,35 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restri
       const int64_t end = (q + 1 < p) ? off[(int64_t)(q + 1) * nblk] : off[last] + hist[last];
       counts[q] = end - off[(int64_t)q * nblk];
     }
+  if (b == 0 && range) {                 // the key range: every tile's min / max (k_pack_hist)
+    __syncthreads();
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t q = tid; q < nblk; q += kBlock) {
+      lo = bmin[q] < lo ? bmin[q] : lo;
+      hi = bmax[q] > hi ? bmax[q] : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t a = __shfl_xor(lo, o, 64), c = __shfl_xor(hi, o, 64);
+      lo = a < lo ? a : lo;
+      hi = c > hi ? c : hi;
+    }
+    __shared__ int64_t rmin[kBlock / 64], rmax[kBlock / 64];
+    if (lane == 0) {
+      rmin[w] = lo;
+      rmax[w] = hi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      for (int q = 1; q < kBlock / 64; ++q) {
+        lo = rmin[q] < rmin[0] ? rmin[q] : rmin[0];
+        hi = rmax[q] > rmax[0] ? rmax[q] : rmax[0];
+        rmin[0] = lo;
+        rmax[0] = hi;
+      }
+      range[0] = rmin[0];
+      range[1] = rmax[0];
+    }
+  }
   if (!vals) return;
   __syncthreads();
   const int64_t rows = (n - t0) < kBlock ? (n - t0) : kBlock;
@@ -366,17 +424,23 @@ extern "C" size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p) {
   size_t cub_bytes = 0;
   (void)rocprim::exclusive_scan(nullptr, cub_bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int64_t)0, (size_t)m,
                                 rocprim::plus<int64_t>(), (hipStream_t)0);
-  return 2 * pack_align(m * sizeof(int64_t)) + pack_align(cub_bytes);
+  return 2 * pack_align(m * sizeof(int64_t)) + 2 * pack_align((nblk < 1 ? 1 : nblk) * sizeof(int64_t)) +
+         pack_align(cub_bytes);
 }
 
 // keys[n] (+ rows vals[n][row_bytes]) -> stable-by-owner layout out_keys / out_vals, optional
-// out_perm (source index of every output slot) and counts[p] (rows per owner).
+// out_perm (source index of every output slot), counts[p] (rows per owner) and range[2] (optional:
+// the smallest and largest key; 0, 0 when n == 0).
 extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
                                    int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts,
-                                   void* scratch, size_t scratch_bytes, void* stream) {
+                                   int64_t* range, void* scratch, size_t scratch_bytes, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (p < 1 || p > kPackMaxP) return MP4X_E_BADARG;
-  if (n <= 0) return counts ? (int)hipMemsetAsync(counts, 0, p * sizeof(int64_t), st) : 0;
+  if (n <= 0) {
+    if (counts)
+      if (hipError_t e = hipMemsetAsync(counts, 0, p * sizeof(int64_t), st)) return (int)e;
+    return range ? (int)hipMemsetAsync(range, 0, 2 * sizeof(int64_t), st) : 0;
+  }
   if (n > INT32_MAX / 2) return MP4X_E_BADARG;
   if (vals && ((row_bytes & 15) || ((((uintptr_t)vals | (uintptr_t)out_vals) & 15)))) return MP4X_E_BADARG;
   if (scratch_bytes < mp4x_partition_pack_scratch_bytes(n, p)) return MP4X_E_BADARG;
@@ -385,9 +449,13 @@ extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_
   char* sc = (char*)scratch;
   int64_t* hist = (int64_t*)sc;
   int64_t* off = (int64_t*)(sc + pack_align(m * sizeof(int64_t)));
-  void* temp = sc + 2 * pack_align(m * sizeof(int64_t));
-  size_t temp_bytes = scratch_bytes - 2 * pack_align(m * sizeof(int64_t));
-  hipLaunchKernelGGL(k_pack_hist, dim3(nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, nblk, hist);
+  int64_t* bmin = (int64_t*)(sc + 2 * pack_align(m * sizeof(int64_t)));
+  int64_t* bmax = (int64_t*)((char*)bmin + pack_align(nblk * sizeof(int64_t)));
+  const size_t head = 2 * pack_align(m * sizeof(int64_t)) + 2 * pack_align(nblk * sizeof(int64_t));
+  void* temp = sc + head;
+  size_t temp_bytes = scratch_bytes - head;
+  hipLaunchKernelGGL(k_pack_hist, dim3(nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, nblk, hist,
+                     range ? bmin : nullptr, range ? bmax : nullptr);
   int e = (int)hipGetLastError();
   if (e) return e;
   e = (int)rocprim::exclusive_scan(temp, temp_bytes, hist, off, (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), st);
@@ -397,6 +465,6 @@ extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_
   while (G < V && G < 64) G <<= 1;
   const size_t lds = ((4 * p * 4 + 15) & ~15) + kBlock * sizeof(int64_t);
   hipLaunchKernelGGL(k_pack_scatter, dim3(nblk), dim3(kBlock), lds, st, keys, (const u32x4*)vals, n, V, G, p, nblk,
-                     off, hist, out_keys, (u32x4*)out_vals, out_perm, counts);
+                     off, hist, out_keys, (u32x4*)out_vals, out_perm, counts, bmin, bmax, range);
   return (int)hipGetLastError();
 }

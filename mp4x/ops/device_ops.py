@@ -254,12 +254,14 @@ PACK_MAX_P = 2048
 
 
 def partition_pack(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, want_perm: bool = False,
-                   stream=None):
+                   want_range: bool = False, stream=None):
     """Fused K4b stable partition by owner ``(uint64)key % p``.
 
     Returns ``(out_keys, out_vals, counts int64[p], perm)``; ``out_vals`` is None when
     ``vals`` is None, ``perm`` (source row of each slot) only with ``want_perm``.  Rows whose
     size is not a multiple of 16 bytes are packed with :func:`gather_rows` through ``perm``.
+    ``want_range``: ``counts`` has two more entries, the smallest and largest key (0, 0 when
+    empty), reduced inside the same kernels.
     """
     _dev_check(keys, vals)
     if keys.dtype != torch.int64:
@@ -281,13 +283,14 @@ def partition_pack(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, wan
     out_keys = torch.empty(n, dtype=torch.int64, device=dev)
     out_vals = torch.empty_like(vals) if vals is not None else None
     perm = torch.empty(n, dtype=torch.int64, device=dev) if need_perm else None
-    counts = torch.empty(p, dtype=torch.int64, device=dev)
+    counts = torch.empty(p + (2 if want_range else 0), dtype=torch.int64, device=dev)
     lib = native.hip()
     sb = lib.mp4x_partition_pack_scratch_bytes(n, p)
     scratch = torch.empty(max(sb, 1), dtype=torch.uint8, device=dev)
     check(lib.mp4x_partition_pack(keys.data_ptr(), vals.data_ptr() if fused_rows else None, n, row_bytes, p,
                                   out_keys.data_ptr(), out_vals.data_ptr() if fused_rows else None,
                                   perm.data_ptr() if perm is not None else None, counts.data_ptr(),
+                                  counts.data_ptr() + 8 * p if want_range else None,
                                   scratch.data_ptr(), sb, stream_ptr(stream)), "mp4x_partition_pack")
     if vals is not None and not fused_rows and n:
         gather_rows(vals.view(n, -1), perm, out=out_vals.view(n, -1), stream=stream)

@@ -213,8 +213,9 @@ def _owner_order(keys: torch.Tensor, p: int):
     return perm, torch.bincount(dest, minlength=p)
 
 
-def _pack_by_owner(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int):
-    """(keys, rows) in stable owner-major order + per-owner counts.
+def _pack_by_owner(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, want_range: bool = False):
+    """(keys, rows) in stable owner-major order + per-owner counts (``want_range``: followed by
+    the smallest and largest key, as :func:`_owner_info` lays them out).
 
     GPU: one fused K4b launch chain (LDS multisplit, :func:`mp4x.ops.device_ops.partition_pack`);
     the sort-based K4 path remains for p beyond the fused kernel's LDS budget and on CPU.
@@ -222,12 +223,12 @@ def _pack_by_owner(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int):
     if keys.is_cuda:
         from ..ops.device_ops import PACK_MAX_P, partition_pack
         if p <= PACK_MAX_P:
-            sk, sv, counts, _ = partition_pack(keys, vals, p)
+            sk, sv, counts, _ = partition_pack(keys, vals, p, want_range=want_range)
             return sk, sv, counts
     perm, hist = _owner_order(keys, p)
     skeys = _gather_rows(keys.view(-1, 1), perm).view(-1)
     svals = _gather_rows(vals, perm) if vals is not None else None
-    return skeys, svals, hist
+    return skeys, svals, (_owner_info(keys, hist) if want_range else hist)
 
 
 def _gather_rows(x: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
@@ -381,15 +382,40 @@ def _count_matrix(engine, hist: torch.Tensor) -> List[List[int]]:
     return torch.stack(ts).tolist()
 
 
+def _owner_info(keys: torch.Tensor, hist: torch.Tensor) -> torch.Tensor:
+    """This rank's count-matrix row plus its key range: hist[p] | min | max (0 | 0 when empty).
+    The range rides the count exchange, so every rank learns the received keys' bit width for
+    free and the reduce-by-key's radix sort runs over those bits only.  (The fused GPU pack
+    produces this row itself: ``_pack_by_owner(..., want_range=True)``.)"""
+    hist = hist.to(torch.int64)
+    if keys.numel() == 0:
+        return torch.cat([hist, hist.new_zeros(2)])
+    mn, mx = torch.aminmax(keys)
+    return torch.cat([hist, mn.view(1), mx.view(1)])
+
+
+def _split_info(rows: List[List[int]], p: int):
+    """(count matrix, key bits of every rank's keys or None) from the :func:`_owner_info` rows."""
+    mat = [r[:p] for r in rows]
+    lo = min(r[p] for r in rows)
+    hi = max(r[p + 1] for r in rows)
+    bits = max(1, int(hi).bit_length()) if lo >= 0 else None
+    return mat, (bits if bits is not None and bits <= 63 else None)
+
+
 # ------------------------------------------------------------------ tensor-level API
 def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor]):
+    """(received keys, received rows, key bits): ``key bits`` bounds every received key (the
+    radix sort's width) when the count exchange carried the ranks' key ranges, else None."""
     p = engine.p
-    skeys, svals, hist = _pack_by_owner(keys, vals, p)
-    if _sparse_ipc_ok(engine, keys):
-        mat = _count_matrix(engine, hist)
+    ipc = _sparse_ipc_ok(engine, keys)
+    skeys, svals, hist = _pack_by_owner(keys, vals, p, want_range=ipc)
+    bits = None
+    if ipc:
+        mat, bits = _split_info(_count_matrix(engine, hist), p)
         got = _ipc_alltoallv(engine, skeys, svals, mat)
         if got is not None:
-            return got
+            return got[0], got[1], bits
         send = mat[engine.rank]
         recv = [mat[j][engine.rank] for j in range(p)]
     else:
@@ -402,7 +428,7 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     if vals is not None:
         rvals = torch.empty((sum(recv),) + tuple(vals.shape[1:]), dtype=vals.dtype, device=vals.device)
         engine.coll.all_to_all_single(rvals, svals, recv, send)
-    return rkeys, rvals
+    return rkeys, rvals, bits
 
 
 def _row_counts(engine, n: int, device) -> List[int]:
@@ -460,8 +486,8 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, k
     squeeze = vals.dim() == 1
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
-    rkeys, rvals = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
+    rkeys, rvals, bits = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or bits)
     sizes = _row_counts(engine, uk.shape[0], uk.device)     # one count round for keys AND rows
     got = _ipc_allgatherv(engine, uk, uv, sizes) if _sparse_ipc_ok(engine, uk) else None
     if got is not None:
@@ -547,16 +573,16 @@ def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root
     squeeze = vals.dim() == 1
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
-    rkeys, rvals = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits)
+    rkeys, rvals, bits = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or bits)
     gk, gv = gather_sparse(engine, uk, uv, root, key_bits)    # disjoint owners: K8 dedupe is a no-op
     return gk, (gv.view(-1) if squeeze else gv)
 
 
 def _set_counts(engine, ids: torch.Tensor):
     ids = torch.unique(ids) if not ids.is_cuda else _reduce_by_key(ids, None, None)[0]
-    rkeys, _ = _exchange_by_owner(engine, ids, None)
-    return _reduce_by_key(rkeys, None, None)
+    rkeys, _, bits = _exchange_by_owner(engine, ids, None)
+    return _reduce_by_key(rkeys, None, None, bits)
 
 
 def set_union(engine, ids: torch.Tensor) -> torch.Tensor:

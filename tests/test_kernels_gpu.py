@@ -245,6 +245,21 @@ def test_partition_pack_is_stable_sort_by_owner(p, n, dim, dtype):
         assert sv is None
 
 
+@pytest.mark.parametrize("n", [0, 1, 255, 257, 70_001])
+def test_partition_pack_key_range(n):
+    """want_range: counts[p:] = the smallest and largest key (0, 0 when empty), reduced inside
+    the pack kernels (the count exchange carries it to size the reduce-by-key's sort)."""
+    K = _native()
+    g = torch.Generator(device="cpu").manual_seed(n + 5)
+    for lo, hi in ((-(1 << 62), 1 << 62), (0, 1 << 24), (7, 8)):
+        keys = torch.randint(lo, hi, (n,), generator=g, dtype=torch.int64).to(DEV)
+        sk, _, counts, _ = K.partition_pack(keys, None, 8, want_range=True)
+        assert counts.numel() == 10
+        assert torch.equal(counts[:8], torch.bincount(_owner_ref(keys, 8), minlength=8))
+        want = [int(keys.min()), int(keys.max())] if n else [0, 0]
+        assert counts[8:].tolist() == want
+
+
 def test_partition_pack_matches_sort_path():
     K = _native()
     keys = torch.randint(0, 1 << 62, (100_000,), device=DEV, dtype=torch.int64)

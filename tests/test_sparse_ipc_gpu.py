@@ -12,18 +12,18 @@ from spawn_ranks import run_spawn  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def _data(r, dim, dtype, n):
+def _data(r, dim, dtype, n, shift=0):
     g = torch.Generator().manual_seed(100 + r)
-    keys = torch.randperm(3 * n, generator=g)[:n].to(torch.int64)          # overlapping id ranges
+    keys = torch.randperm(3 * n, generator=g)[:n].to(torch.int64) + shift  # overlapping id ranges
     vals = torch.randint(-8, 8, (n, dim), generator=g).to(dtype)
     return keys, vals
 
 
-def _sparse_fn(comm, dim, dtype_name, n, empty_rank):
+def _sparse_fn(comm, dim, dtype_name, n, empty_rank, shift):
     from mp4x import Operators
     dtype = getattr(torch, dtype_name)
     r, p = comm.getRank(), comm.getSlaveNum()
-    k, v = _data(r, dim, dtype, 0 if r == empty_rank else n)
+    k, v = _data(r, dim, dtype, 0 if r == empty_rank else n, shift)
     eng = comm.device
     before = dict(eng.stats)
     op = Operators.Float.SUM if dtype == torch.float32 else Operators.BFloat16.SUM
@@ -36,13 +36,16 @@ def _sparse_fn(comm, dim, dtype_name, n, empty_rank):
     return rk.cpu().numpy(), rv.float().cpu().numpy(), gk.cpu().numpy(), gv.float().cpu().numpy(), sizes, used
 
 
-@pytest.mark.parametrize("p,dim,dtype,empty", [(2, 64, "float32", -1), (3, 8, "bfloat16", -1), (4, 64, "float32", 2),
-                                               (3, 3, "float32", -1), (8, 16, "float32", 5)])
-def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty):
+# shift: the keys' range — non-negative ids let the reduce-by-key sort only the bits the ranks'
+# key ranges (carried by the count exchange) need; negative ids (-2**40 + ...) the full width
+@pytest.mark.parametrize("p,dim,dtype,empty,shift", [(2, 64, "float32", -1, 0), (3, 8, "bfloat16", -1, -(1 << 40)),
+                                                     (4, 64, "float32", 2, 1 << 50), (3, 3, "float32", -1, 0),
+                                                     (8, 16, "float32", 5, 0)])
+def test_sparse_exchange_over_ipc_exact(p, dim, dtype, empty, shift):
     n = 20000
-    out = run_spawn(p, _sparse_fn, args=(dim, dtype, n, empty))
+    out = run_spawn(p, _sparse_fn, args=(dim, dtype, n, empty, shift))
     dt = getattr(torch, dtype)
-    ins = [_data(j, dim, dt, 0 if j == empty else n) for j in range(p)]
+    ins = [_data(j, dim, dt, 0 if j == empty else n, shift) for j in range(p)]
     ref = {}
     for k, v in ins:
         for kk, vv in zip(k.tolist(), v.float()):
