@@ -350,24 +350,45 @@ extern "C" int mp4x_key_owner(const int64_t* keys, int64_t n, int p, int32_t* de
   return (int)hipGetLastError();
 }
 
+// rocPRIM's dispatch sorts up to 1 M items by block sort + merge passes (log2 of the block count,
+// whatever the key width); onesweep runs one pass per 8 key bits.  A sort over few bits (dense
+// ids, the key range the sparse count exchange carries) can force onesweep: MergeSortLimit = 0.
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+
 extern "C" size_t mp4x_sort_pairs_temp_bytes(int64_t n, int key_is_i32) {
-  size_t bytes = 0;
+  size_t bytes = 0, ob = 0;
   const size_t sz = (size_t)(n < 1 ? 1 : n);
-  if (key_is_i32)
+  if (key_is_i32) {
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
                                     (const int64_t*)nullptr, (int64_t*)nullptr, sz, 0, 32, (hipStream_t)0);
-  else
+  } else {
     (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int64_t*)nullptr, (int64_t*)nullptr,
                                     (const int64_t*)nullptr, (int64_t*)nullptr, sz, 0, 64, (hipStream_t)0);
-  return bytes;
+    (void)rocprim::radix_sort_pairs<OnesweepSort>(nullptr, ob, (const int64_t*)nullptr, (int64_t*)nullptr,
+                                                  (const int64_t*)nullptr, (int64_t*)nullptr, sz, 0, 64,
+                                                  (hipStream_t)0);
+  }
+  return bytes > ob ? bytes : ob;
+}
+
+// algo: 0 = rocPRIM's own choice, 1 = onesweep (one pass per 8 bits of [begin_bit, end_bit)).
+extern "C" int mp4x_sort_pairs_i64_ex(const int64_t* keys_in, int64_t* keys_out, const int64_t* idx_in,
+                                      int64_t* idx_out, int64_t n, int begin_bit, int end_bit, int algo, void* temp,
+                                      size_t temp_bytes, void* stream) {
+  if (n <= 0) return 0;
+  if (algo == 1)
+    return (int)rocprim::radix_sort_pairs<OnesweepSort>(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out,
+                                                        (size_t)n, (unsigned)begin_bit, (unsigned)end_bit,
+                                                        (hipStream_t)stream);
+  return (int)rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (size_t)n,
+                                        (unsigned)begin_bit, (unsigned)end_bit, (hipStream_t)stream);
 }
 
 extern "C" int mp4x_sort_pairs_i64(const int64_t* keys_in, int64_t* keys_out, const int64_t* idx_in, int64_t* idx_out,
                                    int64_t n, int begin_bit, int end_bit, void* temp, size_t temp_bytes,
                                    void* stream) {
-  if (n <= 0) return 0;
-  return (int)rocprim::radix_sort_pairs(temp, temp_bytes, keys_in, keys_out, idx_in, idx_out, (size_t)n,
-                                        (unsigned)begin_bit, (unsigned)end_bit, (hipStream_t)stream);
+  return mp4x_sort_pairs_i64_ex(keys_in, keys_out, idx_in, idx_out, n, begin_bit, end_bit, 0, temp, temp_bytes, stream);
 }
 
 extern "C" int mp4x_sort_pairs_i32key(const int32_t* keys_in, int32_t* keys_out, const int64_t* idx_in,

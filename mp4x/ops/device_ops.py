@@ -6,6 +6,7 @@ the current torch stream.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Sequence, Tuple
 
 import torch
@@ -297,8 +298,25 @@ def partition_pack(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, wan
     return out_keys, out_vals, counts, perm
 
 
-def sort_pairs(keys: torch.Tensor, idx: Optional[torch.Tensor] = None, end_bit: Optional[int] = None, stream=None):
-    """Stable radix sort of int64 (or int32) keys with an int64 payload (default arange)."""
+# int64 key sorts: rocPRIM's own dispatch (block sort + merge passes below 1 M items, whatever the
+# key width) or forced onesweep (csrc/kernels/sparse.hip OnesweepSort: ~27 us per 8-bit pass at
+# 200 k items).  Measured on MI355X (profiles/r6/sparse/sort_ab.jsonl): onesweep wins at <= 16 bits
+# from 200 k items and at <= 40 bits from ~1 M items (0.107 vs 0.199 ms at 1 M x 24 bits).
+# MP4X_SORT_ALGO=rocprim | onesweep pins one.
+SORT_ALGO = os.environ.get("MP4X_SORT_ALGO", "auto").lower()
+
+
+def sort_algo(n: int, bits: int) -> int:
+    """0 = rocPRIM's dispatch, 1 = onesweep, for ``n`` int64 keys over ``bits`` bits."""
+    if SORT_ALGO in ("rocprim", "onesweep"):
+        return int(SORT_ALGO == "onesweep")
+    return 1 if bits <= 16 or (n >= 400_000 and bits <= 40) else 0
+
+
+def sort_pairs(keys: torch.Tensor, idx: Optional[torch.Tensor] = None, end_bit: Optional[int] = None, stream=None,
+               algo: Optional[int] = None):
+    """Stable radix sort of int64 (or int32) keys with an int64 payload (default arange).
+    ``algo`` (int64 keys): 0 = rocPRIM's choice, 1 = onesweep; None = by key width."""
     _dev_check(keys)
     n = keys.numel()
     if idx is None:
@@ -310,9 +328,14 @@ def sort_pairs(keys: torch.Tensor, idx: Optional[torch.Tensor] = None, end_bit: 
     tb = lib.mp4x_sort_pairs_temp_bytes(n, int(is32))
     temp = torch.empty(max(tb, 1), dtype=torch.uint8, device=keys.device)
     eb = end_bit if end_bit is not None else (32 if is32 else 64)
-    fn = lib.mp4x_sort_pairs_i32key if is32 else lib.mp4x_sort_pairs_i64
-    check(fn(keys.data_ptr(), ko.data_ptr(), idx.data_ptr(), io.data_ptr(), n, 0, eb, temp.data_ptr(), tb,
-             stream_ptr(stream)), "mp4x_sort_pairs")
+    if is32:
+        check(lib.mp4x_sort_pairs_i32key(keys.data_ptr(), ko.data_ptr(), idx.data_ptr(), io.data_ptr(), n, 0, eb,
+                                         temp.data_ptr(), tb, stream_ptr(stream)), "mp4x_sort_pairs")
+        return ko, io
+    if algo is None:
+        algo = sort_algo(n, eb)
+    check(lib.mp4x_sort_pairs_i64_ex(keys.data_ptr(), ko.data_ptr(), idx.data_ptr(), io.data_ptr(), n, 0, eb, int(algo),
+                                     temp.data_ptr(), tb, stream_ptr(stream)), "mp4x_sort_pairs")
     return ko, io
 
 

@@ -55,6 +55,8 @@ _HIP_SIGS = {
     "mp4x_key_owner": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p]),
     "mp4x_sort_pairs_temp_bytes": (c_size_t, [c_int64, c_int]),
     "mp4x_sort_pairs_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_size_t, c_void_p]),
+    "mp4x_sort_pairs_i64_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_int, c_void_p,
+                                       c_size_t, c_void_p]),
     "mp4x_sort_pairs_i32key": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_int, c_void_p, c_size_t, c_void_p]),
     "mp4x_partition_pack_scratch_bytes": (c_size_t, [c_int64, c_int]),
     "mp4x_partition_pack": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,

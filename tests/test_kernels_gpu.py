@@ -379,3 +379,18 @@ def test_reduce_by_key_is_deterministic_in_input_order():
             acc = acc + r
         j = int((runs[0][0].cpu() == k).nonzero()[0])
         assert torch.equal(runs[0][1][j].cpu(), acc), k
+
+
+@pytest.mark.parametrize("n,bits", [(1, 8), (5000, 12), (300_000, 16), (600_000, 40), (200_000, 64)])
+def test_sort_pairs_onesweep_matches_rocprim_dispatch(n, bits):
+    """The forced-onesweep key sort (narrow keys, large counts) is the same stable sort as
+    rocPRIM's own dispatch: identical keys and payload order, ties by input index."""
+    K = _native()
+    g = torch.Generator(device="cpu").manual_seed(n + bits)
+    hi = (1 << bits) if bits < 63 else (1 << 62)
+    keys = torch.randint(0, hi, (n,), generator=g, dtype=torch.int64).to(DEV)
+    k0, i0 = K.sort_pairs(keys, end_bit=min(bits, 64), algo=0)
+    k1, i1 = K.sort_pairs(keys, end_bit=min(bits, 64), algo=1)
+    ref = torch.argsort(keys.cpu(), stable=True)
+    assert torch.equal(i0.cpu(), ref) and torch.equal(i1.cpu(), ref)
+    assert torch.equal(k0, k1)
