@@ -23,6 +23,7 @@ def worker(port, q, nkeys, dim, iters):
     import torch
     from mp4x import Operators, ProcessCommSlave
     from mp4x.operators import dtype_of_torch, for_dtype
+    from mp4x.ops import device_ops as K
     from mp4x.parallel import sparse as sp
     torch.cuda.set_device(0)
     os.environ.setdefault("MP4X_DEVICE_INDEX", "0")
@@ -48,11 +49,12 @@ def worker(port, q, nkeys, dim, iters):
         eng.barrier()
         torch.cuda.synchronize()
         t = time.perf_counter()
-        skeys, svals, info = sp._pack_by_owner(ids, vals, eng.p, want_range=True)
-        t = tick("pack_by_owner", t)
-        mat, bits = sp._split_info(sp._count_matrix(eng, info), eng.p)
+        pc = K.partition_count(ids, eng.p)                     # K4b first half: counts + key range
+        t = tick("pack_count", t)
+        mat, bits = sp._split_info(sp._count_matrix(eng, pc.info), eng.p)
         t = tick("count_matrix", t)
-        rk, rv = sp._ipc_alltoallv(eng, skeys, svals, mat)
+        rk, rv = sp._ipc_alltoallv(eng, ids, vals, mat,         # scatter into staging + the plan
+                                   stage=lambda a, b: K.partition_scatter(pc, vals, a, b, 2))
         t = tick("ipc_alltoallv", t)
         uk, uv, _ = sp._reduce_by_key(rk, rv, op, bits)
         t = tick("reduce_by_key", t)

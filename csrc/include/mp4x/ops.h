@@ -102,6 +102,14 @@ size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p);
 int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
                         int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts, int64_t* range,
                         void* scratch, size_t scratch_bytes, void* stream);
+// The two halves of mp4x_partition_pack (the same scratch between them): count -> counts[p],
+// range[2]; scatter -> out_keys (key_stride 1: int64[n]; 2: the key half of 16-byte vectors),
+// out_vals, out_perm.
+int mp4x_partition_pack_count(const int64_t* keys, int64_t n, int p, int64_t* counts, int64_t* range, void* scratch,
+                              size_t scratch_bytes, void* stream);
+int mp4x_partition_pack_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
+                                int64_t* out_keys, int key_stride, void* out_vals, int64_t* out_perm, void* scratch,
+                                size_t scratch_bytes, void* stream);
 // Run-length encode a SORTED key array: starts[u] = first index of run u, *nruns (device int64).
 size_t mp4x_rle_temp_bytes(int64_t n);
 int mp4x_run_starts(const int64_t* sorted_keys, int64_t n, int64_t* starts, int64_t* nruns_dev,

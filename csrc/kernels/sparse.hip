@@ -238,18 +238,54 @@ __global__ __launch_bounds__(kBlock) void k_pack_hist(const int64_t* __restrict_
   }
 }
 
+// One block: counts[q] = rows for owner q (from the scanned (owner, tile) bases) and, when asked,
+// range = the smallest / largest key (every tile's min / max from k_pack_hist).
+__global__ __launch_bounds__(kBlock) void k_pack_counts(const int64_t* __restrict__ off,
+                                                        const int64_t* __restrict__ hist, int p, int64_t nblk,
+                                                        int64_t* __restrict__ counts,
+                                                        const int64_t* __restrict__ bmin,
+                                                        const int64_t* __restrict__ bmax,
+                                                        int64_t* __restrict__ range) {
+  __shared__ int64_t rmin[kBlock / 64], rmax[kBlock / 64];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int64_t last = (int64_t)p * nblk - 1;
+  for (int q = tid; q < p; q += kBlock) {
+    const int64_t end = (q + 1 < p) ? off[(int64_t)(q + 1) * nblk] : off[last] + hist[last];
+    counts[q] = end - off[(int64_t)q * nblk];
+  }
+  if (!range) return;
+  int64_t lo = INT64_MAX, hi = INT64_MIN;
+  for (int64_t q = tid; q < nblk; q += kBlock) {
+    lo = bmin[q] < lo ? bmin[q] : lo;
+    hi = bmax[q] > hi ? bmax[q] : hi;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(lo, o, 64), c = __shfl_xor(hi, o, 64);
+    lo = a < lo ? a : lo;
+    hi = c > hi ? c : hi;
+  }
+  if (lane == 0) {
+    rmin[w] = lo;
+    rmax[w] = hi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < kBlock / 64; ++q) {
+      lo = rmin[q] < lo ? rmin[q] : lo;
+      hi = rmax[q] > hi ? rmax[q] : hi;
+    }
+    range[0] = lo;
+    range[1] = hi;
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restrict__ keys,
                                                          const u32x4* __restrict__ vals, int64_t n, int64_t V,
                                                          int G, int p, int64_t nblk,
                                                          const int64_t* __restrict__ off,
-                                                         const int64_t* __restrict__ hist,
-                                                         int64_t* __restrict__ out_keys,
+                                                         int64_t* __restrict__ out_keys, int key_stride,
                                                          u32x4* __restrict__ out_vals,
-                                                         int64_t* __restrict__ out_perm,
-                                                         int64_t* __restrict__ counts,
-                                                         const int64_t* __restrict__ bmin,
-                                                         const int64_t* __restrict__ bmax,
-                                                         int64_t* __restrict__ range) {
+                                                         int64_t* __restrict__ out_perm) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int32_t* wcnt = reinterpret_cast<int32_t*>(smem);                         // [4][p]
   int64_t* pos = reinterpret_cast<int64_t*>(smem + ((4 * p * 4 + 15) & ~15));  // [kBlock]
@@ -276,44 +312,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_scatter(const int64_t* __restri
     for (int q = 0; q < w; ++q) inb += wcnt[q * p + d];
     const int64_t ps = off[(int64_t)d * nblk + b] + inb;
     MP4X_DASSERT(ps >= 0 && ps < n);
-    out_keys[ps] = k;
+    out_keys[ps * key_stride] = k;       // stride 2: the key half of a 16-byte {key, -} vector
     if (out_perm) out_perm[ps] = i;
     pos[tid] = ps;
-  }
-  if (b == 0 && counts)
-    for (int q = tid; q < p; q += kBlock) {
-      const int64_t last = (int64_t)p * nblk - 1;
-      const int64_t end = (q + 1 < p) ? off[(int64_t)(q + 1) * nblk] : off[last] + hist[last];
-      counts[q] = end - off[(int64_t)q * nblk];
-    }
-  if (b == 0 && range) {                 // the key range: every tile's min / max (k_pack_hist)
-    __syncthreads();
-    int64_t lo = INT64_MAX, hi = INT64_MIN;
-    for (int64_t q = tid; q < nblk; q += kBlock) {
-      lo = bmin[q] < lo ? bmin[q] : lo;
-      hi = bmax[q] > hi ? bmax[q] : hi;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      const int64_t a = __shfl_xor(lo, o, 64), c = __shfl_xor(hi, o, 64);
-      lo = a < lo ? a : lo;
-      hi = c > hi ? c : hi;
-    }
-    __shared__ int64_t rmin[kBlock / 64], rmax[kBlock / 64];
-    if (lane == 0) {
-      rmin[w] = lo;
-      rmax[w] = hi;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      for (int q = 1; q < kBlock / 64; ++q) {
-        lo = rmin[q] < rmin[0] ? rmin[q] : rmin[0];
-        hi = rmax[q] > rmax[0] ? rmax[q] : rmax[0];
-        rmin[0] = lo;
-        rmax[0] = hi;
-      }
-      range[0] = rmin[0];
-      range[1] = rmax[0];
-    }
   }
   if (!vals) return;
   __syncthreads();
@@ -449,43 +450,85 @@ extern "C" size_t mp4x_partition_pack_scratch_bytes(int64_t n, int p) {
          pack_align(cub_bytes);
 }
 
-// keys[n] (+ rows vals[n][row_bytes]) -> stable-by-owner layout out_keys / out_vals, optional
-// out_perm (source index of every output slot), counts[p] (rows per owner) and range[2] (optional:
-// the smallest and largest key; 0, 0 when n == 0).
-extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
-                                   int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts,
-                                   int64_t* range, void* scratch, size_t scratch_bytes, void* stream) {
+namespace {
+struct PackScratch {
+  int64_t nblk, m;
+  int64_t *hist, *off, *bmin, *bmax;
+  void* temp;
+  size_t temp_bytes;
+};
+
+PackScratch pack_scratch(void* scratch, size_t scratch_bytes, int64_t n, int p) {
+  PackScratch S;
+  S.nblk = (n + kBlock - 1) / kBlock;
+  S.m = (int64_t)p * S.nblk;
+  char* sc = (char*)scratch;
+  S.hist = (int64_t*)sc;
+  S.off = (int64_t*)(sc + pack_align(S.m * sizeof(int64_t)));
+  S.bmin = (int64_t*)(sc + 2 * pack_align(S.m * sizeof(int64_t)));
+  S.bmax = (int64_t*)((char*)S.bmin + pack_align(S.nblk * sizeof(int64_t)));
+  const size_t head = 2 * pack_align(S.m * sizeof(int64_t)) + 2 * pack_align(S.nblk * sizeof(int64_t));
+  S.temp = sc + head;
+  S.temp_bytes = scratch_bytes - head;
+  return S;
+}
+}  // namespace
+
+// K4b in two halves, so a caller can exchange the counts before it picks where the packed rows
+// go (the sparse owner exchange scatters them straight into its IPC staging buffer).
+// Count: per-tile owner histogram + scan -> counts[p] (rows per owner) and range[2] (optional: the
+// smallest and largest key; 0, 0 when n == 0).  The scratch then holds the scan for the scatter.
+extern "C" int mp4x_partition_pack_count(const int64_t* keys, int64_t n, int p, int64_t* counts, int64_t* range,
+                                         void* scratch, size_t scratch_bytes, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (p < 1 || p > kPackMaxP) return MP4X_E_BADARG;
+  if (p < 1 || p > kPackMaxP || !counts) return MP4X_E_BADARG;
   if (n <= 0) {
-    if (counts)
-      if (hipError_t e = hipMemsetAsync(counts, 0, p * sizeof(int64_t), st)) return (int)e;
+    if (hipError_t e = hipMemsetAsync(counts, 0, p * sizeof(int64_t), st)) return (int)e;
     return range ? (int)hipMemsetAsync(range, 0, 2 * sizeof(int64_t), st) : 0;
   }
   if (n > INT32_MAX / 2) return MP4X_E_BADARG;
-  if (vals && ((row_bytes & 15) || ((((uintptr_t)vals | (uintptr_t)out_vals) & 15)))) return MP4X_E_BADARG;
   if (scratch_bytes < mp4x_partition_pack_scratch_bytes(n, p)) return MP4X_E_BADARG;
-  const int64_t nblk = (n + kBlock - 1) / kBlock;
-  const int64_t m = (int64_t)p * nblk;
-  char* sc = (char*)scratch;
-  int64_t* hist = (int64_t*)sc;
-  int64_t* off = (int64_t*)(sc + pack_align(m * sizeof(int64_t)));
-  int64_t* bmin = (int64_t*)(sc + 2 * pack_align(m * sizeof(int64_t)));
-  int64_t* bmax = (int64_t*)((char*)bmin + pack_align(nblk * sizeof(int64_t)));
-  const size_t head = 2 * pack_align(m * sizeof(int64_t)) + 2 * pack_align(nblk * sizeof(int64_t));
-  void* temp = sc + head;
-  size_t temp_bytes = scratch_bytes - head;
-  hipLaunchKernelGGL(k_pack_hist, dim3(nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, nblk, hist,
-                     range ? bmin : nullptr, range ? bmax : nullptr);
+  PackScratch S = pack_scratch(scratch, scratch_bytes, n, p);
+  hipLaunchKernelGGL(k_pack_hist, dim3(S.nblk), dim3(kBlock), p * sizeof(int32_t), st, keys, n, p, S.nblk, S.hist,
+                     range ? S.bmin : nullptr, range ? S.bmax : nullptr);
   int e = (int)hipGetLastError();
   if (e) return e;
-  e = (int)rocprim::exclusive_scan(temp, temp_bytes, hist, off, (int64_t)0, (size_t)m, rocprim::plus<int64_t>(), st);
+  e = (int)rocprim::exclusive_scan(S.temp, S.temp_bytes, S.hist, S.off, (int64_t)0, (size_t)S.m,
+                                   rocprim::plus<int64_t>(), st);
   if (e) return e;
+  hipLaunchKernelGGL(k_pack_counts, dim3(1), dim3(kBlock), 0, st, (const int64_t*)S.off, (const int64_t*)S.hist, p,
+                     S.nblk, counts, (const int64_t*)S.bmin, (const int64_t*)S.bmax, range);
+  return (int)hipGetLastError();
+}
+
+// Scatter (after mp4x_partition_pack_count on the same keys, p and scratch): out_keys (key_stride
+// 1: int64[n]; 2: the key half of n 16-byte vectors) / out_vals (rows of row_bytes, 16-B aligned;
+// vals may be NULL) in owner-major, input-stable order; out_perm (optional) = source row of
+// every slot.
+extern "C" int mp4x_partition_pack_scatter(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes,
+                                           int p, int64_t* out_keys, int key_stride, void* out_vals,
+                                           int64_t* out_perm, void* scratch, size_t scratch_bytes, void* stream) {
+  if (n <= 0) return 0;
+  if (p < 1 || p > kPackMaxP || n > INT32_MAX / 2 || (key_stride != 1 && key_stride != 2)) return MP4X_E_BADARG;
+  if (vals && ((row_bytes & 15) || ((((uintptr_t)vals | (uintptr_t)out_vals) & 15)))) return MP4X_E_BADARG;
+  if (scratch_bytes < mp4x_partition_pack_scratch_bytes(n, p)) return MP4X_E_BADARG;
+  const PackScratch S = pack_scratch(scratch, scratch_bytes, n, p);
   const int64_t V = vals ? row_bytes / 16 : 0;
   int G = 1;
   while (G < V && G < 64) G <<= 1;
   const size_t lds = ((4 * p * 4 + 15) & ~15) + kBlock * sizeof(int64_t);
-  hipLaunchKernelGGL(k_pack_scatter, dim3(nblk), dim3(kBlock), lds, st, keys, (const u32x4*)vals, n, V, G, p, nblk,
-                     off, hist, out_keys, (u32x4*)out_vals, out_perm, counts, bmin, bmax, range);
+  hipLaunchKernelGGL(k_pack_scatter, dim3(S.nblk), dim3(kBlock), lds, (hipStream_t)stream, keys, (const u32x4*)vals,
+                     n, V, G, p, S.nblk, (const int64_t*)S.off, out_keys, key_stride, (u32x4*)out_vals, out_perm);
   return (int)hipGetLastError();
+}
+
+// Both halves: keys[n] (+ rows vals[n][row_bytes]) -> stable-by-owner layout out_keys / out_vals,
+// optional out_perm, counts[p] and range[2] (optional).
+extern "C" int mp4x_partition_pack(const int64_t* keys, const void* vals, int64_t n, int64_t row_bytes, int p,
+                                   int64_t* out_keys, void* out_vals, int64_t* out_perm, int64_t* counts,
+                                   int64_t* range, void* scratch, size_t scratch_bytes, void* stream) {
+  if (vals && ((row_bytes & 15) || ((((uintptr_t)vals | (uintptr_t)out_vals) & 15)))) return MP4X_E_BADARG;
+  if (int e = mp4x_partition_pack_count(keys, n, p, counts, range, scratch, scratch_bytes, stream)) return e;
+  return mp4x_partition_pack_scatter(keys, vals, n, row_bytes, p, out_keys, 1, out_vals, out_perm, scratch,
+                                     scratch_bytes, stream);
 }

@@ -7,7 +7,7 @@ the current torch stream.
 from __future__ import annotations
 
 import os
-from typing import Optional, Sequence, Tuple
+from typing import NamedTuple, Optional, Sequence, Tuple
 
 import torch
 
@@ -296,6 +296,53 @@ def partition_pack(keys: torch.Tensor, vals: Optional[torch.Tensor], p: int, wan
     if vals is not None and not fused_rows and n:
         gather_rows(vals.view(n, -1), perm, out=out_vals.view(n, -1), stream=stream)
     return out_keys, out_vals, counts, perm
+
+
+class PackCount(NamedTuple):
+    """The first half of K4b (:func:`partition_count`): ``info`` = counts[p] + [min key, max
+    key]; ``scratch`` holds the scan the second half (:func:`partition_scatter`) reads."""
+    keys: torch.Tensor
+    p: int
+    info: torch.Tensor
+    scratch: torch.Tensor
+
+
+def partition_count(keys: torch.Tensor, p: int, stream=None) -> PackCount:
+    """K4b's histogram + scan: rows per owner ``(uint64)key % p`` and the key range, with no rows
+    moved yet (the caller can exchange the counts first)."""
+    _dev_check(keys)
+    if keys.dtype != torch.int64:
+        raise ValueError("partition_count: keys must be int64")
+    if not 1 <= p <= PACK_MAX_P:
+        raise ValueError(f"partition_count: p must be in [1, {PACK_MAX_P}]")
+    n = keys.numel()
+    lib = native.hip()
+    sb = lib.mp4x_partition_pack_scratch_bytes(n, p)
+    scratch = torch.empty(max(sb, 1), dtype=torch.uint8, device=keys.device)
+    info = torch.empty(p + 2, dtype=torch.int64, device=keys.device)
+    check(lib.mp4x_partition_pack_count(keys.data_ptr(), n, p, info.data_ptr(), info.data_ptr() + 8 * p,
+                                        scratch.data_ptr(), sb, stream_ptr(stream)), "mp4x_partition_pack_count")
+    return PackCount(keys, p, info, scratch)
+
+
+def partition_scatter(pc: PackCount, vals: Optional[torch.Tensor], out_vals_ptr: int, out_keys_ptr: int,
+                      key_stride: int = 1, stream=None) -> None:
+    """K4b's scatter after :func:`partition_count`: rows of ``vals`` (whole 16-byte vectors) to
+    device address ``out_vals_ptr`` and keys to ``out_keys_ptr`` (``key_stride`` 2: the key half
+    of 16-byte vectors) in stable owner-major order."""
+    keys = pc.keys
+    n = keys.numel()
+    if n == 0:
+        return
+    _dev_check(keys, vals)
+    rb = 0 if vals is None else vals[0].numel() * vals.element_size()
+    if rb % 16 or (vals is not None and vals.shape[0] != n):
+        raise ValueError("partition_scatter: rows of whole 16-byte vectors, one per key")
+    check(native.hip().mp4x_partition_pack_scatter(keys.data_ptr(), vals.data_ptr() if vals is not None else None, n,
+                                                   rb, pc.p, out_keys_ptr, int(key_stride),
+                                                   out_vals_ptr if vals is not None else None, None,
+                                                   pc.scratch.data_ptr(), pc.scratch.numel(), stream_ptr(stream)),
+          "mp4x_partition_pack_scatter")
 
 
 # int64 key sorts: rocPRIM's own dispatch (block sort + merge passes below 1 M items, whatever the

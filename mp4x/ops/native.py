@@ -61,6 +61,9 @@ _HIP_SIGS = {
     "mp4x_partition_pack_scratch_bytes": (c_size_t, [c_int64, c_int]),
     "mp4x_partition_pack": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mp4x_partition_pack_count": (c_int, [c_void_p, c_int64, c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "mp4x_partition_pack_scatter": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int, c_void_p, c_int, c_void_p,
+                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_rle_temp_bytes": (c_size_t, [c_int64]),
     "mp4x_run_starts": (c_int, [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "mp4x_segment_reduce_rows": (c_int, [c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int64,

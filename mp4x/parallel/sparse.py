@@ -274,11 +274,13 @@ def _sparse_ipc_ok(engine, keys: torch.Tensor) -> bool:
         engine.coll.__class__.__name__ == "TorchColl" and not capturing_now() and engine.ipc() is not None
 
 
-def _split_exchange(engine, keys, vals, rb: int, nmax: int, blocks, grid_rows: int):
+def _split_exchange(engine, keys, vals, rb: int, nmax: int, blocks, grid_rows: int, stage=None):
     """Stage (keys, rows) in this rank's buffer (rows at vector 0, keys at ``nmax * V``) and run
     one copy plan; ``blocks`` = [(peer, src_row, rows)] pulled in order; ``grid_rows`` = the
-    largest block of ANY rank (the plan's grid must be rank-independent).  Returns the received
-    (keys, rows), or None when the largest rank's payload does not fit (rank-independent)."""
+    largest block of ANY rank (the plan's grid must be rank-independent).  ``stage(rows_ptr,
+    keys16_ptr)`` writes the staged layout itself (the owner exchange's pack scatters straight
+    into the buffer); default: a copy of ``keys`` / ``vals``.  Returns the received (keys, rows),
+    or None when the largest rank's payload does not fit (rank-independent)."""
     from ..ops.device_ops import keys_from16, stage_split
     inst = _ipc_inst(engine, nmax * (rb + 16))
     if inst is None:
@@ -287,7 +289,10 @@ def _split_exchange(engine, keys, vals, rb: int, nmax: int, blocks, grid_rows: i
     koff = nmax * V                               # first key vector: the same on every rank
     inst._launch_stream()                         # the communicator's stream order, then stage
     base = inst._data.value
-    stage_split(keys.contiguous(), vals.contiguous() if vals is not None else None, base, base + koff * 16)
+    if stage is not None:
+        stage(base, base + koff * 16)
+    else:
+        stage_split(keys.contiguous(), vals.contiguous() if vals is not None else None, base, base + koff * 16)
     total = sum(c for _, _, c in blocks)
     out = torch.empty(total * (rb + 16), dtype=torch.uint8, device=keys.device)
     pulls, off = [], 0
@@ -307,17 +312,18 @@ def _split_exchange(engine, keys, vals, rb: int, nmax: int, blocks, grid_rows: i
     return rk, rv
 
 
-def _ipc_alltoallv(engine, skeys, svals, mat: List[List[int]]):
+def _ipc_alltoallv(engine, skeys, svals, mat: List[List[int]], stage=None):
     """Owner exchange over the IPC mesh; ``mat[i][j]`` = rows rank i sends to rank j.  Returns
     (keys, rows) received in source-rank order, or None when rows are not 16-byte vectors or the
-    largest rank's payload exceeds the staging buffers (both rank-independent)."""
+    largest rank's payload exceeds the staging buffers (both rank-independent).  ``stage``: see
+    :func:`_split_exchange` (then ``skeys`` / ``svals`` only give the device, shapes and dtype)."""
     rb = _row_bytes(svals)
     if rb < 0:
         return None
     p, r = engine.p, engine.rank
     blocks = [(j, sum(mat[j][:r]), mat[j][r]) for j in range(p)]     # rank j's block for this rank
     got = _split_exchange(engine, skeys, svals, rb, max(sum(row) for row in mat), blocks,
-                          max(max(row) for row in mat))
+                          max(max(row) for row in mat), stage)
     if got is not None:
         engine._count("sparse.a2a.ipc")
     return got
@@ -409,9 +415,27 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     radix sort's width) when the count exchange carried the ranks' key ranges, else None."""
     p = engine.p
     ipc = _sparse_ipc_ok(engine, keys)
-    skeys, svals, hist = _pack_by_owner(keys, vals, p, want_range=ipc)
     bits = None
-    if ipc:
+    from ..ops.device_ops import PACK_MAX_P
+    if ipc and p <= PACK_MAX_P and _row_bytes(vals) >= 0:
+        # K4b in two halves: count, exchange the counts (they pick the staging instance), then
+        # scatter the owner-sorted rows and keys straight into the staging buffer
+        from ..ops.device_ops import partition_count, partition_scatter
+        keys = keys.contiguous()
+        vals = vals.contiguous() if vals is not None else None
+        pc = partition_count(keys, p)
+        mat, bits = _split_info(_count_matrix(engine, pc.info), p)
+        got = _ipc_alltoallv(engine, keys, vals, mat,
+                             stage=lambda rows_ptr, keys16_ptr: partition_scatter(pc, vals, rows_ptr, keys16_ptr, 2))
+        if got is not None:
+            return got[0], got[1], bits
+        skeys = torch.empty_like(keys)                 # too large for the staging buffers
+        svals = torch.empty_like(vals) if vals is not None else None
+        partition_scatter(pc, vals, svals.data_ptr() if vals is not None else 0, skeys.data_ptr())
+        send = mat[engine.rank]
+        recv = [mat[j][engine.rank] for j in range(p)]
+    elif ipc:
+        skeys, svals, hist = _pack_by_owner(keys, vals, p, want_range=True)
         mat, bits = _split_info(_count_matrix(engine, hist), p)
         got = _ipc_alltoallv(engine, skeys, svals, mat)
         if got is not None:
@@ -419,6 +443,7 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
         send = mat[engine.rank]
         recv = [mat[j][engine.rank] for j in range(p)]
     else:
+        skeys, svals, hist = _pack_by_owner(keys, vals, p)
         recv_counts = torch.empty_like(hist)
         engine.coll.all_to_all_single(recv_counts, hist)
         send, recv = torch.stack([hist, recv_counts]).tolist()      # one host sync for both

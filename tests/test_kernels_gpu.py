@@ -394,3 +394,26 @@ def test_sort_pairs_onesweep_matches_rocprim_dispatch(n, bits):
     ref = torch.argsort(keys.cpu(), stable=True)
     assert torch.equal(i0.cpu(), ref) and torch.equal(i1.cpu(), ref)
     assert torch.equal(k0, k1)
+
+
+@pytest.mark.parametrize("n,p,dim", [(0, 4, 16), (1, 3, 4), (70_001, 8, 64), (5000, 1000, 8)])
+def test_partition_pack_halves_match_the_fused_pack(n, p, dim):
+    """K4b split in two (count, then scatter anywhere — the sparse exchange scatters straight into
+    its staging buffer): the same layout as partition_pack, keys at stride 1 or as the key half
+    of 16-byte vectors, and the counts + key range of want_range."""
+    K = _native()
+    g = torch.Generator(device="cpu").manual_seed(n + p)
+    keys = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g, dtype=torch.int64).to(DEV)
+    vals = torch.randn(n, dim, generator=g).to(DEV)
+    sk, sv, counts, _ = K.partition_pack(keys, vals, p, want_range=True)
+    pc = K.partition_count(keys, p)
+    assert torch.equal(pc.info, counts)
+    k1 = torch.empty_like(keys)
+    v1 = torch.empty_like(vals)
+    K.partition_scatter(pc, vals, v1.data_ptr(), k1.data_ptr())
+    k2 = torch.zeros(n, 2, dtype=torch.int64, device=DEV)
+    v2 = torch.empty_like(vals)
+    K.partition_scatter(pc, vals, v2.data_ptr(), k2.data_ptr(), key_stride=2)
+    torch.cuda.synchronize()
+    assert torch.equal(k1, sk) and torch.equal(v1, sv)
+    assert torch.equal(k2[:, 0], sk) and torch.equal(v2, sv) and not k2[:, 1].any()
