@@ -98,3 +98,23 @@ def test_alltoallv_rows_over_ipc(p, dim, dtype_name, ipc):
     for r, (ok, st) in out.items():
         assert ok, r
         assert (st.get("all_to_all_v.ipc", 0) == 1) == ipc, st
+
+
+def test_sparse_exchange_too_large_for_staging_takes_the_transport():
+    """Payloads above both staging buffers (shrunk here to 1 / 2 MiB): the owner exchange counts
+    (K4b first half), finds no instance that fits on ANY rank, scatters into plain tensors and
+    runs the transport's all-to-all; results exact, no IPC exchange counted."""
+    p, dim, n = 3, 64, 20000
+    env = {"MP4X_IPC_BYTES": str(1 << 20), "MP4X_IPC_LARGE_BYTES": str(2 << 20)}
+    out = run_spawn(p, _sparse_fn, args=(dim, "float32", n, -1, 0), env=env)
+    ins = [_data(j, dim, torch.float32, n) for j in range(p)]
+    ref = {}
+    for k, v in ins:
+        for kk, vv in zip(k.tolist(), v.float()):
+            ref[kk] = ref[kk] + vv if kk in ref else vv.clone()
+    for r, (rk, rv, gk, gv, sizes, used) in out.items():
+        rk, rv = torch.from_numpy(rk), torch.from_numpy(rv)
+        assert sorted(rk.tolist()) == sorted(ref)
+        got = dict(zip(rk.tolist(), rv))
+        assert all(torch.equal(got[kk], ref[kk]) for kk in ref), r
+        assert "sparse.a2a.ipc" not in used and "sparse.allgatherv.ipc" not in used, used
