@@ -51,12 +51,12 @@ def worker(port, q, nkeys, dim, iters):
         t = time.perf_counter()
         pc = K.partition_count(ids, eng.p)                     # K4b first half: counts + key range
         t = tick("pack_count", t)
-        mat, bits = sp._split_info(sp._count_matrix(eng, pc.info), eng.p)
+        mat, bits, rng = sp._split_info(sp._count_matrix(eng, pc.info), eng.p, with_range=True)
         t = tick("count_matrix", t)
         rk, rv = sp._ipc_alltoallv(eng, ids, vals, mat,         # scatter into staging + the plan
                                    stage=lambda a, b: K.partition_scatter(pc, vals, a, b, 2))
         t = tick("ipc_alltoallv", t)
-        uk, uv, _ = sp._reduce_by_key(rk, rv, op, bits)
+        uk, uv, _ = sp._reduce_by_key(rk, rv, op, bits, sp._dense_plan(rng, eng.p, rk))
         t = tick("reduce_by_key", t)
         sizes = sp._row_counts(eng, uk.shape[0], uk.device)
         t = tick("row_counts", t)

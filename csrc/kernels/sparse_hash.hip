@@ -21,6 +21,7 @@
 //            the rows in that order (= input = rank order): the same values, bit for bit, as the
 //            sort path, which also combines in input order
 //
+#include <rocprim/device/device_scan.hpp>
 #include <type_traits>
 
 #include "common.hpp"
@@ -239,6 +240,105 @@ __global__ __launch_bounds__(kBlock) void k_hash_reduce(const int32_t* __restric
   }
 }
 
+// ---------------------------------------------------------------- K5d: dense keys
+// When the keys of a reduce-by-key are dense — k / stride - base in [0, T) with T a small multiple
+// of n (dictionary ids; an owner's share of them, stride = p) — the hash is the identity: no
+// probing, and the occupied slots in slot order ARE the keys in ascending order.  The same row
+// lists and in-order reduce as K5h, so the output is the sort path's, bit for bit and in the same
+// (ascending) key order.  A key outside [0, T) or two keys on one slot set m_flag[1]: the caller
+// falls back to the sort path.
+__global__ __launch_bounds__(kBlock) void k_dense_init(unsigned long long* __restrict__ tkeys,
+                                                       int32_t* __restrict__ thead, int64_t T,
+                                                       unsigned long long* __restrict__ m_flag) {
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t0 == 0) {
+    m_flag[0] = 0;
+    m_flag[1] = 0;
+  }
+  for (int64_t h = t0; h < T; h += nthr) {
+    tkeys[h] = kHashEmpty;
+    thead[h] = -1;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_dense_insert(const int64_t* __restrict__ keys, int64_t n, int64_t base,
+                                                         int64_t stride, int64_t T,
+                                                         unsigned long long* __restrict__ tkeys,
+                                                         int32_t* __restrict__ thead, int32_t* __restrict__ next,
+                                                         unsigned long long* __restrict__ m_flag) {
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) {
+    const int64_t k = keys[i];
+    const int64_t h = k >= 0 ? k / stride - base : -1;
+    if (h < 0 || h >= T) {                               // not dense after all
+      atomicOr(&m_flag[1], 1ull);
+      next[i] = -1;
+      continue;
+    }
+    const unsigned long long cur = atomicCAS(&tkeys[h], kHashEmpty, (unsigned long long)k);
+    if (cur != kHashEmpty && cur != (unsigned long long)k) atomicOr(&m_flag[1], 1ull);   // two keys, one slot
+    next[i] = atomicExch(&thead[h], (int32_t)i);
+  }
+}
+
+// Tiles of kBlock * kCompactPer consecutive slots, kCompactPer consecutive slots per lane (so
+// the dense run index follows the slot order): the occupied count of every tile.
+__global__ __launch_bounds__(kBlock) void k_dense_count(const int32_t* __restrict__ thead, int64_t T,
+                                                        int64_t* __restrict__ tile_cnt) {
+  __shared__ int s_sum[kBlock / 64];
+  const int64_t h0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kCompactPer;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactPer; ++j) c += (h0 + j < T && thead[h0 + j] >= 0) ? 1 : 0;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int q = 0; q < kBlock / 64; ++q) t += s_sum[q];
+    tile_cnt[blockIdx.x] = t;
+  }
+}
+
+// Dense run indices in slot order: the tile's base (scanned) + the lane prefix in LDS.
+__global__ __launch_bounds__(kBlock) void k_dense_compact(const unsigned long long* __restrict__ tkeys,
+                                                          const int32_t* __restrict__ thead, int64_t T,
+                                                          const int64_t* __restrict__ tile_base,
+                                                          const int64_t* __restrict__ tile_cnt, int64_t ntiles,
+                                                          int64_t* __restrict__ out_keys,
+                                                          int32_t* __restrict__ rhead,
+                                                          unsigned long long* __restrict__ m_flag) {
+  __shared__ int s_pre[kBlock];
+  const int64_t h0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * kCompactPer;
+  int mine = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactPer; ++j) mine += (h0 + j < T && thead[h0 + j] >= 0) ? 1 : 0;
+  s_pre[threadIdx.x] = mine;
+  __syncthreads();
+  for (int off = 1; off < kBlock; off <<= 1) {           // inclusive Hillis-Steele scan in LDS
+    const int v = threadIdx.x >= off ? s_pre[threadIdx.x - off] : 0;
+    __syncthreads();
+    s_pre[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int64_t u = tile_base[blockIdx.x] + s_pre[threadIdx.x] - mine;
+#pragma unroll
+  for (int j = 0; j < kCompactPer; ++j) {
+    const int64_t h = h0 + j;
+    if (h < T) {
+      const int32_t hd = thead[h];
+      if (hd >= 0) {
+        out_keys[u] = (int64_t)tkeys[h];
+        rhead[u] = hd;
+        ++u;
+      }
+    }
+  }
+  if (blockIdx.x == ntiles - 1 && threadIdx.x == 0)
+    m_flag[0] = (unsigned long long)(tile_base[ntiles - 1] + tile_cnt[ntiles - 1]);
+}
+
 int64_t table_slots(int64_t n) {
   int64_t t = 1024;
   while (t < 2 * n) t <<= 1;
@@ -308,6 +408,34 @@ int reduce_dt(int op, const int32_t* rhead, const int32_t* next, const unsigned 
 
 }  // namespace mp4x
 
+namespace mp4x {
+namespace {
+struct DenseLayout {
+  size_t tkeys, thead, next, rhead, tcnt, tbase, temp, total, temp_bytes;
+  int64_t ntiles;
+};
+
+DenseLayout dense_layout(int64_t n, int64_t T) {
+  DenseLayout L;
+  const int64_t tile = (int64_t)kBlock * kCompactPer;
+  L.ntiles = (T + tile - 1) / tile;
+  size_t o = 0;
+  L.tkeys = o;  o += align256((size_t)T * 8);
+  L.thead = o;  o += align256((size_t)T * 4);
+  L.next = o;   o += align256((size_t)n * 4);
+  L.rhead = o;  o += align256((size_t)(n < T ? n : T) * 4);
+  L.tcnt = o;   o += align256((size_t)L.ntiles * 8);
+  L.tbase = o;  o += align256((size_t)L.ntiles * 8);
+  L.temp_bytes = 0;
+  (void)rocprim::exclusive_scan(nullptr, L.temp_bytes, (const int64_t*)nullptr, (int64_t*)nullptr, (int64_t)0,
+                                (size_t)(L.ntiles < 1 ? 1 : L.ntiles), rocprim::plus<int64_t>(), (hipStream_t)0);
+  L.temp = o;   o += align256(L.temp_bytes);
+  L.total = o;
+  return L;
+}
+}  // namespace
+}  // namespace mp4x
+
 using namespace mp4x;
 
 extern "C" size_t mp4x_hash_rbk_scratch_bytes(int64_t n) { return layout(n < 0 ? 0 : n).total; }
@@ -351,6 +479,59 @@ extern "C" int mp4x_hash_reduce_by_key(int dtype, int op, const int64_t* keys, i
                      (const SideRun*)side);
   if (int e = (int)hipGetLastError()) return e;
   const unsigned long long* m_dev = counter;
+  switch (dtype) {
+    case MP4X_F64: return reduce_dt<MP4X_F64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_F32: return reduce_dt<MP4X_F32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I64: return reduce_dt<MP4X_I64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I32: return reduce_dt<MP4X_I32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_BF16: return reduce_dt<MP4X_BF16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_F16: return reduce_dt<MP4X_F16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I16: return reduce_dt<MP4X_I16>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_I8: return reduce_dt<MP4X_I8>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    case MP4X_U8: return reduce_dt<MP4X_U8>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
+    default: return MP4X_E_UNSUPPORTED;
+  }
+}
+
+extern "C" size_t mp4x_dense_rbk_scratch_bytes(int64_t n, int64_t T) {
+  return dense_layout(n < 0 ? 0 : n, T < 1 ? 1 : T).total;
+}
+
+// K5d: keys[n] with k / stride - base in [0, T) (e.g. an owner's share of dense ids, stride = p),
+// vals[n][dim] -> out_keys[m] ascending, out_vals[m][dim] (rows combined in input order: the sort
+// path's result bit for bit), out_count[m] (optional); m_flag[0] = m, m_flag[1] != 0 when the keys
+// were not dense after all (then nothing else is meaningful: use the sort path).
+extern "C" int mp4x_dense_reduce_by_key(int dtype, int op, const int64_t* keys, int64_t n, const void* vals,
+                                        int64_t dim, int64_t base, int64_t stride, int64_t T, void* scratch,
+                                        size_t scratch_bytes, int64_t* out_keys, void* out_vals, int32_t* out_count,
+                                        int64_t* m_flag, void* stream) {
+  if (!mp4x_hash_rbk_supported(dtype, op) || n <= 0 || dim <= 0 || n >= (1ll << 30) || T < 1 || T >= (1ll << 31) ||
+      stride < 1 || base < 0)
+    return MP4X_E_UNSUPPORTED;
+  const DenseLayout L = dense_layout(n, T);
+  if (scratch_bytes < L.total || ((uintptr_t)scratch & 255) || ((uintptr_t)m_flag & 7)) return MP4X_E_BADARG;
+  hipStream_t st = (hipStream_t)stream;
+  char* p = (char*)scratch;
+  auto* tkeys = (unsigned long long*)(p + L.tkeys);
+  auto* thead = (int32_t*)(p + L.thead);
+  auto* next = (int32_t*)(p + L.next);
+  auto* rhead = (int32_t*)(p + L.rhead);
+  auto* tcnt = (int64_t*)(p + L.tcnt);
+  auto* tbase = (int64_t*)(p + L.tbase);
+  auto* flag = (unsigned long long*)m_flag;
+  hipLaunchKernelGGL(k_dense_init, dim3(grid_for(T, 2)), dim3(kBlock), 0, st, tkeys, thead, T, flag);
+  hipLaunchKernelGGL(k_dense_insert, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, keys, n, base, stride, T, tkeys, thead,
+                     next, flag);
+  hipLaunchKernelGGL(k_dense_count, dim3((unsigned)L.ntiles), dim3(kBlock), 0, st, (const int32_t*)thead, T, tcnt);
+  size_t tb = L.temp_bytes;
+  if (hipError_t e = rocprim::exclusive_scan(p + L.temp, tb, (const int64_t*)tcnt, tbase, (int64_t)0, (size_t)L.ntiles,
+                                             rocprim::plus<int64_t>(), st))
+    return (int)e;
+  hipLaunchKernelGGL(k_dense_compact, dim3((unsigned)L.ntiles), dim3(kBlock), 0, st, (const unsigned long long*)tkeys,
+                     (const int32_t*)thead, T, (const int64_t*)tbase, (const int64_t*)tcnt, L.ntiles, out_keys, rhead,
+                     flag);
+  if (int e = (int)hipGetLastError()) return e;
+  const unsigned long long* m_dev = flag;
   switch (dtype) {
     case MP4X_F64: return reduce_dt<MP4X_F64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
     case MP4X_F32: return reduce_dt<MP4X_F32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);

@@ -74,6 +74,9 @@ _HIP_SIGS = {
     "mp4x_hash_rbk_supported": (c_int, [c_int, c_int]),
     "mp4x_hash_reduce_by_key": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_size_t,
                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "mp4x_dense_rbk_scratch_bytes": (c_size_t, [c_int64, c_int64]),
+    "mp4x_dense_reduce_by_key": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64, c_int64,
+                                         c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mp4x_set_k1_variant": (None, [c_int]),
     "mp4x_set_k1_grid": (None, [c_int64]),
     "mp4x_version": (ctypes.c_char_p, []),

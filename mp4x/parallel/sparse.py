@@ -26,7 +26,7 @@ from __future__ import annotations
 import itertools
 import os
 from collections.abc import MutableMapping
-from typing import Dict, List, Optional
+from typing import Dict, List, NamedTuple, Optional
 
 import numpy as np
 import torch
@@ -159,11 +159,19 @@ def _sync_new_keys(engine, new: List) -> None:
 # the same values bit for bit, 1.4-1.6x faster on config 4's owner rows; keys in table order,
 # which depends on the CAS races of colliding keys).  A/B: profiles/r6/sparse/v3_*.
 RBK_MODE = os.environ.get("MP4X_SPARSE_RBK", "sort").lower()
-def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bits: Optional[int] = None):
+def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bits: Optional[int] = None,
+                   dense=None):
     """``key_bits``: every key is in [0, 2**key_bits) (dense dictionary ids) — the radix sort
-    covers those bits only."""
+    covers those bits only.  ``dense`` = (base, stride, T) from :func:`_dense_plan`: K5d runs
+    instead (no sort; the same result, order included) unless the keys turn out not dense."""
     if keys.is_cuda:
         from ..ops.device_ops import reduce_by_key
+        if dense is not None and vals is not None and RBK_MODE != "hash" and not getattr(op, "is_custom", False):
+            from ..ops.device_ops import dense_reduce_by_key, hash_rbk_supported
+            if hash_rbk_supported(vals.dtype, int(op.code)):
+                got = dense_reduce_by_key(keys, vals, int(op.code), *dense)
+                if got is not None:
+                    return got
         if vals is not None and RBK_MODE == "hash" and not getattr(op, "is_custom", False):
             from ..ops.device_ops import hash_rbk_supported, hash_reduce_by_key
             if hash_rbk_supported(vals.dtype, int(op.code)):
@@ -400,22 +408,47 @@ def _owner_info(keys: torch.Tensor, hist: torch.Tensor) -> torch.Tensor:
     return torch.cat([hist, mn.view(1), mx.view(1)])
 
 
-def _split_info(rows: List[List[int]], p: int):
-    """(count matrix, key bits of every rank's keys or None) from the :func:`_owner_info` rows."""
+class KeyRange(NamedTuple):
+    """Every rank's keys lie in [lo, hi] (carried by the count exchange); ``bits`` bounds them for
+    the radix sort (None when a key is negative)."""
+    lo: int
+    hi: int
+    bits: Optional[int]
+
+
+def _split_info(rows: List[List[int]], p: int, with_range: bool = False):
+    """(count matrix, key bits of every rank's keys or None[, KeyRange]) from the
+    :func:`_owner_info` rows."""
     mat = [r[:p] for r in rows]
     lo = min(r[p] for r in rows)
     hi = max(r[p + 1] for r in rows)
     bits = max(1, int(hi).bit_length()) if lo >= 0 else None
-    return mat, (bits if bits is not None and bits <= 63 else None)
+    bits = bits if bits is not None and bits <= 63 else None
+    return (mat, bits, KeyRange(lo, hi, bits)) if with_range else (mat, bits)
+
+
+DENSE_FACTOR = float(os.environ.get("MP4X_SPARSE_DENSE_FACTOR", 2.0))
+
+
+def _dense_plan(rng: Optional["KeyRange"], p: int, rkeys: torch.Tensor):
+    """K5d's (base, stride, T) for an owner's received keys — every key k has k % p == this
+    owner, so k // p - lo // p indexes a table of T slots — when that table is at most
+    ``DENSE_FACTOR`` x the rows (dense ids: dictionary numbering, feature ids), else None."""
+    n = rkeys.shape[0]
+    if rng is None or rng.lo < 0 or n == 0 or not rkeys.is_cuda or DENSE_FACTOR <= 0:
+        return None
+    base = rng.lo // p
+    T = rng.hi // p - base + 1
+    return (base, p, T) if T <= DENSE_FACTOR * n else None
 
 
 # ------------------------------------------------------------------ tensor-level API
 def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor]):
-    """(received keys, received rows, key bits): ``key bits`` bounds every received key (the
-    radix sort's width) when the count exchange carried the ranks' key ranges, else None."""
+    """(received keys, received rows, key range): the ranks' :class:`KeyRange` when the count
+    exchange carried it (the IPC path), else None."""
     p = engine.p
     ipc = _sparse_ipc_ok(engine, keys)
-    bits = None
+    rng = None
     from ..ops.device_ops import PACK_MAX_P
     if ipc and p <= PACK_MAX_P and _row_bytes(vals) >= 0:
         # K4b in two halves: count, exchange the counts (they pick the staging instance), then
@@ -424,11 +457,11 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
         keys = keys.contiguous()
         vals = vals.contiguous() if vals is not None else None
         pc = partition_count(keys, p)
-        mat, bits = _split_info(_count_matrix(engine, pc.info), p)
+        mat, _, rng = _split_info(_count_matrix(engine, pc.info), p, with_range=True)
         got = _ipc_alltoallv(engine, keys, vals, mat,
                              stage=lambda rows_ptr, keys16_ptr: partition_scatter(pc, vals, rows_ptr, keys16_ptr, 2))
         if got is not None:
-            return got[0], got[1], bits
+            return got[0], got[1], rng
         skeys = torch.empty_like(keys)                 # too large for the staging buffers
         svals = torch.empty_like(vals) if vals is not None else None
         partition_scatter(pc, vals, svals.data_ptr() if vals is not None else 0, skeys.data_ptr())
@@ -436,10 +469,10 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
         recv = [mat[j][engine.rank] for j in range(p)]
     elif ipc:
         skeys, svals, hist = _pack_by_owner(keys, vals, p, want_range=True)
-        mat, bits = _split_info(_count_matrix(engine, hist), p)
+        mat, _, rng = _split_info(_count_matrix(engine, hist), p, with_range=True)
         got = _ipc_alltoallv(engine, skeys, svals, mat)
         if got is not None:
-            return got[0], got[1], bits
+            return got[0], got[1], rng
         send = mat[engine.rank]
         recv = [mat[j][engine.rank] for j in range(p)]
     else:
@@ -453,7 +486,7 @@ def _exchange_by_owner(engine, keys: torch.Tensor, vals: Optional[torch.Tensor])
     if vals is not None:
         rvals = torch.empty((sum(recv),) + tuple(vals.shape[1:]), dtype=vals.dtype, device=vals.device)
         engine.coll.all_to_all_single(rvals, svals, recv, send)
-    return rkeys, rvals, bits
+    return rkeys, rvals, rng
 
 
 def _row_counts(engine, n: int, device) -> List[int]:
@@ -511,8 +544,9 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, k
     squeeze = vals.dim() == 1
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
-    rkeys, rvals, bits = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or bits)
+    rkeys, rvals, rng = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or (rng.bits if rng else None),
+                               _dense_plan(rng, engine.p, rkeys))
     sizes = _row_counts(engine, uk.shape[0], uk.device)     # one count round for keys AND rows
     got = _ipc_allgatherv(engine, uk, uv, sizes) if _sparse_ipc_ok(engine, uk) else None
     if got is not None:
@@ -598,16 +632,17 @@ def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root
     squeeze = vals.dim() == 1
     v2 = vals.view(-1, 1) if squeeze else vals
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
-    rkeys, rvals, bits = _exchange_by_owner(engine, keys, v2)
-    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or bits)
+    rkeys, rvals, rng = _exchange_by_owner(engine, keys, v2)
+    uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or (rng.bits if rng else None),
+                               _dense_plan(rng, engine.p, rkeys))
     gk, gv = gather_sparse(engine, uk, uv, root, key_bits)    # disjoint owners: K8 dedupe is a no-op
     return gk, (gv.view(-1) if squeeze else gv)
 
 
 def _set_counts(engine, ids: torch.Tensor):
     ids = torch.unique(ids) if not ids.is_cuda else _reduce_by_key(ids, None, None)[0]
-    rkeys, _, bits = _exchange_by_owner(engine, ids, None)
-    return _reduce_by_key(rkeys, None, None, bits)
+    rkeys, _, rng = _exchange_by_owner(engine, ids, None)
+    return _reduce_by_key(rkeys, None, None, rng.bits if rng else None)
 
 
 def set_union(engine, ids: torch.Tensor) -> torch.Tensor:

@@ -87,3 +87,73 @@ def test_sparse_allreduce_in_hash_mode(monkeypatch):
     hk, hv, _ = sparse._reduce_by_key(keys, rows, op)
     o = torch.argsort(hk)
     assert torch.equal(hk[o], sk) and torch.equal(hv[o], sv)
+
+
+def _dense_owner_rows(p, owner, nids, ranks, dim, dtype, seed):
+    """An owner's received rows of DENSE ids (dictionary numbering): every rank holds a random
+    subset of [0, nids); the owner gets the ids with id % p == owner, rank after rank."""
+    g = torch.Generator().manual_seed(seed)
+    ks, vs = [], []
+    for r in range(ranks):
+        ids = torch.randperm(nids, generator=g)[: nids * 2 // 3]
+        ids = ids[ids % p == owner]
+        ks.append(ids)
+        vs.append(torch.randn(ids.numel(), dim, generator=g).to(dtype))
+    return torch.cat(ks).cuda(), torch.cat(vs).cuda()
+
+
+@pytest.mark.parametrize("p,dim,dtype", [(8, 64, torch.float32), (2, 3, torch.float32), (4, 8, torch.bfloat16),
+                                         (1, 16, torch.float64)])
+@pytest.mark.parametrize("op", [0, 1])
+def test_dense_reduce_by_key_is_the_sort_path_bit_for_bit(p, dim, dtype, op):
+    """K5d (direct addressing of dense ids): the same keys IN THE SAME ORDER (ascending), the same
+    values bit for bit (rows combine in input order) and the same counts as the sort path, on
+    random floats."""
+    from mp4x.ops.device_ops import dense_reduce_by_key, reduce_by_key
+    owner = p - 1
+    keys, vals = _dense_owner_rows(p, owner, 300_000, 8, dim, dtype, seed=p * 10 + op)
+    base, T = int(keys.min()) // p, int(keys.max()) // p - int(keys.min()) // p + 1
+    got = dense_reduce_by_key(keys, vals, op, base, p, T)
+    assert got is not None
+    ref = reduce_by_key(keys, vals, op)
+    for a, b in zip(got, ref):
+        assert torch.equal(a, b)
+
+
+def test_dense_reduce_by_key_refuses_keys_that_are_not_dense():
+    """A key outside the table, or two keys on one slot (a wrong stride), is reported (None) —
+    the caller takes the sort path."""
+    from mp4x.ops.device_ops import dense_reduce_by_key
+    keys = torch.tensor([4, 8, 12, 8], device="cuda")
+    vals = torch.ones(4, 4, device="cuda")
+    assert dense_reduce_by_key(keys, vals, 0, 1, 4, 3) is not None          # slots 0, 1, 2
+    assert dense_reduce_by_key(keys, vals, 0, 1, 4, 2) is None              # 12 // 4 - 1 = 2: outside
+    assert dense_reduce_by_key(keys + torch.tensor([0, 1, 0, 0], device="cuda"), vals, 0, 1, 4, 3) is None  # 9, 8
+    assert dense_reduce_by_key(keys - 20, vals, 0, 0, 4, 3) is None         # negative keys
+
+
+def test_sparse_allreduce_of_dense_ids_takes_k5d(monkeypatch):
+    """allreduce_sparse on dense ids routes the owner's reduce-by-key through K5d (keys ascending
+    per owner as before); the fallback on non-dense keys keeps the sort path."""
+    from mp4x.ops import device_ops
+    from mp4x.parallel import sparse
+    calls = []
+    real = device_ops.dense_reduce_by_key
+
+    def spy(*a, **k):
+        out = real(*a, **k)
+        calls.append(out is not None)
+        return out
+    monkeypatch.setattr(device_ops, "dense_reduce_by_key", spy)
+    keys, vals = _dense_owner_rows(4, 1, 100_000, 4, 16, torch.float32, seed=5)
+    rng = sparse.KeyRange(int(keys.min()), int(keys.max()), None)
+    plan = sparse._dense_plan(rng, 4, keys)
+    assert plan is not None
+    from mp4x import Operators
+    from mp4x.operators import dtype_of_torch, for_dtype
+    op = for_dtype(Operators.Float.SUM, dtype_of_torch(vals.dtype))
+    uk, uv, _ = sparse._reduce_by_key(keys, vals, op, None, plan)
+    rk, rv, _ = device_ops.reduce_by_key(keys, vals, 0)
+    assert calls == [True] and torch.equal(uk, rk) and torch.equal(uv, rv)
+    # ids 10x apart: the table would be 10x the rows -> no plan (the sort path)
+    assert sparse._dense_plan(sparse.KeyRange(0, int(keys.max()) * 10, None), 4, keys) is None
