@@ -427,19 +427,23 @@ def _split_info(rows: List[List[int]], p: int, with_range: bool = False):
     return (mat, bits, KeyRange(lo, hi, bits)) if with_range else (mat, bits)
 
 
-DENSE_FACTOR = float(os.environ.get("MP4X_SPARSE_DENSE_FACTOR", 2.0))
+# K5d pays ~12 bytes of table per slot (init, count, compact passes); measured on config 4's owner
+# rows it beats the sort up to ~26 slots per row (0.096 vs 0.140 ms; profiles/r6/sparse/k5d_*)
+DENSE_FACTOR = float(os.environ.get("MP4X_SPARSE_DENSE_FACTOR", 32.0))
+DENSE_MAX_SLOTS = 1 << 26
 
 
 def _dense_plan(rng: Optional["KeyRange"], p: int, rkeys: torch.Tensor):
     """K5d's (base, stride, T) for an owner's received keys — every key k has k % p == this
     owner, so k // p - lo // p indexes a table of T slots — when that table is at most
-    ``DENSE_FACTOR`` x the rows (dense ids: dictionary numbering, feature ids), else None."""
+    ``DENSE_FACTOR`` x the rows (dense or moderately sparse ids: dictionary numbering, feature
+    ids, config 4's ranges) and ``DENSE_MAX_SLOTS``, else None."""
     n = rkeys.shape[0]
     if rng is None or rng.lo < 0 or n == 0 or not rkeys.is_cuda or DENSE_FACTOR <= 0:
         return None
     base = rng.lo // p
     T = rng.hi // p - base + 1
-    return (base, p, T) if T <= DENSE_FACTOR * n else None
+    return (base, p, T) if T <= min(DENSE_FACTOR * n, DENSE_MAX_SLOTS) else None
 
 
 # ------------------------------------------------------------------ tensor-level API

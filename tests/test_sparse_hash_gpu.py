@@ -155,5 +155,6 @@ def test_sparse_allreduce_of_dense_ids_takes_k5d(monkeypatch):
     uk, uv, _ = sparse._reduce_by_key(keys, vals, op, None, plan)
     rk, rv, _ = device_ops.reduce_by_key(keys, vals, 0)
     assert calls == [True] and torch.equal(uk, rk) and torch.equal(uv, rv)
-    # ids 10x apart: the table would be 10x the rows -> no plan (the sort path)
-    assert sparse._dense_plan(sparse.KeyRange(0, int(keys.max()) * 10, None), 4, keys) is None
+    # a range 100x wider: the table would be > DENSE_FACTOR x the rows -> no plan (the sort path)
+    assert sparse._dense_plan(sparse.KeyRange(0, int(keys.max()) * 100, None), 4, keys) is None
+    assert sparse._dense_plan(sparse.KeyRange(-5, int(keys.max()), None), 4, keys) is None
