@@ -153,8 +153,10 @@ def _sync_new_keys(engine, new: List) -> None:
 
 
 # ------------------------------------------------------------------ local kernels (GPU) / CPU twins
-# Reduce-by-key of the device map collectives (K5): "sort" (default: rocPRIM radix sort + run
-# starts + the segmented reduce — deterministic, keys ascending per owner) or "hash" (K5h,
+# Reduce-by-key of the device map collectives (K5): "sort" (default: deterministic, keys ascending
+# per owner — K5d's direct addressing when the carried key range is dense enough (_dense_plan),
+# else rocPRIM radix sort + run starts + the segmented reduce; both give the same result and
+# order) or "hash" (K5h,
 # csrc/kernels/sparse_hash.hip: open addressing, a row list per key, rows combined in input order —
 # the same values bit for bit, 1.4-1.6x faster on config 4's owner rows; keys in table order,
 # which depends on the CAS races of colliding keys).  A/B: profiles/r6/sparse/v3_*.
