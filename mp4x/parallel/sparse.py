@@ -435,6 +435,11 @@ DENSE_FACTOR = float(os.environ.get("MP4X_SPARSE_DENSE_FACTOR", 32.0))
 DENSE_MAX_SLOTS = 1 << 26
 
 
+def _bits_range(key_bits: Optional[int]) -> Optional["KeyRange"]:
+    """The key range a caller's ``key_bits`` promises ([0, 2**key_bits)), or None."""
+    return KeyRange(0, (1 << int(key_bits)) - 1, int(key_bits)) if key_bits else None
+
+
 def _dense_plan(rng: Optional["KeyRange"], p: int, rkeys: torch.Tensor):
     """K5d's (base, stride, T) for an owner's received keys — every key k has k % p == this
     owner, so k // p - lo // p indexes a table of T slots — when that table is at most
@@ -552,7 +557,7 @@ def allreduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, k
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
     rkeys, rvals, rng = _exchange_by_owner(engine, keys, v2)
     uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or (rng.bits if rng else None),
-                               _dense_plan(rng, engine.p, rkeys))
+                               _dense_plan(rng or _bits_range(key_bits), engine.p, rkeys))
     sizes = _row_counts(engine, uk.shape[0], uk.device)     # one count round for keys AND rows
     got = _ipc_allgatherv(engine, uk, uv, sizes) if _sparse_ipc_ok(engine, uk) else None
     if got is not None:
@@ -640,7 +645,7 @@ def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(vals.dtype))
     rkeys, rvals, rng = _exchange_by_owner(engine, keys, v2)
     uk, uv, _ = _reduce_by_key(rkeys, rvals, op, key_bits or (rng.bits if rng else None),
-                               _dense_plan(rng, engine.p, rkeys))
+                               _dense_plan(rng or _bits_range(key_bits), engine.p, rkeys))
     gk, gv = gather_sparse(engine, uk, uv, root, key_bits)    # disjoint owners: K8 dedupe is a no-op
     return gk, (gv.view(-1) if squeeze else gv)
 
@@ -1048,7 +1053,13 @@ def reduce_scatter_map_device(engine, mapDataList: List[Dict], operator) -> Dict
     rv = torch.empty((sum(rc), vals.shape[1]), dtype=vals.dtype, device=vals.device)
     engine.coll.all_to_all_single(rv, vals, rc, counts)
     op = operator if getattr(operator, "is_custom", False) else for_dtype(operator, dtype_of_torch(rv.dtype))
-    uk, uv, _ = _reduce_by_key(rk, rv, op, _dictionary(engine).bits)
+    d = _dictionary(engine)
+    # dense dictionary ids in [0, len): K5d by direct addressing (stride 1) when the table is small
+    # enough for the rows received, else the sort over the ids' bits
+    T = len(d.id2key)
+    dense = (0, 1, T) if rk.is_cuda and rk.shape[0] and 0 < T <= min(DENSE_FACTOR * rk.shape[0], DENSE_MAX_SLOTS) \
+        else None
+    uk, uv, _ = _reduce_by_key(rk, rv, op, d.bits, dense)
     return _tensors_map(engine, uk, uv, shape)
 
 
