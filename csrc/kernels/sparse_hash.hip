@@ -339,6 +339,20 @@ __global__ __launch_bounds__(kBlock) void k_dense_compact(const unsigned long lo
     m_flag[0] = (unsigned long long)(tile_base[ntiles - 1] + tile_cnt[ntiles - 1]);
 }
 
+// Keys only (set operations): every run's row count, one lane per run walking its list.
+__global__ __launch_bounds__(kBlock) void k_run_counts(const int32_t* __restrict__ rhead,
+                                                       const int32_t* __restrict__ next,
+                                                       const unsigned long long* __restrict__ m_dev,
+                                                       int32_t* __restrict__ out_count) {
+  const int64_t m = (int64_t)*m_dev;
+  const int64_t nthr = (int64_t)gridDim.x * kBlock;
+  for (int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x; u < m; u += nthr) {
+    int32_t L = 0;
+    for (int32_t i = rhead[u]; i >= 0; i = next[i]) ++L;
+    out_count[u] = L;
+  }
+}
+
 int64_t table_slots(int64_t n) {
   int64_t t = 1024;
   while (t < 2 * n) t <<= 1;
@@ -498,15 +512,15 @@ extern "C" size_t mp4x_dense_rbk_scratch_bytes(int64_t n, int64_t T) {
 }
 
 // K5d: keys[n] with k / stride - base in [0, T) (e.g. an owner's share of dense ids, stride = p),
-// vals[n][dim] -> out_keys[m] ascending, out_vals[m][dim] (rows combined in input order: the sort
-// path's result bit for bit), out_count[m] (optional); m_flag[0] = m, m_flag[1] != 0 when the keys
+// vals[n][dim] (or NULL: keys only) -> out_keys[m] ascending, out_vals[m][dim] (rows combined in
+// input order: the sort path's result bit for bit), out_count[m] (optional); m_flag[0] = m, m_flag[1] != 0 when the keys
 // were not dense after all (then nothing else is meaningful: use the sort path).
 extern "C" int mp4x_dense_reduce_by_key(int dtype, int op, const int64_t* keys, int64_t n, const void* vals,
                                         int64_t dim, int64_t base, int64_t stride, int64_t T, void* scratch,
                                         size_t scratch_bytes, int64_t* out_keys, void* out_vals, int32_t* out_count,
                                         int64_t* m_flag, void* stream) {
-  if (!mp4x_hash_rbk_supported(dtype, op) || n <= 0 || dim <= 0 || n >= (1ll << 30) || T < 1 || T >= (1ll << 31) ||
-      stride < 1 || base < 0)
+  if ((vals && (!mp4x_hash_rbk_supported(dtype, op) || dim <= 0)) || n <= 0 || n >= (1ll << 30) || T < 1 ||
+      T >= (1ll << 31) || stride < 1 || base < 0)
     return MP4X_E_UNSUPPORTED;
   const DenseLayout L = dense_layout(n, T);
   if (scratch_bytes < L.total || ((uintptr_t)scratch & 255) || ((uintptr_t)m_flag & 7)) return MP4X_E_BADARG;
@@ -532,6 +546,12 @@ extern "C" int mp4x_dense_reduce_by_key(int dtype, int op, const int64_t* keys, 
                      flag);
   if (int e = (int)hipGetLastError()) return e;
   const unsigned long long* m_dev = flag;
+  if (!vals) {                                           // keys only: unique keys + counts
+    if (!out_count) return 0;
+    hipLaunchKernelGGL(k_run_counts, dim3(grid_for(n, 1)), dim3(kBlock), 0, st, (const int32_t*)rhead,
+                       (const int32_t*)next, m_dev, out_count);
+    return (int)hipGetLastError();
+  }
   switch (dtype) {
     case MP4X_F64: return reduce_dt<MP4X_F64>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);
     case MP4X_F32: return reduce_dt<MP4X_F32>(op, rhead, next, m_dev, n, vals, dim, out_vals, out_count, st);

@@ -470,7 +470,7 @@ def hash_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, stream=N
     return out_keys[:m], out_vals[:m], out_count[:m]
 
 
-def dense_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, base: int, stride: int, T: int,
+def dense_reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op: int, base: int, stride: int, T: int,
                         stream=None):
     """K5d (csrc/kernels/sparse_hash.hip): reduce-by-key of DENSE keys — ``k // stride - base`` in
     [0, T) — by direct addressing: (unique_keys ascending, reduced_rows, counts), the same as
@@ -479,12 +479,12 @@ def dense_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, base: i
     :func:`reduce_by_key`."""
     _dev_check(keys, vals)
     n = keys.numel()
-    if keys.dtype != torch.int64 or vals.dim() not in (1, 2) or vals.shape[0] != n:
-        raise ValueError("dense_reduce_by_key: int64 keys[n] and vals[n] / vals[n, dim]")
-    if n == 0 or T < 1 or stride < 1 or base < 0 or not hash_rbk_supported(vals.dtype, op):
+    if keys.dtype != torch.int64 or (vals is not None and (vals.dim() not in (1, 2) or vals.shape[0] != n)):
+        raise ValueError("dense_reduce_by_key: int64 keys[n] and vals[n] / vals[n, dim] (or None)")
+    if n == 0 or T < 1 or stride < 1 or base < 0 or (vals is not None and not hash_rbk_supported(vals.dtype, op)):
         return None
     dev = keys.device
-    dim = 1 if vals.dim() == 1 else int(vals.shape[1])
+    dim = 0 if vals is None else (1 if vals.dim() == 1 else int(vals.shape[1]))
     lib = native.hip()
     sb = lib.mp4x_dense_rbk_scratch_bytes(n, T)
     scratch = torch.empty(sb + 256, dtype=torch.uint8, device=dev)
@@ -492,16 +492,17 @@ def dense_reduce_by_key(keys: torch.Tensor, vals: torch.Tensor, op: int, base: i
     sp += (-sp) % 256
     m_flag = torch.empty(2, dtype=torch.int64, device=dev)
     out_keys = torch.empty(n, dtype=torch.int64, device=dev)
-    out_vals = torch.empty_like(vals)
+    out_vals = torch.empty_like(vals) if vals is not None else None
     out_count = torch.empty(n, dtype=torch.int32, device=dev)
-    check(lib.mp4x_dense_reduce_by_key(int(dtype_of_torch(vals.dtype)), int(op), keys.data_ptr(), n, vals.data_ptr(),
-                                       dim, int(base), int(stride), int(T), sp, sb, out_keys.data_ptr(),
-                                       out_vals.data_ptr(), out_count.data_ptr(), m_flag.data_ptr(),
-                                       stream_ptr(stream)), "mp4x_dense_reduce_by_key")
+    check(lib.mp4x_dense_reduce_by_key(int(dtype_of_torch(vals.dtype)) if vals is not None else 0, int(op),
+                                       keys.data_ptr(), n, vals.data_ptr() if vals is not None else None, dim,
+                                       int(base), int(stride), int(T), sp, sb, out_keys.data_ptr(),
+                                       out_vals.data_ptr() if vals is not None else None, out_count.data_ptr(),
+                                       m_flag.data_ptr(), stream_ptr(stream)), "mp4x_dense_reduce_by_key")
     m, bad = m_flag.tolist()                                # one sync for both
     if bad:
         return None
-    return out_keys[:m], out_vals[:m], out_count[:m]
+    return out_keys[:m], (out_vals[:m] if out_vals is not None else None), out_count[:m]
 
 
 def reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op: int, key_bits: Optional[int] = None,

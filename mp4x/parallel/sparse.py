@@ -168,10 +168,10 @@ def _reduce_by_key(keys: torch.Tensor, vals: Optional[torch.Tensor], op, key_bit
     instead (no sort; the same result, order included) unless the keys turn out not dense."""
     if keys.is_cuda:
         from ..ops.device_ops import reduce_by_key
-        if dense is not None and vals is not None and RBK_MODE != "hash" and not getattr(op, "is_custom", False):
+        if dense is not None and RBK_MODE != "hash" and (vals is None or not getattr(op, "is_custom", False)):
             from ..ops.device_ops import dense_reduce_by_key, hash_rbk_supported
-            if hash_rbk_supported(vals.dtype, int(op.code)):
-                got = dense_reduce_by_key(keys, vals, int(op.code), *dense)
+            if vals is None or hash_rbk_supported(vals.dtype, int(op.code)):
+                got = dense_reduce_by_key(keys, vals, int(op.code) if vals is not None else 0, *dense)
                 if got is not None:
                     return got
         if vals is not None and RBK_MODE == "hash" and not getattr(op, "is_custom", False):
@@ -653,7 +653,7 @@ def reduce_sparse(engine, keys: torch.Tensor, vals: torch.Tensor, operator, root
 def _set_counts(engine, ids: torch.Tensor):
     ids = torch.unique(ids) if not ids.is_cuda else _reduce_by_key(ids, None, None)[0]
     rkeys, _, rng = _exchange_by_owner(engine, ids, None)
-    return _reduce_by_key(rkeys, None, None, rng.bits if rng else None)
+    return _reduce_by_key(rkeys, None, None, rng.bits if rng else None, _dense_plan(rng, engine.p, rkeys))
 
 
 def set_union(engine, ids: torch.Tensor) -> torch.Tensor:

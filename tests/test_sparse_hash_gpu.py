@@ -158,3 +158,14 @@ def test_sparse_allreduce_of_dense_ids_takes_k5d(monkeypatch):
     # a range 100x wider: the table would be > DENSE_FACTOR x the rows -> no plan (the sort path)
     assert sparse._dense_plan(sparse.KeyRange(0, int(keys.max()) * 100, None), 4, keys) is None
     assert sparse._dense_plan(sparse.KeyRange(-5, int(keys.max()), None), 4, keys) is None
+
+
+def test_dense_keys_only_is_the_sort_paths_unique_and_counts():
+    """K5d without rows (the set operations): unique keys ascending + run lengths, as the sort."""
+    from mp4x.ops.device_ops import dense_reduce_by_key, reduce_by_key
+    g = torch.Generator().manual_seed(11)
+    keys = (torch.randint(0, 50_000, (120_000,), generator=g) * 4 + 1).cuda()     # owner 1 of p = 4
+    got = dense_reduce_by_key(keys, None, 0, int(keys.min()) // 4, 4, int(keys.max()) // 4 - int(keys.min()) // 4 + 1)
+    ref = reduce_by_key(keys, None, 0)
+    assert got is not None and got[1] is None
+    assert torch.equal(got[0], ref[0]) and torch.equal(got[2], ref[2])

@@ -118,3 +118,27 @@ def test_sparse_exchange_too_large_for_staging_takes_the_transport():
         got = dict(zip(rk.tolist(), rv))
         assert all(torch.equal(got[kk], ref[kk]) for kk in ref), r
         assert "sparse.a2a.ipc" not in used and "sparse.allgatherv.ipc" not in used, used
+
+
+def _setops_fn(comm, n):
+    g = torch.Generator().manual_seed(50 + comm.getRank())
+    ids = torch.randint(0, 3 * n, (n,), generator=g).cuda()          # dense ids, duplicates
+    u = comm.allreduceSetUnion(ids)
+    i = comm.allreduceSetIntersection(ids)
+    torch.cuda.synchronize()
+    return u.cpu().numpy(), i.cpu().numpy()
+
+
+def test_set_ops_over_ipc_with_dense_ids():
+    """Set union / intersection of dense ids across real processes: the owners' de-duplication
+    runs K5d keys-only (unique keys ascending + counts); against Python sets."""
+    p, n = 3, 30000
+    out = run_spawn(p, _setops_fn, args=(n,))
+    sets = []
+    for r in range(p):
+        g = torch.Generator().manual_seed(50 + r)
+        sets.append(set(torch.randint(0, 3 * n, (n,), generator=g).tolist()))
+    union, inter = set.union(*sets), set.intersection(*sets)
+    for r, (u, i) in out.items():
+        assert sorted(u.tolist()) == sorted(union) and len(u) == len(union), r
+        assert sorted(i.tolist()) == sorted(inter) and len(i) == len(inter), r
