@@ -21,6 +21,15 @@
 //            the rows in that order (= input = rank order): the same values, bit for bit, as the
 //            sort path, which also combines in input order
 //
+// Differences from the sort path (why K5h stays opt-in): the output keys come in table order,
+// which depends on which of two colliding keys' CAS wins, not ascending; a run longer than 64
+// rows combines in list order (float SUM / PROD of such a key is then not bit-reproducible;
+// integer data and MAX / MIN are exact either way); the FIRST rule (K8) is not served.  Rows
+// whose key equals -1 (the EMPTY marker) form a side run of their own.
+//
+// K5d (below) is the identity-hash form for DENSE keys (k / stride - base in [0, T)): no
+// probing, an ordered compaction, so the keys come out ascending — the sort path's result and
+// order — and the tensor forms take it by default where the carried key range allows.
 #include <rocprim/device/device_scan.hpp>
 #include <type_traits>
 
