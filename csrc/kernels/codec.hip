@@ -23,7 +23,7 @@ namespace mp4x {
 // 16-byte loads in flight before the first amax reduction.
 constexpr int QU = 4;
 
-template <int DT>
+template <int DT, int QU>
 __global__ __launch_bounds__(kBlock) void k_quant(const void* __restrict__ in, int64_t n, uint32_t* __restrict__ q,
                                                   float* __restrict__ scales) {
   const int lane = threadIdx.x & 63;
@@ -43,7 +43,8 @@ __global__ __launch_bounds__(kBlock) void k_quant(const void* __restrict__ in, i
 
 template <int NIN> struct QIn { const uint32_t* q[NIN]; const float* s[NIN]; };
 
-template <int DT, int NIN>
+// DU consecutive quant blocks per wave iteration: DU * NIN independent loads in flight.
+template <int DT, int NIN, int DU = 1>
 __global__ __launch_bounds__(kBlock) void k_dequant_reduce(void* __restrict__ out, QIn<NIN> in, int64_t n,
                                                            int accumulate, uint32_t* __restrict__ q_out,
                                                            float* __restrict__ s_out) {
@@ -51,29 +52,51 @@ __global__ __launch_bounds__(kBlock) void k_dequant_reduce(void* __restrict__ ou
   const int64_t nblk = (n + kQBlock - 1) / kQBlock;
   const int64_t wave = wave_id();
   const int64_t nwaves = ((int64_t)gridDim.x * kBlock) >> 6;
-  for (int64_t b = wave; b < nblk; b += nwaves) {
-    const int64_t e = b * kQBlock + lane * 4;
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (accumulate && out) load4<DT>(out, e, n, acc);
-    uint32_t w[NIN];
-    float s[NIN];
+  for (int64_t b0 = wave * DU; b0 < nblk; b0 += nwaves * DU) {
+    uint32_t w[DU][NIN];
+    float s[DU][NIN];
 #pragma unroll
-    for (int k = 0; k < NIN; ++k) {   // issue every load first: NIN independent requests in flight
-      w[k] = __builtin_nontemporal_load(in.q[k] + b * 64 + lane);
-      s[k] = in.s[k][b];
+    for (int d = 0; d < DU; ++d)
+#pragma unroll
+      for (int k = 0; k < NIN; ++k) {   // issue every load first: DU * NIN requests in flight
+        const int64_t b = b0 + d < nblk ? b0 + d : nblk - 1;
+        w[d][k] = __builtin_nontemporal_load(in.q[k] + b * 64 + lane);
+        s[d][k] = in.s[k][b];
+      }
+#pragma unroll
+    for (int d = 0; d < DU; ++d) {
+      const int64_t b = b0 + d;
+      if (b >= nblk) break;
+      const int64_t e = b * kQBlock + lane * 4;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      if (accumulate && out) load4<DT>(out, e, n, acc);
+#pragma unroll
+      for (int k = 0; k < NIN; ++k) fp8_fma_acc(w[d][k], s[d][k], acc);
+      if (out) store4<DT>(out, e, n, acc);
+      if (q_out) quant_block(acc, q_out, s_out, b, lane);
     }
-#pragma unroll
-    for (int k = 0; k < NIN; ++k) fp8_fma_acc(w[k], s[k], acc);
-    if (out) store4<DT>(out, e, n, acc);
-    if (q_out) quant_block(acc, q_out, s_out, b, lane);
   }
+}
+
+// Streaming codec kernels launch their whole grid (one wave iteration each, up to 2^20 blocks)
+// instead of grid_for's kMaxGrid cap with a grid-stride loop: measured 5.55 -> 6.14 TB/s for the
+// quantise of 1 GiB f32 (profiles/r6/codec/grid_ab.jsonl).
+static int g_codec_grid = 1;      // 0 = grid_for's capped grid-stride form (A/B)
+static int g_dq_unroll = 0;       // A/B: quant blocks per wave iteration of the dequant-reduce (0 = by NIN)
+
+static int codec_grid(int64_t threads, int per_wave_iter_blocks) {
+  if (!g_codec_grid) return grid_for(threads, 1);
+  int64_t g = (threads + kBlock - 1) / kBlock / per_wave_iter_blocks;
+  if (g < 1) g = 1;
+  if (g > (1 << 20)) g = 1 << 20;
+  return (int)g;
 }
 
 template <int DT>
 static int launch_quant(const void* in, int64_t n, uint32_t* q, float* s, hipStream_t st) {
   int64_t nblk = (n + kQBlock - 1) / kQBlock;
-  int g = grid_for(nblk * 64, 1);
-  hipLaunchKernelGGL(k_quant<DT>, dim3(g), dim3(kBlock), 0, st, in, n, q, s);
+  const int g = codec_grid(nblk * 64, QU);        // a wave takes QU quant blocks per iteration
+  hipLaunchKernelGGL((k_quant<DT, QU>), dim3(g), dim3(kBlock), 0, st, in, n, q, s);
   return (int)hipGetLastError();
 }
 
@@ -86,9 +109,20 @@ static int launch_dr(void* out, const uint8_t* const* qs, const float* const* ss
     in.s[k] = ss[k];
   }
   int64_t nblk = (n + kQBlock - 1) / kQBlock;
-  int g = grid_for(nblk * 64, 1);
-  hipLaunchKernelGGL((k_dequant_reduce<DT, NIN>), dim3(g), dim3(kBlock), 0, st, out, in, n, acc,
-                     reinterpret_cast<uint32_t*>(qo), so);
+  const int g = grid_for(nblk * 64, 1);
+  // quant blocks per wave iteration: more loads in flight for the multi-input reduce (NIN = 8:
+  // 0.91 -> 0.61 ms for 8 x 256 Mi elements, 3.5 -> 5.3 TB/s), one for the single-input dequant
+  // (more costs it 15 %; profiles/r6/codec/grid_ab.jsonl)
+  const int du = g_dq_unroll ? g_dq_unroll : (NIN >= 4 ? 4 : (NIN >= 2 ? 2 : 1));
+  if (du == 2)
+    hipLaunchKernelGGL((k_dequant_reduce<DT, NIN, 2>), dim3(g), dim3(kBlock), 0, st, out, in, n, acc,
+                       reinterpret_cast<uint32_t*>(qo), so);
+  else if (du == 4)
+    hipLaunchKernelGGL((k_dequant_reduce<DT, NIN, 4>), dim3(g), dim3(kBlock), 0, st, out, in, n, acc,
+                       reinterpret_cast<uint32_t*>(qo), so);
+  else
+    hipLaunchKernelGGL((k_dequant_reduce<DT, NIN, 1>), dim3(g), dim3(kBlock), 0, st, out, in, n, acc,
+                       reinterpret_cast<uint32_t*>(qo), so);
   return (int)hipGetLastError();
 }
 
@@ -569,6 +603,9 @@ static int zs_decode_t(const uint64_t* masks, const int32_t* counts, const void*
 }  // namespace mp4x
 
 using namespace mp4x;
+
+extern "C" void mp4x_set_codec_grid(int full) { g_codec_grid = full; }
+extern "C" void mp4x_set_dq_unroll(int du) { g_dq_unroll = du; }
 
 extern "C" int mp4x_quant_fp8(int dtype_in, const void* in, int64_t n, uint8_t* q, float* scales, void* stream) {
   if (n <= 0) return 0;

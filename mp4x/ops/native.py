@@ -78,6 +78,8 @@ _HIP_SIGS = {
     "mp4x_dense_reduce_by_key": (c_int, [c_int, c_int, c_void_p, c_int64, c_void_p, c_int64, c_int64, c_int64, c_int64,
                                          c_void_p, c_size_t, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "mp4x_set_k1_variant": (None, [c_int]),
+    "mp4x_set_dq_unroll": (None, [c_int]),
+    "mp4x_set_codec_grid": (None, [c_int]),
     "mp4x_set_k1_grid": (None, [c_int64]),
     "mp4x_version": (ctypes.c_char_p, []),
     "mp4x_clear_error": (c_int, []),
