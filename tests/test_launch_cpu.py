@@ -23,8 +23,11 @@ def _run(tmp_path, nproc=4, extra_env=None, steps=3):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--cpu", "--gpus", str(nproc), "--steps", str(steps), "--warmup", "1", "--bytes", "4000000"]
-    r = subprocess.run(cmd, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300,
+    # stderr apart from stdout, as the driver reads it: the ranks' warnings (a failed verification
+    # is reported on stderr by every rank) must not interleave with rank 0's JSON lines
+    r = subprocess.run(cmd, cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=300,
                        env=dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {})))
+    r.stdout = r.stdout + r.stderr[-3000:]
     lines = [json.loads(x) for x in r.stdout.splitlines() if x.startswith('{"metric"')]
     return r, lines
 
