@@ -330,7 +330,25 @@ __global__ __launch_bounds__(kBlock) void k_scale(void* out_, const void* in_, d
   const S* in = reinterpret_cast<const S*>(in_);
   S* out = reinterpret_cast<S*>(out_);
   const A s = (A)scale;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += nthr) out[i] = E::store(E::load(in[i]) * s);
+  const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int64_t done = 0;
+  if (((((uintptr_t)in | (uintptr_t)out) & 15) == 0)) {   // 16-byte vectors (the bf16 / f16 rows too)
+    constexpr int W = 16 / (int)sizeof(S);
+    const int64_t nv = n / W;
+    const u32x4* vin = reinterpret_cast<const u32x4*>(in);
+    u32x4* vout = reinterpret_cast<u32x4*>(out);
+    for (int64_t v = t0; v < nv; v += nthr) {
+      u32x4 t = __builtin_nontemporal_load(vin + v);
+      S x[W];
+      __builtin_memcpy(x, &t, 16);
+#pragma unroll
+      for (int j = 0; j < W; ++j) x[j] = E::store(E::load(x[j]) * s);
+      __builtin_memcpy(&t, x, 16);
+      __builtin_nontemporal_store(t, vout + v);
+    }
+    done = nv * W;
+  }
+  for (int64_t i = done + t0; i < n; i += nthr) out[i] = E::store(E::load(in[i]) * s);
 }
 
 }  // namespace mp4x

@@ -124,12 +124,19 @@ def test_reduce_unaligned_views():
     torch.testing.assert_close(out, xs[0] + xs[1] + xs[2])
 
 
-def test_scale():
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("off", [0, 1])
+def test_scale(dtype, off):
+    """K1 scale: the 16-byte vector form (aligned, with a scalar tail) and the scalar form
+    (misaligned view) against torch, in place too."""
     K = _native()
-    x = torch.randn(12345, device=DEV)
-    y = torch.empty_like(x)
+    x = torch.randn(12345 + off, device=DEV).to(dtype)[off:]
+    y = torch.empty(12345 + off, device=DEV, dtype=dtype)[off:]
     K.scale_(y, x, 0.125)
-    torch.testing.assert_close(y, x * 0.125)
+    torch.testing.assert_close(y, (x.double() * 0.125).to(dtype), rtol=0, atol=0)
+    z = x.clone()
+    K.scale_(z, z, 0.125)
+    assert torch.equal(z, y)
 
 
 def test_segment_copy_and_gather_rows():
